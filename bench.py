@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident batched CRC32C on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
+
+One "step" = one batch CRC32C launch over this rank's whole synthetic batch,
+inputs already resident in HBM.  Default workload (N=1 headline, BASELINE.json
+configs[2]): 262,144 SSTable-sized 4 KiB blocks = 1 GiB per GPU, offsets
+i*4096, seed 0, splitmix64 payload generated on the device.  With N>1
+(torchrun) every rank checksums its own shard of the same shape (weak
+scaling, no data-path collective; the only collectives are the timing
+barrier and the max-over-ranks of the elapsed time).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+`roofline` (kernel launch duration by HIP events on the launch stream vs the
+8 TB/s HBM3E peak) and `cpu_baseline` (the CPU oracle — a restatement of the
+reference's SSE4.2 `extend_hw`, crc32c.rs:86-118 — timed single-threaded on
+this host over a bounded sample of the same blocks).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "leveldb-rs_amd"))
+
+METRIC = "GiB/s device-resident batched CRC32C, 4KiB blocks; %HBM-peak at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md), GB/s
+PAYLOAD_SEED = 0x4C444231
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"])
+    p.add_argument("--api", default="offsets", choices=["offsets", "strided"])
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--pmc-csv", default=None, help="rocprofv3 --pmc counter CSV for roofline.traffic")
+    return p.parse_args()
+
+
+def build_workload(torch, lvgpu, name, dev, rank):
+    """Returns (arena, off, len, nbytes, description) on `dev`."""
+    import numpy as np
+    seed = PAYLOAD_SEED ^ (rank * 0x9E3779B9)
+    if name in ("c3", "c5"):
+        n = 262144 if name == "c3" else 2097152  # c5: 64 GiB over 8 GPUs = 8 GiB per GPU
+        bl = 4096
+        arena = torch.empty(n * bl, dtype=torch.uint8, device=dev)
+        lvgpu.fill_splitmix(arena, 0, seed)
+        off = torch.arange(n, dtype=torch.int64, device=dev) * bl
+        ln = torch.full((n,), bl, dtype=torch.int32, device=dev)
+        desc = f"{name}: {n} x {bl} B SSTable blocks per GPU ({n * bl / 2**30:.0f} GiB), offsets i*{bl}, seed 0"
+        return arena, off, ln, n * bl, desc
+    rng = np.random.default_rng(0xC0FFEE + rank)
+    if name == "c4":  # Zipf(1.1) multiples of 32 B on 1..2048, shuffled
+        k = np.minimum(rng.zipf(1.1, size=1048576), 2048)
+        lens = (32 * k).astype(np.uint32)
+        desc = "c4: 1,048,576 buffers, L = 32*k, k ~ Zipf(1.1) on 1..2048, byte-packed"
+    else:  # c2: WAL physical records from Random(301).skewed(17) record sizes
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        lens = wal_unit_lengths(1048576)
+        desc = "c2: 1,048,576 WAL CRC units [type||fragment], sizes from Random(301).skewed(17) fragmented per add_record"
+    offs = np.zeros(lens.size, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(offs[-1] + lens[-1])
+    arena = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, seed)
+    off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    return arena, off, ln, total, desc
+
+
+def wal_unit_lengths(n):
+    """CRC unit lengths (1 + fragment) of the WAL the reference writer produces for
+    records of size Random(301).skewed(17) (log_writer.rs:62-110, random.rs:66-69)."""
+    import numpy as np
+    B, H = 32768, 7
+    out = np.empty(n, dtype=np.uint32)
+    m = 0
+    state = 301 & 0x7FFFFFFF
+    block_off = 0
+
+    def nxt():
+        nonlocal state
+        prod = state * 16807
+        s = ((prod >> 31) + (prod & 2147483647)) & 0xFFFFFFFF
+        if s > 2147483647:
+            s -= 2147483647
+        state = s
+        return s
+    while m < n:
+        r = 1 << (nxt() % 18)
+        left = nxt() % r
+        while m < n:
+            if B - block_off < H:
+                block_off = 0
+            avail = B - block_off - H
+            frag = min(left, avail)
+            out[m] = frag + 1
+            m += 1
+            block_off += H + frag
+            left -= frag
+            if left <= 0:
+                break
+    return out
+
+
+def read_pmc_traffic(path):
+    """HBM bytes per launch of the CRC kernel from a rocprofv3 --pmc CSV
+    (FETCH_SIZE in KiB, doubled for gfx950's half-count on wide streaming
+    reads: MI355X_MICROARCH.md §HBM)."""
+    import csv
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if "crc32c_batch_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == "FETCH_SIZE":
+                vals.append(float(row["Counter_Value"]))
+    if not vals:
+        return None
+    return 2.0 * 1024.0 * sorted(vals)[len(vals) // 2]
+
+
+def cpu_baseline(torch, arena, nbytes_block, seconds):
+    """Single-thread oracle extend_hw (restating crc32c.rs:86-118) over a bounded
+    sample of the same blocks; also checks the GPU results for the sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import wal_oracle as W
+    L = W.lib()
+    nsample = 16384  # 64 MiB of the batch's first blocks
+    host = arena[: nsample * nbytes_block].cpu().numpy()
+    base = host.ctypes.data
+    passes = 0
+    t0 = time.perf_counter()
+    crcs = None
+    while True:
+        res = [L.oracle_extend_hw(0, ctypes.cast(base + i * nbytes_block, ctypes.c_char_p), nbytes_block)
+               for i in range(nsample)]
+        if crcs is None:
+            crcs = np.array(res, dtype=np.uint32)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    gib = passes * nsample * nbytes_block / 2**30
+    return {"value": round(gib / el, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"first {nsample} of the 4 KiB blocks ({nsample * nbytes_block >> 20} MiB), "
+                      f"{passes} passes in {el:.1f} s, oracle extend_hw (SSE4.2 crc32, 1 thread)"}, crcs
+
+
+def main():
+    args = parse()
+    import torch
+    import lvgpu
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    lvgpu.device_init()
+
+    arena, off, ln, nbytes, desc = build_workload(torch, lvgpu, args.workload, dev, rank)
+    n = off.numel()
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+
+    if args.api == "strided" and args.workload in ("c3", "c5"):
+        def step():
+            lvgpu.batch_strided(arena, 4096, 4096, n, out=out, stream=stream)
+    else:
+        def step():
+            lvgpu.batch(arena, off, ln, out=out, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-launch HIP events on the launch stream (roofline.achieved)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s, e in evs:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kern_ms = sorted(s.elapsed_time(e) for s, e in evs)
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+
+    total_bytes = nbytes * world
+    value = total_bytes * args.steps / 2**30 / el
+    achieved_gbs = nbytes / (kern_avg_ms * 1e-3) / 1e9
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0 and args.workload in ("c3", "c5"):
+            cpu, crcs = cpu_baseline(torch, arena, 4096, args.cpu_seconds)
+            got = out[: crcs.size].cpu().numpy().view("uint32")
+            if not (got == crcs).all():
+                raise SystemExit("bench parity check failed: GPU CRCs differ from the oracle on the sample")
+        traffic = read_pmc_traffic(args.pmc_csv) if args.pmc_csv else None
+        result = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 payload generated in HBM)",
+            "config": {"workload": desc, "buffers_per_gpu": n, "bytes_per_gpu": nbytes,
+                       "api": "lv_crc32c_batch_strided" if args.api == "strided" else "lv_crc32c_batch_device",
+                       "parallelism": f"dp{world} (independent shards, no collective)"},
+            "hbm_peak_frac": round(value * 2**30 / world / 1e9 / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "kernel": "lvk::crc32c_batch_kernel", "kernel_ms_avg": round(kern_avg_ms, 4),
+                         "kernel_ms_min": round(kern_ms[0], 4), "bytes_per_launch": nbytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,104 @@
+/*
+ * lvgpu — MI355X-native batched CRC32C for leveldb-rs's WAL and table-block
+ * checksum path.  C ABI (no HIP, torch or C++ types in any signature).
+ *
+ * The reference exposes Rust free functions in `leveldb::util::crc32c`
+ * (src/util/mod.rs:23); each scalar entry point below is the C twin of one of
+ * them, bit-identical on every input, so a Rust `extern "C"` shim maps
+ * `&[u8]` to (ptr, len) one-to-one.  The batch entry points
+ * are new: they checksum many independent buffers per call on the GPU.
+ *
+ * Conventions
+ *   - Scalar functions: pure, reentrant, infallible, never allocate
+ *     (crc32c.rs:40-118).  They run on the host CPU: a single WAL record is
+ *     far below a kernel launch's cost.
+ *   - Batch functions: device buffers are caller-owned and never freed by the
+ *     library; calls are stream-ordered and asynchronous on `stream` (a
+ *     hipStream_t passed as void*, NULL = default stream); the return is 0 or
+ *     a nonzero lv_status / hipError_t code, with lv_last_error() describing
+ *     it.  No host fallback exists: without a usable GPU the batch calls fail.
+ */
+#ifndef LVGPU_CRC32C_H
+#define LVGPU_CRC32C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- scalar drop-ins (host) -------------------------------------------- */
+
+/* crc32c.rs:40      pub fn value(data: &[u8]) -> u32 */
+uint32_t lv_crc32c_value(const uint8_t *data, size_t n);
+/* crc32c.rs:42-51   pub fn extend(crc: u32, data: &[u8]) -> u32 */
+uint32_t lv_crc32c_extend(uint32_t crc, const uint8_t *data, size_t n);
+/* crc32c.rs:53-57   pub fn mask(crc: u32) -> u32 */
+uint32_t lv_crc32c_mask(uint32_t crc);
+/* crc32c.rs:59-63   pub fn unmask(masked_crc: u32) -> u32 */
+uint32_t lv_crc32c_unmask(uint32_t masked_crc);
+/* crc32c.rs:65-84   pub fn extend_sw(crc: u32, data: &[u8]) -> u32 */
+uint32_t lv_crc32c_extend_sw(uint32_t crc, const uint8_t *data, size_t n);
+/* crc32c.rs:86-118  pub unsafe fn extend_hw(crc: u32, data: &[u8]) -> u32
+ * (requires SSE4.2 on the host, as the reference's #[target_feature] does) */
+uint32_t lv_crc32c_extend_hw(uint32_t crc, const uint8_t *data, size_t n);
+
+/* ---- batch API (device) ------------------------------------------------- */
+
+/* flags */
+#define LV_CRC_MASK 0x1u /* store mask(crc) (crc32c.rs:54) instead of crc      */
+/* Tuning/test hook: force the lanes-per-buffer group size G of the kernel
+ * (g in {1,4,16,64}) instead of the library's choice by length. */
+#define LV_CRC_GROUP(g) ((g) == 1 ? 0x100u : (g) == 4 ? 0x200u : (g) == 16 ? 0x300u : (g) == 64 ? 0x400u : 0u)
+#define LV_CRC_GROUP_MASK 0x700u
+
+/* status codes (besides hipError_t values passed through) */
+#define LV_OK 0
+#define LV_ERR_INVALID (-1) /* bad argument                                   */
+#define LV_ERR_NO_DEVICE (-2) /* no usable GPU / HIP runtime error at init     */
+
+/* out[i] = [mask](extend(seed ? seed[i] : 0, arena[off[i] .. off[i]+len[i])))
+ * for i < n.  All pointers are device pointers; `d_seed` may be NULL (all
+ * seeds 0, i.e. value()).  Buffers may start at any byte offset and overlap.
+ * This is the batched form of the per-record calls at log_writer.rs:123-124
+ * (seed = type_crc[t], LV_CRC_MASK) and log_reader.rs:335-336 (seed 0). */
+int lv_crc32c_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                           const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
+                           void *stream);
+
+/* Fixed-stride form for table blocks: buffer i is
+ * d_base[i*stride .. i*stride + block_len).  Same semantics as above. */
+int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t block_len, size_t n,
+                            const uint32_t *d_seed, uint32_t *d_out, uint32_t flags, void *stream);
+
+/* Host-memory form (the path starts and ends in host memory: log/SST file
+ * buffers).  Copies arena[0 .. arena_bytes) and the metadata to `device`
+ * through pinned staging with hipMemcpyAsync, runs the batch kernel and
+ * copies the n results back; synchronous.  Offsets index into h_arena. */
+int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off,
+                         const uint32_t *h_len, const uint32_t *h_seed, uint32_t *h_out, size_t n,
+                         uint32_t flags, int device);
+
+/* ---- runtime ----------------------------------------------------------- */
+
+/* Uploads the lookup tables to the current device (idempotent; the batch
+ * calls do it on first use).  Returns 0 or an error code. */
+int lv_device_init(void);
+/* Human-readable description of the last error on this thread ("" if none). */
+const char *lv_last_error(void);
+/* Library version string. */
+const char *lv_version(void);
+
+/* ---- synthetic data (bench / tests) ------------------------------------- */
+
+/* d_dst[k] = byte ((begin+k) & 7) of splitmix64(seed ^ ((begin+k) >> 3)) for
+ * k < nbytes: the payload generator of the benchmark configurations (SURVEY
+ * 8d), generated in place in HBM.  Stream-ordered. */
+int lv_fill_splitmix(uint8_t *d_dst, uint64_t begin, uint64_t nbytes, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LVGPU_CRC32C_H */

@@ -1,0 +1,210 @@
+"""lvgpu — Python mirror of the reference's `leveldb::util::crc32c` module
+(src/util/crc32c.rs) over the C ABI in include/lvgpu/crc32c.h, plus the
+batched MI355X entry points.
+
+Names and argument meaning follow the reference:
+    value(data) -> int            crc32c.rs:40
+    extend(crc, data) -> int      crc32c.rs:42-51
+    mask(crc) / unmask(masked)    crc32c.rs:53-63
+    extend_sw / extend_hw         crc32c.rs:65-118
+The batch functions take torch tensors that already live on the GPU (torch is
+used only for device memory and streams) and call the HIP kernels through
+ctypes.  There is no CPU fallback: if the shared library or the GPU is
+missing they raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "liblvgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "lvgpu", "crc32c.h")
+
+MASK = 0x1  # LV_CRC_MASK
+GROUP_FLAGS = {None: 0, 1: 0x100, 4: 0x200, 16: 0x300, 64: 0x400}  # LV_CRC_GROUP(g)
+
+# log_format.rs:22-29, 62-66
+ZERO, FULL, FIRST, MIDDLE, LAST = 0, 1, 2, 3, 4
+BLOCK_SIZE = 32768
+HEADER_SIZE = 7
+
+
+class LvError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load liblvgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LvError(f"{LIB_PATH} missing: build it with `make -C leveldb-rs_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    u8p, u32, u64, sz, vp = ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
+    L.lv_crc32c_value.restype = u32
+    L.lv_crc32c_value.argtypes = [u8p, sz]
+    for f in ("lv_crc32c_extend", "lv_crc32c_extend_sw", "lv_crc32c_extend_hw"):
+        getattr(L, f).restype = u32
+        getattr(L, f).argtypes = [u32, u8p, sz]
+    for f in ("lv_crc32c_mask", "lv_crc32c_unmask"):
+        getattr(L, f).restype = u32
+        getattr(L, f).argtypes = [u32]
+    L.lv_crc32c_batch_device.restype = ctypes.c_int
+    L.lv_crc32c_batch_device.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp]
+    L.lv_crc32c_batch_strided.restype = ctypes.c_int
+    L.lv_crc32c_batch_strided.argtypes = [vp, u64, u32, sz, vp, vp, u32, vp]
+    L.lv_crc32c_batch_host.restype = ctypes.c_int
+    L.lv_crc32c_batch_host.argtypes = [vp, sz, vp, vp, vp, vp, sz, u32, ctypes.c_int]
+    L.lv_device_init.restype = ctypes.c_int
+    L.lv_device_init.argtypes = []
+    L.lv_last_error.restype = ctypes.c_char_p
+    L.lv_last_error.argtypes = []
+    L.lv_version.restype = ctypes.c_char_p
+    L.lv_version.argtypes = []
+    L.lv_fill_splitmix.restype = ctypes.c_int
+    L.lv_fill_splitmix.argtypes = [vp, u64, u64, u64, vp]
+    _lib = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise LvError(f"lvgpu error {rc}: {lib().lv_last_error().decode()}")
+
+
+def declared_symbols() -> list:
+    """Function names declared in include/lvgpu/crc32c.h."""
+    import re
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s+\*?\s*(lv_[a-z0-9_]+)\s*\(", text, re.M)
+
+
+# ---- scalar drop-ins (crc32c.rs) -------------------------------------------
+
+def value(data) -> int:
+    b = bytes(data)
+    return lib().lv_crc32c_value(b, len(b))
+
+
+def extend(crc: int, data) -> int:
+    b = bytes(data)
+    return lib().lv_crc32c_extend(crc & 0xFFFFFFFF, b, len(b))
+
+
+def extend_sw(crc: int, data) -> int:
+    b = bytes(data)
+    return lib().lv_crc32c_extend_sw(crc & 0xFFFFFFFF, b, len(b))
+
+
+def extend_hw(crc: int, data) -> int:
+    b = bytes(data)
+    return lib().lv_crc32c_extend_hw(crc & 0xFFFFFFFF, b, len(b))
+
+
+def mask(crc: int) -> int:
+    return lib().lv_crc32c_mask(crc & 0xFFFFFFFF)
+
+
+def unmask(masked_crc: int) -> int:
+    return lib().lv_crc32c_unmask(masked_crc & 0xFFFFFFFF)
+
+
+# ---- batch (GPU) -----------------------------------------------------------
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_ptr(stream):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dev_ptr(t, name):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise LvError(f"{name} must be a CUDA/HIP tensor")
+    if not t.is_contiguous():
+        raise LvError(f"{name} must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _flags(masked, group):
+    if group not in GROUP_FLAGS:
+        raise LvError(f"group must be one of {sorted(k for k in GROUP_FLAGS if k)}")
+    return (MASK if masked else 0) | GROUP_FLAGS[group]
+
+
+def batch(arena, off, length, seed=None, out=None, masked=False, stream=None, group=None):
+    """Device batch: out[i] = [mask](extend(seed[i] or 0, arena[off[i]:off[i]+length[i]])).
+
+    arena: uint8 CUDA tensor; off: int64 (read as u64); length/seed/out: int32
+    or uint32 CUDA tensors (read as u32).  Returns `out` (uint32 bits in an
+    int32 tensor when allocated here).  Asynchronous on `stream`.
+    """
+    torch = _torch()
+    n = off.numel()
+    if length.numel() != n or (seed is not None and seed.numel() != n):
+        raise LvError("off/length/seed size mismatch")
+    if off.dtype not in (torch.int64, torch.uint64):
+        raise LvError("off must be int64")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=arena.device)
+    _check(lib().lv_crc32c_batch_device(
+        _dev_ptr(arena, "arena"), _dev_ptr(off, "off"), _dev_ptr(length, "length"),
+        _dev_ptr(seed, "seed"), _dev_ptr(out, "out"), n, _flags(masked, group), _stream_ptr(stream)))
+    return out
+
+
+def batch_strided(base, stride: int, block_len: int, n: int, seed=None, out=None, masked=False, stream=None,
+                  group=None):
+    """Device batch over n fixed-size blocks base[i*stride : i*stride+block_len]."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    if n and (n - 1) * stride + block_len > base.numel():
+        raise LvError("blocks exceed base tensor")
+    _check(lib().lv_crc32c_batch_strided(
+        _dev_ptr(base, "base"), stride, block_len, n, _dev_ptr(seed, "seed"), _dev_ptr(out, "out"),
+        _flags(masked, group), _stream_ptr(stream)))
+    return out
+
+
+def batch_host(arena: bytes, off, length, seed=None, masked=False, device: int = 0):
+    """Host-memory batch (pinned staging + H2D + kernel + D2H, synchronous).
+    off/length/seed are numpy arrays (uint64 / uint32); returns np.uint32 array."""
+    import numpy as np
+    a = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else np.ascontiguousarray(arena, dtype=np.uint8)
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(length, dtype=np.uint32)
+    sd = None if seed is None else np.ascontiguousarray(seed, dtype=np.uint32)
+    n = o.size
+    out = np.empty(n, dtype=np.uint32)
+    _check(lib().lv_crc32c_batch_host(
+        a.ctypes.data_as(ctypes.c_void_p), a.size, o.ctypes.data_as(ctypes.c_void_p),
+        ln.ctypes.data_as(ctypes.c_void_p), None if sd is None else sd.ctypes.data_as(ctypes.c_void_p),
+        out.ctypes.data_as(ctypes.c_void_p), n, MASK if masked else 0, device))
+    return out
+
+
+def fill_splitmix(dst, begin: int, seed: int, stream=None):
+    """Fill a uint8 CUDA tensor with the synthetic payload bytes [begin, begin+numel)."""
+    _check(lib().lv_fill_splitmix(_dev_ptr(dst, "dst"), begin, dst.numel(), seed, _stream_ptr(stream)))
+    return dst
+
+
+def device_init() -> None:
+    _check(lib().lv_device_init())
+
+
+def version() -> str:
+    return lib().lv_version().decode()

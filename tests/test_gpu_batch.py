@@ -1,0 +1,214 @@
+"""GPU parity: the HIP batch kernels (through the C ABI) against the CPU oracle
+(restating crc32c.rs) — bit-exact, on the reference KATs, the committed golden
+cases, edge cases (empty, < 4 bytes, every start alignment, ragged tails,
+max WAL fragment, 64 KiB+), every kernel group size, masked and seeded
+outputs, and the full-size configuration (262,144 x 4 KiB = 1 GiB)."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from conftest import kat_bytes
+import lvgpu
+import wal_oracle as W
+
+pytestmark = pytest.mark.gpu
+
+GROUPS = [1, 4, 16, 64]
+
+
+def oracle_batch(arena: bytes, off, ln, seed, masked):
+    L = W.lib()
+    a = np.frombuffer(arena, dtype=np.uint8)
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    n = np.ascontiguousarray(ln, dtype=np.uint32)
+    s = None if seed is None else np.ascontiguousarray(seed, dtype=np.uint32)
+    out = np.zeros(o.size, dtype=np.uint32)
+    L.oracle_batch(a.ctypes.data, o.ctypes.data, n.ctypes.data, None if s is None else s.ctypes.data,
+                   out.ctypes.data, o.size, 1 if masked else 0)
+    return out
+
+
+def gpu_batch(torch, dev, arena: bytes, off, ln, seed, masked, group=None):
+    a = torch.frombuffer(bytearray(arena), dtype=torch.uint8).to(dev)
+    o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
+    n = torch.from_numpy(np.ascontiguousarray(ln, dtype=np.uint32).view(np.int32)).to(dev)
+    s = None if seed is None else torch.from_numpy(np.ascontiguousarray(seed, dtype=np.uint32).view(np.int32)).to(dev)
+    out = lvgpu.batch(a, o, n, s, masked=masked, group=group)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def torch_dev(gpu):
+    import torch
+    return torch, gpu
+
+
+@pytest.mark.parametrize("group", [None] + GROUPS)
+def test_kats_every_alignment(torch_dev, kat, group):
+    torch, dev = torch_dev
+    pieces, offs, lens, want = bytearray(), [], [], []
+    for k in kat["kats"]:
+        d = kat_bytes(k)
+        for shift in range(16):
+            pieces += bytes(shift)
+            offs.append(len(pieces))
+            lens.append(len(d))
+            pieces += d
+            want.append(k["value"])
+    got = gpu_batch(torch, dev, bytes(pieces), offs, lens, None, False, group)
+    assert list(got) == want
+
+
+@pytest.mark.parametrize("group", [None] + GROUPS)
+@pytest.mark.parametrize("masked", [False, True])
+def test_golden_cases(torch_dev, kat, arena, group, masked):
+    torch, dev = torch_dev
+    c = np.array(kat["cases"], dtype=np.uint64)
+    got = gpu_batch(torch, dev, arena, c[:, 0], c[:, 1], c[:, 2], masked, group)
+    want = c[:, 4] if masked else c[:, 3]
+    bad = np.nonzero(got != want.astype(np.uint32))[0]
+    assert bad.size == 0, [(int(c[i, 0]), int(c[i, 1]), hex(int(got[i])), hex(int(want[i]))) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("group", [None] + GROUPS)
+def test_small_lengths_all_offsets(torch_dev, arena, group):
+    """Every length 0..300 at every start offset mod 64, random seeds."""
+    torch, dev = torch_dev
+    rng = random.Random(11 + (group or 0))
+    offs, lens, seeds = [], [], []
+    for ln in range(0, 301):
+        for mis in range(0, 64, 3):
+            offs.append(4096 * rng.randrange(1, 200) + mis)
+            lens.append(ln)
+            seeds.append(rng.getrandbits(32))
+    want = oracle_batch(arena, offs, lens, seeds, False)
+    got = gpu_batch(torch, dev, arena, offs, lens, seeds, False, group)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(offs[i], lens[i]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("group", GROUPS)
+@pytest.mark.parametrize("block_len", [1, 3, 4, 5, 15, 16, 17, 100, 128, 129, 1000, 1024, 1025, 4096,
+                                       4100, 16384, 16385, 32762, 65536, 70001])
+def test_strided_blocks(torch_dev, group, block_len):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(block_len)
+    n = max(8, min(600, (4 << 20) // max(block_len, 1)))
+    stride = block_len + int(rng.integers(0, 40))
+    total = stride * n + 64
+    host = rng.integers(0, 256, size=total, dtype=np.uint8).tobytes()
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    base_off = int(rng.integers(0, 16))
+    offs = base_off + np.arange(n, dtype=np.uint64) * stride
+    want = oracle_batch(host, offs, np.full(n, block_len, np.uint32), seeds, True)
+    t = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out = lvgpu.batch_strided(t[base_off:], stride, block_len, n, seed=sd, masked=True, group=group)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+
+
+def test_mixed_lengths_zipf(torch_dev):
+    """Config-4 shape (Zipf 32 B - 64 KiB, misaligned), reduced count."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(0xC0FFEE)
+    k = np.minimum(rng.zipf(1.1, size=20000), 2048)
+    lens = (32 * k - rng.integers(0, 32, size=k.size)).astype(np.uint32)
+    offs = np.zeros(lens.size, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(offs[-1] + lens[-1]) + 16
+    host = bytearray(total)
+    W.lib().oracle_fill_splitmix(ctypes.addressof(ctypes.c_char.from_buffer(host)), 0, total, 77)
+    host = bytes(host)
+    want = oracle_batch(host, offs, lens, None, False)
+    got = gpu_batch(torch, dev, host, offs, lens, None, False)
+    assert np.array_equal(got, want)
+
+
+def test_wal_units(torch_dev, wal_golden):
+    """Batched form of log_reader.rs:335-336 over the WAL fixtures' CRC units:
+    value([type||payload]) of every physical record of the fragmentation scenario."""
+    torch, dev = torch_dev
+    dest = bytearray()
+    wr = W.Writer(dest)
+    for m in ("small", W.big_string("medium", 50000), W.big_string("large", 100000)):
+        wr.add_record(m.encode())
+    log = bytes(dest)
+    recs = W.wal_physical_records(log)
+    offs = [o + 6 for o, _, _ in recs]
+    lens = [ln + 1 for _, ln, _ in recs]
+    got = gpu_batch(torch, dev, log, offs, lens, None, False)
+    want = [W.unmask(W.decode_fixed_32(log[o:o + 4])) for o, _, _ in recs]
+    assert list(got) == want
+    scen = {s["name"]: s for s in wal_golden["scenarios"]}["fragmentation"]
+    assert [u[1] for u in scen["crc_units"]] == want
+
+
+def test_wal_writer_seeded_masked(torch_dev):
+    """Batched form of log_writer.rs:123-125: mask(extend(type_crc[t], payload))."""
+    torch, dev = torch_dev
+    dest = bytearray()
+    wr = W.Writer(dest)
+    rnd = W.Random(301)
+    for i in range(300):
+        wr.add_record(W.random_skewed_string(i, rnd).encode())
+    log = bytes(dest)
+    recs = W.wal_physical_records(log)
+    offs = [o + 7 for o, _, _ in recs]
+    lens = [ln for _, ln, _ in recs]
+    seeds = [wr.type_crc[t] for _, _, t in recs]
+    got = gpu_batch(torch, dev, log, offs, lens, seeds, True)
+    want = [W.decode_fixed_32(log[o:o + 4]) for o, _, _ in recs]
+    assert list(got) == want
+
+
+def test_host_api(kat, arena):
+    c = np.array(kat["cases"], dtype=np.uint64)
+    got = lvgpu.batch_host(arena, c[:, 0], c[:, 1], c[:, 2].astype(np.uint32), masked=True)
+    assert np.array_equal(got, c[:, 4].astype(np.uint32))
+
+
+def test_fill_matches_oracle_generator(torch_dev):
+    torch, dev = torch_dev
+    for begin, n in ((0, 4096), (13, 1001), (8, 64)):
+        t = torch.empty(n, dtype=torch.uint8, device=dev)
+        lvgpu.fill_splitmix(t, begin, 0x4C444231)
+        torch.cuda.synchronize()
+        h = ctypes.create_string_buffer(n)
+        W.lib().oracle_fill_splitmix(h, begin, n, 0x4C444231)
+        assert bytes(t.cpu().numpy()) == h.raw
+
+
+def test_full_size_c3(torch_dev):
+    """Config 3 at full size: 262,144 x 4 KiB = 1 GiB, bit-exact vs the oracle
+    for every block, masked and unmasked, through both batch entry points."""
+    torch, dev = torch_dev
+    n, bl = 262144, 4096
+    seed = 0x4C444231
+    t = torch.empty(n * bl, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(t, 0, seed)
+    offs = torch.arange(n, dtype=torch.int64, device=dev) * bl
+    lens = torch.full((n,), bl, dtype=torch.int32, device=dev)
+    out1 = lvgpu.batch(t, offs, lens)
+    out2 = lvgpu.batch_strided(t, bl, bl, n, masked=True)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    want = oracle_batch(host.tobytes(), np.arange(n, dtype=np.uint64) * bl, np.full(n, bl, np.uint32), None, False)
+    assert np.array_equal(out1.cpu().numpy().view(np.uint32), want)
+    mk = np.array([W.mask(int(x)) for x in want[:4096]], dtype=np.uint32)
+    got2 = out2.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got2[:4096], mk)
+    # size-independent: unmask(masked) must reproduce every unmasked CRC
+    assert np.array_equal(np.array([W.unmask(int(x)) for x in got2[-4096:]], dtype=np.uint32), want[-4096:])
+
+
+def test_bad_arguments_raise(torch_dev):
+    torch, dev = torch_dev
+    with pytest.raises(lvgpu.LvError):
+        lvgpu.lib()  # loads fine
+        rc = lvgpu.lib().lv_crc32c_batch_device(None, None, None, None, None, 5, 0, None)
+        lvgpu._check(rc)
