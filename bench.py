@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"])
     p.add_argument("--api", default="offsets", choices=["offsets", "strided"])
+    p.add_argument("--group", type=int, default=None, choices=[1, 4, 16, 64],
+                   help="force the kernel's lanes-per-buffer group size (tuning)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--pmc-csv", default=None, help="rocprofv3 --pmc counter CSV for roofline.traffic")
     return p.parse_args()
@@ -178,10 +180,10 @@ def main():
 
     if args.api == "strided" and args.workload in ("c3", "c5"):
         def step():
-            lvgpu.batch_strided(arena, 4096, 4096, n, out=out, stream=stream)
+            lvgpu.batch_strided(arena, 4096, 4096, n, out=out, stream=stream, group=args.group)
     else:
         def step():
-            lvgpu.batch(arena, off, ln, out=out, stream=stream)
+            lvgpu.batch(arena, off, ln, out=out, stream=stream, group=args.group)
 
     for _ in range(args.warmup):
         step()

@@ -129,8 +129,20 @@ __device__ __forceinline__ uint32_t fix_word(uint32_t w, int64_t rel, uint32_t s
     return w ^ (s0 >> (static_cast<uint32_t>(rel) * 8u));
 }
 
+// Global (address space 1) pointers: global_load_* counts only in vmcnt, so
+// outstanding HBM loads never hold up the LDS lookups' lgkmcnt waits (a flat
+// load would count in both).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef const __attribute__((address_space(1))) uint8_t g_uint8;
+
 __device__ __forceinline__ uint4 load_granule(uint64_t g) {
-    return *reinterpret_cast<const uint4 *>(g << 4);
+    const u32x4 v = *reinterpret_cast<g_u32x4 *>(g << 4);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t load_byte(uint64_t addr) {
+    return *reinterpret_cast<g_uint8 *>(addr);
 }
 
 __device__ __forceinline__ uint32_t mask_crc(uint32_t c) {  // crc32c.rs:54-57
@@ -147,7 +159,7 @@ __device__ __forceinline__ uint32_t crc_group(uint64_t a, uint32_t len, uint32_t
         uint32_t s = s0;
         if (gl == 0)
             for (uint32_t i = 0; i < len; ++i)
-                s = byte_step(s, *reinterpret_cast<const uint8_t *>(a + i), L.c4);
+                s = byte_step(s, load_byte(a + i), L.c4);
         return ~s;
     }
     const uint64_t e = a + len;
@@ -162,27 +174,48 @@ __device__ __forceinline__ uint32_t crc_group(uint64_t a, uint32_t len, uint32_t
     uint4 tail = make_uint4(0, 0, 0, 0);
     if (gl == 0 && tail_hi != 0) tail = load_granule(gend);
 
-    uint32_t A = 0;
-    for (uint32_t r = 0; r < nrows; ++r) {
+    // Rows are consumed in batches of U with the next batch's loads in flight
+    // (software pipeline: 2*U granules = 2*U*16*64 B per wave outstanding).
+    constexpr uint32_t U = 4;
+    const int64_t g0s = static_cast<int64_t>(g0);
+    auto load_row = [&](uint32_t r) -> uint4 {
         const int64_t g = gs + static_cast<int64_t>(G) * r + gl;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (g >= static_cast<int64_t>(g0)) {
-            v = load_granule(static_cast<uint64_t>(g));
-            const int64_t rel = static_cast<int64_t>(static_cast<uint64_t>(g) << 4) -
-                                static_cast<int64_t>(a);
-            if (rel < 4) {
+        if (r < nrows && g >= g0s) return load_granule(static_cast<uint64_t>(g));
+        return make_uint4(0, 0, 0, 0);
+    };
+    uint4 cur[U], nxt[U];
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) cur[j] = load_row(j);
+
+    uint32_t A = 0;
+    for (uint32_t r = 0; r < nrows; r += U) {
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) nxt[j] = load_row(r + U + j);
+        uint32_t p[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) {
+            uint4 v = cur[j];
+            const int64_t g = gs + static_cast<int64_t>(G) * (r + j) + gl;
+            const int64_t rel = g * 16 - static_cast<int64_t>(a);
+            if (rel < 4 && g >= g0s) {  // head granule(s): zero pre-buffer bytes, xor seed
                 v.x = fix_word(v.x, rel, s0);
                 v.y = fix_word(v.y, rel + 4, s0);
                 v.z = fix_word(v.z, rel + 8, s0);
                 v.w = fix_word(v.w, rel + 12, s0);
             }
+            if constexpr (G == 1) {
+                if (r + j < nrows) A = chain16(A, v, L);
+            } else {
+                p[j] = chain16(0u, v, L);
+            }
         }
-        if constexpr (G == 1) {
-            A = chain16(A, v, L);
-        } else {
-            const uint32_t p = chain16(0u, v, L);
-            A = lookup4<kShiftOff>(A, L) ^ p;
+        if constexpr (G != 1) {
+#pragma unroll
+            for (uint32_t j = 0; j < U; ++j)
+                if (r + j < nrows) A = lookup4<kShiftOff>(A, L) ^ p[j];
         }
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) cur[j] = nxt[j];
     }
 #pragma unroll
     for (int k = 0; (1 << k) < G; ++k) {
