@@ -35,23 +35,31 @@ PAYLOAD_SEED = 0x4C444231
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    # MI355X needs ~50-60 back-to-back 1 GiB launches (~12 ms) before its
+    # clocks settle (launch time drifts 0.17 -> 0.24 -> 0.17 ms); the default
+    # warmup covers that transient so the timed steps are steady state.
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"])
-    p.add_argument("--api", default="offsets", choices=["offsets", "strided"])
+    p.add_argument("--api", default="strided", choices=["offsets", "strided"],
+                   help="strided = lv_crc32c_batch_strided (fixed-size table blocks); "
+                        "offsets = lv_crc32c_batch_device (arbitrary buffers)")
     p.add_argument("--group", type=int, default=None, choices=[1, 4, 16, 64],
                    help="force the kernel's lanes-per-buffer group size (tuning)")
+    p.add_argument("--blocks", type=int, default=None, help="override the c3/c5 block count (diagnostics)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--pmc-csv", default=None, help="rocprofv3 --pmc counter CSV for roofline.traffic")
     return p.parse_args()
 
 
-def build_workload(torch, lvgpu, name, dev, rank):
+def build_workload(torch, lvgpu, name, dev, rank, blocks=None):
     """Returns (arena, off, len, nbytes, description) on `dev`."""
     import numpy as np
     seed = PAYLOAD_SEED ^ (rank * 0x9E3779B9)
     if name in ("c3", "c5"):
         n = 262144 if name == "c3" else 2097152  # c5: 64 GiB over 8 GPUs = 8 GiB per GPU
+        if blocks:
+            n = blocks
         bl = 4096
         arena = torch.empty(n * bl, dtype=torch.uint8, device=dev)
         lvgpu.fill_splitmix(arena, 0, seed)
@@ -173,7 +181,7 @@ def main():
     torch.cuda.set_device(dev)
     lvgpu.device_init()
 
-    arena, off, ln, nbytes, desc = build_workload(torch, lvgpu, args.workload, dev, rank)
+    arena, off, ln, nbytes, desc = build_workload(torch, lvgpu, args.workload, dev, rank, args.blocks)
     n = off.numel()
     out = torch.empty(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
@@ -207,7 +215,10 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kern_ms = sorted(s.elapsed_time(e) for s, e in evs)
+    kern_seq = [s.elapsed_time(e) for s, e in evs]
+    kern_ms = sorted(kern_seq)
+    if os.environ.get("LVGPU_BENCH_TRACE"):
+        print("per-launch ms:", " ".join(f"{x:.4f}" for x in kern_seq), file=sys.stderr)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
 
     total_bytes = nbytes * world
@@ -236,7 +247,9 @@ def main():
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "kernel": "lvk::crc32c_batch_kernel", "kernel_ms_avg": round(kern_avg_ms, 4),
-                         "kernel_ms_min": round(kern_ms[0], 4), "bytes_per_launch": nbytes},
+                         "kernel_ms_min": round(kern_ms[0], 4),
+                         "kernel_ms_p50": round(kern_ms[len(kern_ms) // 2], 4),
+                         "kernel_ms_max": round(kern_ms[-1], 4), "bytes_per_launch": nbytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

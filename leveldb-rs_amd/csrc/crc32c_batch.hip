@@ -43,20 +43,27 @@
 
 namespace lvk {
 
-constexpr int kThreads = 1024;                   // 16 waves: 4 per SIMD
+constexpr int kThreads = 1024;  // 16 waves: 4 per SIMD, one workgroup per CU
 constexpr int kWaves = kThreads / 64;
-constexpr int kCombWords = 6 * 4 * 256;          // Shift_{16*2^k} byte tables, k = 0..5
-constexpr int kLatinWords = 256 * 64;            // 256 rows x 256 B
-constexpr int kImageWords = kCombWords + kLatinWords;  // 22528 dwords = 88 KiB
-constexpr uint32_t kLatinBase = kCombWords * 4;  // 24576, fits the ds offset field
-constexpr uint32_t kShiftOff = 128;              // W tables: dwords 32..63 of a row
+constexpr uint32_t U = 4;       // rows per batch (= interleaved Horner accumulators)
+
+// LDS image (bytes):
+//   [0, 64K)      region A, 256 rows x 256 B: dwords 0..31 T0..T3 (Latin),
+//                 dwords 32..63 W4 = Shift_{16*G*U} (Latin)
+//   [64K, 128K)   region B: dwords 0..31 W1 = Shift_{16*G}, 32..63 W2 = Shift_{32*G}
+//   [128K, 152K)  combine tables Shift_{16*2^k}, k = 0..5, plain byte tables
+constexpr uint32_t kRegionA = 0;
+constexpr uint32_t kRegionB = 65536;
+constexpr uint32_t kHalf = 128;  // second table set of a region: +32 dwords
+constexpr uint32_t kComb = 131072;
+constexpr int kImageWords = (131072 + 6 * 4 * 1024) / 4;  // 38912 dwords = 152 KiB
 
 __shared__ __attribute__((aligned(16))) uint32_t g_lds[kImageWords];
 
 // Per-lane lookup constants: lv byte i = 4*beta_i (dword of the lane's table
-// copy for instruction i); sel_i moves that byte to bits 0..7 and the state
-// byte indexing table k_i to bits 8..15 (v_perm selector: 0-3 = S1 bytes,
-// 4-7 = S0 bytes, 12 = 0x00).
+// copy for lookup instruction i); sel_i moves that byte to bits 0..7 and the
+// state byte that indexes table k_i to bits 8..15 (v_perm selector: 0-3 = S1
+// bytes, 4-7 = S0 bytes, 12 = 0x00).
 struct Lut {
     uint32_t lv, sel0, sel1, sel2, sel3, c4;
 };
@@ -84,191 +91,459 @@ __device__ __forceinline__ uint32_t lds_word(uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(g_lds) + byte_addr);
 }
 
-// XOR of the four Latin-region tables at OFF (0: T, kShiftOff: W) indexed by
-// the four bytes of s.  OFF = 0: one slice-by-4 step, T3[b0]^T2[b1]^T1[b2]^T0[b3].
+// XOR of the four Latin tables at byte offset OFF indexed by the bytes of s.
+// OFF = 0 is one slice-by-4 step T3[b0]^T2[b1]^T1[b2]^T0[b3]; the shift
+// regions hold S[3-k] at table slot k so the same selectors index them.
 template <uint32_t OFF>
 __device__ __forceinline__ uint32_t lookup4(uint32_t s, const Lut &L) {
     const uint32_t a0 = __builtin_amdgcn_perm(s, L.lv, L.sel0);
     const uint32_t a1 = __builtin_amdgcn_perm(s, L.lv, L.sel1);
     const uint32_t a2 = __builtin_amdgcn_perm(s, L.lv, L.sel2);
     const uint32_t a3 = __builtin_amdgcn_perm(s, L.lv, L.sel3);
-    return lds_word(a0 + kLatinBase + OFF) ^ lds_word(a1 + kLatinBase + OFF) ^
-           lds_word(a2 + kLatinBase + OFF) ^ lds_word(a3 + kLatinBase + OFF);
+    return lds_word(a0 + OFF) ^ lds_word(a1 + OFF) ^ lds_word(a2 + OFF) ^ lds_word(a3 + OFF);
 }
 
-// R(s, 16 bytes of v).
-__device__ __forceinline__ uint32_t chain16(uint32_t s, uint4 v, const Lut &L) {
-    s = lookup4<0>(s ^ v.x, L);
-    s = lookup4<0>(s ^ v.y, L);
-    s = lookup4<0>(s ^ v.z, L);
-    return lookup4<0>(s ^ v.w, L);
+// R(0, 16 bytes of v): four slice-by-4 steps.
+__device__ __forceinline__ uint32_t r0_granule(uint4 v, const Lut &L) {
+    uint32_t s = lookup4<kRegionA>(v.x, L);
+    s = lookup4<kRegionA>(s ^ v.y, L);
+    s = lookup4<kRegionA>(s ^ v.z, L);
+    return lookup4<kRegionA>(s ^ v.w, L);
 }
 
-// Shift_{16*2^k}(a) from the unreplicated combine tables.
+// Address of lookup i of state s (one v_perm_b32).
+template <int I>
+__device__ __forceinline__ uint32_t lut_addr(uint32_t s, const Lut &L) {
+    const uint32_t sel = I == 0 ? L.sel0 : I == 1 ? L.sel1 : I == 2 ? L.sel2 : L.sel3;
+    return __builtin_amdgcn_perm(s, L.lv, sel);
+}
+
+// The U granules of a batch folded step-major: every slice-by-4 step issues
+// the 4U lookups of all U chains (plus, in step 0, the U row-shift lookups of
+// the accumulators) before consuming any, so 4U+ LDS reads are in flight per
+// wave instead of one chain's 4.  p[i] = R(0, v[i]); A[i] = W4(A[i]) ^ p[i]
+// (or A[i] = p[i] when FIRST).
+template <bool FIRST>
+__device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U], const Lut &L) {
+    uint32_t s[U], w[U];
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) s[i] = v[i].x;
+    if constexpr (!FIRST) {
+        uint32_t aa[U][4];
+#pragma unroll
+        for (uint32_t i = 0; i < U; ++i) {
+            aa[i][0] = lut_addr<0>(A[i], L);
+            aa[i][1] = lut_addr<1>(A[i], L);
+            aa[i][2] = lut_addr<2>(A[i], L);
+            aa[i][3] = lut_addr<3>(A[i], L);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < U; ++i)
+            w[i] = lds_word(aa[i][0] + kRegionA + kHalf) ^ lds_word(aa[i][1] + kRegionA + kHalf) ^
+                   lds_word(aa[i][2] + kRegionA + kHalf) ^ lds_word(aa[i][3] + kRegionA + kHalf);
+    }
+#pragma unroll
+    for (uint32_t step = 0; step < 4; ++step) {
+        uint32_t ad[U][4];
+#pragma unroll
+        for (uint32_t i = 0; i < U; ++i) {
+            ad[i][0] = lut_addr<0>(s[i], L);
+            ad[i][1] = lut_addr<1>(s[i], L);
+            ad[i][2] = lut_addr<2>(s[i], L);
+            ad[i][3] = lut_addr<3>(s[i], L);
+        }
+        uint32_t t[U][4];
+#pragma unroll
+        for (uint32_t i = 0; i < U; ++i)
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) t[i][k] = lds_word(ad[i][k] + kRegionA);
+#pragma unroll
+        for (uint32_t i = 0; i < U; ++i) {
+            const uint32_t nw = step == 0 ? v[i].y : step == 1 ? v[i].z : step == 2 ? v[i].w : 0u;
+            s[i] = (t[i][0] ^ t[i][1]) ^ (t[i][2] ^ t[i][3]) ^ nw;
+        }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) A[i] = FIRST ? s[i] : (w[i] ^ s[i]);
+}
+
+// Shift_{16*2^k}(a) from the plain combine tables.
 __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
-    const uint32_t *t = g_lds + k * 1024;
+    const uint32_t *t = g_lds + (kComb / 4) + k * 1024;
     return t[a & 0xffu] ^ t[256 + ((a >> 8) & 0xffu)] ^ t[512 + ((a >> 16) & 0xffu)] ^
            t[768 + (a >> 24)];
 }
 
-// One byte through T0 (copy of this lane): crc32c.rs:81.
+// One byte through T0 (this lane's copy): crc32c.rs:81.
 __device__ __forceinline__ uint32_t byte_step(uint32_t s, uint32_t b, uint32_t c4) {
     const uint32_t e = (s ^ b) & 0xffu;
-    return g_lds[kCombWords + e * 64u + c4] ^ (s >> 8);
+    return g_lds[e * 64u + c4] ^ (s >> 8);
 }
 
-// Head fix-up of word d of a granule: rel = (word address) - (buffer start).
-// Bytes before the buffer become 0; bytes 0..3 of the buffer get s0 xored in.
-__device__ __forceinline__ uint32_t fix_word(uint32_t w, int64_t rel, uint32_t s0) {
-    if (rel >= 4) return w;
-    if (rel <= -4) return 0u;
-    if (rel < 0) {
-        const uint32_t sh = static_cast<uint32_t>(-rel) * 8u;
-        return (w & (0xffffffffu << sh)) ^ (s0 << sh);
-    }
-    return w ^ (s0 >> (static_cast<uint32_t>(rel) * 8u));
+// Head fix-up of one word at byte offset rel from the buffer start: bytes
+// before the buffer become 0 and buffer bytes 0..3 get s0 xored in.
+// Branch-free (selects); only executed for lanes that hold head bytes.
+__device__ __forceinline__ uint32_t fix_word(uint32_t w, int32_t rel, uint32_t s0) {
+    const int32_t z = -rel;  // leading bytes of the word that precede the buffer
+    const uint32_t keep = z <= 0 ? 0xffffffffu : (z >= 4 ? 0u : 0xffffffffu << (8 * z));
+    const uint32_t sx =
+        (rel >= 4 || rel <= -4) ? 0u : (rel >= 0 ? s0 >> (8 * rel) : s0 << (8 * z));
+    return (w & keep) ^ sx;
 }
 
-// Global (address space 1) pointers: global_load_* counts only in vmcnt, so
+// Global (address space 1) loads: global_load_* counts only in vmcnt, so
 // outstanding HBM loads never hold up the LDS lookups' lgkmcnt waits (a flat
 // load would count in both).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
-typedef const __attribute__((address_space(1))) uint8_t g_uint8;
 
-__device__ __forceinline__ uint4 load_granule(uint64_t g) {
-    const u32x4 v = *reinterpret_cast<g_u32x4 *>(g << 4);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
+__device__ __forceinline__ uint4 to_uint4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
-__device__ __forceinline__ uint32_t load_byte(uint64_t addr) {
-    return *reinterpret_cast<g_uint8 *>(addr);
+// Payload loads are non-temporal (global_load_dwordx4 ... nt): every byte is
+// read exactly once, and keeping the stream out of L2/MALL measured +13-15 %
+// on the 1 GiB configuration (tools/crc_ideal_probe.hip).
+__device__ __forceinline__ uint4 load16(uint64_t addr) {
+    return to_uint4(__builtin_nontemporal_load(reinterpret_cast<g_u32x4 *>(addr)));
 }
 
 __device__ __forceinline__ uint32_t mask_crc(uint32_t c) {  // crc32c.rs:54-57
     return ((c >> 15) | (c << 17)) + 0xa282ead8u;
 }
 
-// CRC of buffer [a, a+len) (absolute device address) with seed, computed by the
-// G lanes of a group; the result is valid in lane gl == 0.
+struct Params {
+    uint64_t base;  // arena address
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint32_t *seed;
+    uint32_t *out;
+    uint64_t n;
+    uint64_t stride;
+    uint32_t blen;
+    uint32_t flags;
+};
+
+// Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of
+// U rows x G granules end at the last whole granule, so every batch is full;
+// granules of batch 0 that precede the buffer are fixed up to zero.
+// Granule index g is expressed relative to g0 = a >> 4: d = g - g0.
+struct Geo {
+    uint64_t abase;  // a & ~15 (address of granule g0)
+    uint32_t len;
+    uint32_t seed;
+    uint32_t nb;     // batches, >= 1
+    int32_t hoff;    // d of batch 0 row 0 lane 0, in (-G*U, 0]
+    uint32_t alow;   // a & 15, | 16 if batch 1 also holds head bytes
+};
+
 template <int G>
-__device__ __forceinline__ uint32_t crc_group(uint64_t a, uint32_t len, uint32_t seed, uint32_t gl,
-                                              const Lut &L) {
-    const uint32_t s0 = ~seed;
-    if (len < 4) {  // crc32c.rs:112-115 path: bytewise from the seeded state
-        uint32_t s = s0;
-        if (gl == 0)
-            for (uint32_t i = 0; i < len; ++i)
-                s = byte_step(s, load_byte(a + i), L.c4);
-        return ~s;
-    }
-    const uint64_t e = a + len;
-    const uint64_t g0 = a >> 4, gend = e >> 4;
-    const uint32_t ng = static_cast<uint32_t>(gend - g0);
-    const uint32_t nrows = (ng + G - 1) / G;
-    const int64_t gs = static_cast<int64_t>(gend) - static_cast<int64_t>(G) * nrows;
-    const uint64_t tail_base = gend << 4;
-    const uint32_t tail_hi = static_cast<uint32_t>(e - tail_base);
-    const uint32_t tail_lo = a > tail_base ? static_cast<uint32_t>(a - tail_base) : 0u;
-
-    uint4 tail = make_uint4(0, 0, 0, 0);
-    if (gl == 0 && tail_hi != 0) tail = load_granule(gend);
-
-    // Rows are consumed in batches of U with the next batch's loads in flight
-    // (software pipeline: 2*U granules = 2*U*16*64 B per wave outstanding).
-    constexpr uint32_t U = 4;
-    const int64_t g0s = static_cast<int64_t>(g0);
-    auto load_row = [&](uint32_t r) -> uint4 {
-        const int64_t g = gs + static_cast<int64_t>(G) * r + gl;
-        if (r < nrows && g >= g0s) return load_granule(static_cast<uint64_t>(g));
-        return make_uint4(0, 0, 0, 0);
-    };
-    uint4 cur[U], nxt[U];
-#pragma unroll
-    for (uint32_t j = 0; j < U; ++j) cur[j] = load_row(j);
-
-    uint32_t A = 0;
-    for (uint32_t r = 0; r < nrows; r += U) {
-#pragma unroll
-        for (uint32_t j = 0; j < U; ++j) nxt[j] = load_row(r + U + j);
-        uint32_t p[U];
-#pragma unroll
-        for (uint32_t j = 0; j < U; ++j) {
-            uint4 v = cur[j];
-            const int64_t g = gs + static_cast<int64_t>(G) * (r + j) + gl;
-            const int64_t rel = g * 16 - static_cast<int64_t>(a);
-            if (rel < 4 && g >= g0s) {  // head granule(s): zero pre-buffer bytes, xor seed
-                v.x = fix_word(v.x, rel, s0);
-                v.y = fix_word(v.y, rel + 4, s0);
-                v.z = fix_word(v.z, rel + 8, s0);
-                v.w = fix_word(v.w, rel + 12, s0);
-            }
-            if constexpr (G == 1) {
-                if (r + j < nrows) A = chain16(A, v, L);
-            } else {
-                p[j] = chain16(0u, v, L);
-            }
-        }
-        if constexpr (G != 1) {
-#pragma unroll
-            for (uint32_t j = 0; j < U; ++j)
-                if (r + j < nrows) A = lookup4<kShiftOff>(A, L) ^ p[j];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < U; ++j) cur[j] = nxt[j];
-    }
-#pragma unroll
-    for (int k = 0; (1 << k) < G; ++k) {
-        const uint32_t other = __shfl_down(A, 1u << k, G);
-        A = comb_shift(A, k) ^ other;
-    }
-    if (gl == 0) {
-        const uint32_t tw[4] = {tail.x, tail.y, tail.z, tail.w};
-        for (uint32_t i = tail_lo; i < tail_hi; ++i) {
-            uint32_t b = (tw[i >> 2] >> (8u * (i & 3u))) & 0xffu;
-            const uint64_t rel = tail_base + i - a;
-            if (rel < 4) b ^= (s0 >> (8u * static_cast<uint32_t>(rel))) & 0xffu;
-            A = byte_step(A, b, L.c4);
-        }
-    }
-    return ~A;
+__device__ __forceinline__ Geo make_geo(uint64_t a, uint32_t len, uint32_t seed) {
+    constexpr int32_t GU = G * static_cast<int32_t>(U);
+    Geo q;
+    q.abase = a & ~static_cast<uint64_t>(15);
+    q.len = len;
+    q.seed = seed;
+    const uint32_t alow = static_cast<uint32_t>(a & 15u);
+    const int32_t ng = static_cast<int32_t>(((alow + len) >> 4));  // whole granules from g0
+    const int32_t nb = ng > 0 ? (ng + GU - 1) / GU : 1;
+    q.nb = static_cast<uint32_t>(nb);
+    q.hoff = ng - GU * nb;
+    const bool fix2 = nb > 1 && q.hoff == -(GU - 1) && alow > 12u;  // seed spills into batch 1
+    q.alow = alow | (fix2 ? 16u : 0u);
+    return q;
 }
 
+template <int G, bool STRIDED>
+__device__ __forceinline__ Geo fetch_geo(const Params &P, uint64_t b) {
+    if constexpr (STRIDED) {
+        return make_geo<G>(P.base + b * P.stride, P.blen, P.seed ? P.seed[b] : 0u);
+    } else {
+        return make_geo<G>(P.base + P.off[b], P.len[b], P.seed ? P.seed[b] : 0u);
+    }
+}
+
+// Batch j >= 1: all rows lie inside the buffer.
+template <int G>
+__device__ __forceinline__ void load_batch(const Geo &q, uint32_t j, uint32_t gl, uint4 (&v)[U]) {
+    const int32_t d = q.hoff + static_cast<int32_t>(G * U * j + gl);
+    const uint64_t p = q.abase + (static_cast<int64_t>(d) << 4);
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) v[i] = load16(p + 16u * G * i);
+}
+
+// Batch 0: rows before the buffer are clamped to granule g0 (a valid
+// address); fix_head zeroes them afterwards.
+template <int G>
+__device__ __forceinline__ void load_batch0(const Geo &q, uint32_t gl, uint4 (&v)[U]) {
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+        int32_t d = q.hoff + static_cast<int32_t>(G * i + gl);
+        d = d < 0 ? 0 : d;
+        v[i] = load16(q.abase + (static_cast<uint32_t>(d) << 4));
+    }
+}
+
+// The tail granule (bytes after the last whole granule), lane 0 only.
+__device__ __forceinline__ uint4 load_tail(const Geo &q, uint32_t gl) {
+    const uint32_t end = (q.alow & 15u) + q.len;
+    if (gl == 0 && (end & 15u)) return load16(q.abase + (end & ~15u));
+    return make_uint4(0, 0, 0, 0);
+}
+
+// Head bytes of batch j: the granule g0 (d == 0) loses its pre-buffer bytes
+// and takes the seed in buffer bytes 0..3; g0+1 (d == 1) takes the seed bytes
+// that spill past g0 when a % 16 > 12.  Only those lanes run the fix-up.
+template <int G>
+__device__ __forceinline__ void fix_head(const Geo &q, uint32_t j, uint32_t gl, uint4 (&v)[U]) {
+    const uint32_t s0 = q.len >= 4 ? ~q.seed : 0u;
+    const int32_t alow = static_cast<int32_t>(q.alow & 15u);
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+        const int32_t d = q.hoff + static_cast<int32_t>(G * (U * j + i) + gl);
+        if (d == 0 || (d == 1 && alow > 12)) {
+            const int32_t rel = d * 16 - alow;
+            v[i].x = fix_word(v[i].x, rel, s0);
+            v[i].y = fix_word(v[i].y, rel + 4, s0);
+            v[i].z = fix_word(v[i].z, rel + 8, s0);
+            v[i].w = fix_word(v[i].w, rel + 12, s0);
+        }
+    }
+}
+
+// Batch 0 rows that lie wholly before the buffer (d < 0) were loaded from a
+// clamped address; they contribute nothing.
+template <int G>
+__device__ __forceinline__ void drop_pre_rows(const Geo &q, uint32_t gl, uint32_t (&A)[U]) {
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i)
+        if (q.hoff + static_cast<int32_t>(G * i + gl) < 0) A[i] = 0u;
+}
+
+// Finish a buffer: merge the U row accumulators, combine the G lanes, fold
+// the tail bytes, apply the short-buffer seed and store (lane 0).
+template <int G>
+__device__ __forceinline__ void finish(const Params &P, uint64_t b, const Geo &q, const uint32_t (&A)[U],
+                                       const uint4 &tail, uint32_t gl, const Lut &L) {
+    // X = W3(A0) ^ W2(A1) ^ W1(A2) ^ A3 = W2(W1(A0) ^ A1) ^ (W1(A2) ^ A3)
+    const uint32_t x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
+    const uint32_t x23 = lookup4<kRegionB>(A[2], L) ^ A[3];
+    uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+#pragma unroll
+    for (int k = 0; (1 << k) < G; ++k) {
+        const uint32_t other = __shfl_down(X, 1u << k, G);
+        X = comb_shift(X, k) ^ other;
+    }
+    const uint32_t alow = q.alow & 15u;
+    const uint32_t end = alow + q.len;
+    if (gl == 0 && ((end & 15u) != 0 || q.len < 4)) {
+        const uint32_t tb = end & ~15u;  // tail granule start, relative to abase
+        const uint32_t hi = end - tb;
+        const uint32_t lo = alow > tb ? alow - tb : 0u;
+        const uint32_t s0 = q.len >= 4 ? ~q.seed : 0u;
+        const uint32_t tw[4] = {tail.x, tail.y, tail.z, tail.w};
+        for (uint32_t i = lo; i < hi; ++i) {
+            uint32_t by = (tw[i >> 2] >> (8u * (i & 3u))) & 0xffu;
+            const uint32_t rel = tb + i - alow;
+            if (rel < 4) by ^= (s0 >> (8u * rel)) & 0xffu;
+            X = byte_step(X, by, L.c4);
+        }
+        if (q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for the unseeded short path
+            uint32_t s = ~q.seed;
+            for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u, L.c4);
+            X ^= s;
+        }
+    }
+    if (gl == 0) {
+        const uint32_t crc = ~X;
+        P.out[b] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+    }
+}
+
+// Per-group streaming state.  The load side runs exactly one batch ahead of
+// the fold side: batch j+1 of the current buffer, or batch 0 of the next
+// buffer when j is the last batch.
+template <int G>
+struct Stream {
+    Geo q, qn;        // current / next buffer
+    uint64_t b, bn;   // their indices
+    uint4 tail;       // tail granule of q (lane 0 only)
+    uint32_t A[U];
+    uint32_t j;
+    bool has_next;
+};
+
+template <int G, bool STRIDED>
+__device__ __forceinline__ bool stream_step(const Params &P, uint64_t gstride, uint32_t gl, const Lut &L,
+                                            Stream<G> &S, uint4 (&cur)[U], uint4 (&nxt)[U]) {
+    const bool last = S.j + 1 == S.q.nb;
+    if (!last)
+        load_batch<G>(S.q, S.j + 1, gl, nxt);
+    else if (S.has_next)
+        load_batch0<G>(S.qn, gl, nxt);
+    if (S.j == 0) {
+        fix_head<G>(S.q, 0, gl, cur);
+        fold_batch<true>(cur, S.A, L);
+        drop_pre_rows<G>(S.q, gl, S.A);
+    } else {
+        if (S.j == 1 && (S.q.alow & 16u)) fix_head<G>(S.q, 1, gl, cur);
+        fold_batch<false>(cur, S.A, L);
+    }
+    if (!last) {
+        ++S.j;
+        return false;
+    }
+    finish<G>(P, S.b, S.q, S.A, S.tail, gl, L);
+    if (!S.has_next) return true;
+    S.b = S.bn;
+    S.q = S.qn;
+    S.tail = load_tail(S.q, gl);  // needed only at this buffer's finish
+    S.bn += gstride;
+    S.has_next = S.bn < P.n;
+    if (S.has_next) S.qn = fetch_geo<G, STRIDED>(P, S.bn);
+    S.j = 0;
+    return false;
+}
+
+// One group streams buffers gid, gid + gstride, ...; the two register slots
+// alternate roles (ping-pong), so no batch is ever copied between registers.
+template <int G, bool STRIDED>
+__device__ __forceinline__ void group_stream(const Params &P, uint64_t gid, uint64_t gstride,
+                                             uint32_t gl, const Lut &L) {
+    if (gid >= P.n) return;
+    Stream<G> S;
+    S.b = gid;
+    S.q = fetch_geo<G, STRIDED>(P, S.b);
+    S.bn = gid + gstride;
+    S.has_next = S.bn < P.n;
+    if (S.has_next) S.qn = fetch_geo<G, STRIDED>(P, S.bn);
+    S.tail = load_tail(S.q, gl);
+    S.j = 0;
+    uint4 slot0[U], slot1[U];
+    load_batch0<G>(S.q, gl, slot0);
+    for (;;) {
+        if (stream_step<G, STRIDED>(P, gstride, gl, L, S, slot0, slot1)) break;
+        if (stream_step<G, STRIDED>(P, gstride, gl, L, S, slot1, slot0)) break;
+    }
+}
+
+// Copy the 152 KiB table image into LDS: every thread issues all of its
+// (<= 10) 16-B loads before the first LDS store, so the copy costs about one
+// L2 round trip rather than ten.
 __device__ __forceinline__ void stage_tables(const uint4 *__restrict__ image) {
+    constexpr int kVec = kImageWords / 4;
+    constexpr int kPer = (kVec + kThreads - 1) / kThreads;
     uint4 *l4 = reinterpret_cast<uint4 *>(g_lds);
-    for (int i = threadIdx.x; i < kImageWords / 4; i += kThreads) l4[i] = image[i];
+    g_u32x4 *src = reinterpret_cast<g_u32x4 *>(reinterpret_cast<uint64_t>(image));
+    u32x4 r[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = threadIdx.x + k * kThreads;
+        if (i < kVec) r[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = threadIdx.x + k * kThreads;
+        if (i < kVec) l4[i] = to_uint4(r[k]);
+    }
     __syncthreads();
 }
 
 template <int G, bool STRIDED>
-__global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off,
-    const uint32_t *__restrict__ len, uint64_t stride, uint32_t blen,
-    const uint32_t *__restrict__ seed, uint32_t *__restrict__ out, uint64_t n, uint32_t flags,
-    const uint4 *__restrict__ image) {
+__global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(Params P, const uint4 *__restrict__ image) {
     stage_tables(image);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const Lut L = make_lut(lane);
     constexpr uint32_t kGroups = 64 / G;
-    const uint32_t gl = lane % G;
-    const uint64_t gid =
-        (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * kGroups + lane / G;
+    const uint64_t gid = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * kGroups + lane / G;
     const uint64_t gstride = static_cast<uint64_t>(gridDim.x) * kWaves * kGroups;
-    const uint64_t base = reinterpret_cast<uint64_t>(arena);
-    for (uint64_t b = gid; b < n; b += gstride) {
-        uint64_t a;
-        uint32_t ln;
-        if constexpr (STRIDED) {
-            a = base + b * stride;
-            ln = blen;
-        } else {
-            a = base + off[b];
-            ln = len[b];
+    group_stream<G, STRIDED>(P, gid, gstride, lane % G, L);
+}
+
+// Uniform-block kernel (SSTable-style fixed-size blocks): block k is
+// base[k*stride, k*stride + blen) with base, stride 16-B aligned and blen a
+// multiple of 16*G*U, so every block is `nb` whole batches and every group
+// of a wave walks the same (block round, batch) sequence: the batch control
+// is wave-uniform (scalar), there is no head/tail work, and the seed enters
+// as lane 0's first word.
+template <int G>
+__device__ __forceinline__ void finish_block(const Params &P, uint64_t blk, const uint32_t (&A)[U],
+                                             uint32_t gl, const Lut &L) {
+    const uint32_t x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
+    const uint32_t x23 = lookup4<kRegionB>(A[2], L) ^ A[3];
+    uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+#pragma unroll
+    for (int k = 0; (1 << k) < G; ++k) {
+        const uint32_t other = __shfl_down(X, 1u << k, G);
+        X = comb_shift(X, k) ^ other;
+    }
+    if (gl == 0) {
+        const uint32_t crc = ~X;
+        P.out[blk] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint32_t nb,
+                                                                 const uint4 *__restrict__ image) {
+    stage_tables(image);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const Lut L = make_lut(lane);
+    constexpr uint32_t kGroups = 64 / G;
+    constexpr uint64_t kRow = 16ull * G;       // bytes between rows of a batch
+    constexpr uint64_t kBatch = kRow * U;      // bytes per batch
+    const uint32_t gl = lane % G;
+    uint64_t blk = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * kGroups + lane / G;
+    const uint64_t gstride = static_cast<uint64_t>(gridDim.x) * kWaves * kGroups;
+    // Rounds of blocks are wave-uniform: the wave runs while its first group
+    // has a block; groups past the end are masked.
+    const uint64_t wblk0 = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * kGroups;
+    if (wblk0 >= P.n) return;
+    const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
+    auto block_ptr = [&](uint64_t k) { return P.base + (k < P.n ? k : 0) * P.stride + 16u * gl; };
+    auto block_s0 = [&](uint64_t k) { return P.seed && k < P.n ? ~P.seed[k] : 0xffffffffu; };
+
+    uint64_t ptr = block_ptr(blk);
+    uint32_t s0 = block_s0(blk);
+    uint4 slot0[U], slot1[U];
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) slot0[i] = load16(ptr + kRow * i);
+    uint32_t A[U];
+
+    // one batch: fold `cur`, prefetch the next batch into `nxt`
+    auto step = [&](uint64_t r, uint32_t j, uint4(&cur)[U], uint4(&nxt)[U]) {
+        const bool lastj = j + 1 == nb;
+        const bool more = !lastj || r + 1 < rounds;
+        const uint64_t nptr = lastj ? block_ptr(blk + gstride) : ptr + kBatch;
+        if (more) {
+#pragma unroll
+            for (uint32_t i = 0; i < U; ++i) nxt[i] = load16(nptr + kRow * i);
         }
-        const uint32_t sd = seed ? seed[b] : 0u;
-        const uint32_t crc = crc_group<G>(a, ln, sd, gl, L);
-        if (gl == 0) out[b] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+        if (j == 0) {
+            if (gl == 0) cur[0].x ^= s0;
+            fold_batch<true>(cur, A, L);
+        } else {
+            fold_batch<false>(cur, A, L);
+        }
+        if (lastj) {
+            if (blk < P.n) finish_block<G>(P, blk, A, gl, L);
+            blk += gstride;
+            s0 = block_s0(blk);
+        }
+        ptr = nptr;
+    };
+
+    const uint64_t total = rounds * nb;  // batches this wave walks
+    uint64_t t = 0;
+    uint64_t r = 0;
+    uint32_t j = 0;
+    for (;;) {
+        step(r, j, slot0, slot1);
+        if (++t == total) break;
+        if (++j == nb) { j = 0; ++r; }
+        step(r, j, slot1, slot0);
+        if (++t == total) break;
+        if (++j == nb) { j = 0; ++r; }
     }
 }
 
@@ -315,7 +590,7 @@ int set_err(int code, const std::string &msg) {
 
 constexpr int kGs[4] = {1, 4, 16, 64};
 
-// Host copy of the LDS image for each G (index into kGs).
+// Host copy of the LDS image for each G (index into kGs); layout in lvk.
 const std::vector<uint32_t> &host_image(int gi) {
     static std::vector<uint32_t> images[4];
     static std::once_flag once;
@@ -324,20 +599,28 @@ const std::vector<uint32_t> &host_image(int gi) {
         lvgpu::slice_tables(T);
         for (int k = 0; k < 6; ++k) lvgpu::shift_tables(16ull << k, C[k]);
         for (int i = 0; i < 4; ++i) {
+            const uint64_t G = static_cast<uint64_t>(kGs[i]);
+            uint32_t W4[4][256], W1[4][256], W2[4][256];
+            lvgpu::shift_tables(16ull * G * lvk::U, W4);
+            lvgpu::shift_tables(16ull * G, W1);
+            lvgpu::shift_tables(32ull * G, W2);
             std::vector<uint32_t> &im = images[i];
             im.assign(lvk::kImageWords, 0u);
-            for (int k = 0; k < 6; ++k)
-                for (int j = 0; j < 4; ++j)
-                    for (int e = 0; e < 256; ++e) im[(k * 4 + j) * 256 + e] = C[k][j][e];
-            uint32_t W[4][256];
-            lvgpu::shift_tables(16ull * kGs[i], W);
+            uint32_t *ra = &im[lvk::kRegionA / 4], *rb = &im[lvk::kRegionB / 4];
             for (int e = 0; e < 256; ++e)
                 for (int c = 0; c < 8; ++c)
                     for (int k = 0; k < 4; ++k) {
-                        uint32_t *row = &im[lvk::kCombWords + e * 64];
-                        row[4 * c + k] = T[k][e];           // T_k indexed by state byte 3-k
-                        row[32 + 4 * c + k] = W[3 - k][e];  // W indexed the same way
+                        // slot k is indexed by state byte 3-k (make_lut), so shift
+                        // tables store their byte-(3-k) table there
+                        ra[e * 64 + 4 * c + k] = T[k][e];
+                        ra[e * 64 + 32 + 4 * c + k] = W4[3 - k][e];
+                        rb[e * 64 + 4 * c + k] = W1[3 - k][e];
+                        rb[e * 64 + 32 + 4 * c + k] = W2[3 - k][e];
                     }
+            uint32_t *rc = &im[lvk::kComb / 4];
+            for (int k = 0; k < 6; ++k)
+                for (int j = 0; j < 4; ++j)
+                    for (int e = 0; e < 256; ++e) rc[(k * 4 + j) * 256 + e] = C[k][j][e];
         }
     });
     return images[gi];
@@ -404,9 +687,18 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
     uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
     if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
     if (grid == 0) grid = 1;
+    lvk::Params P;
+    P.base = reinterpret_cast<uint64_t>(arena);
+    P.off = off;
+    P.len = len;
+    P.seed = seed;
+    P.out = out;
+    P.n = n;
+    P.stride = stride;
+    P.blen = blen;
+    P.flags = flags;
     hipLaunchKernelGGL((lvk::crc32c_batch_kernel<G, STRIDED>), dim3(static_cast<uint32_t>(grid)),
-                       dim3(lvk::kThreads), 0, s, arena, off, len, stride, blen, seed, out, n,
-                       flags, c.image[gi]);
+                       dim3(lvk::kThreads), 0, s, P, c.image[gi]);
 }
 
 template <bool STRIDED>
@@ -418,6 +710,49 @@ void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off
         case 1: launch_one<4, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
         case 2: launch_one<16, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
         default: launch_one<64, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
+    }
+}
+
+// Group size for the uniform-block kernel, or -1 when the blocks are not
+// 16-B aligned whole batches for any supported G.
+int pick_block_gi(uint64_t base, uint64_t stride, uint64_t blen, int forced) {
+    if (blen == 0 || base % 16 || stride % 16) return -1;
+    auto fits = [&](int gi) { return blen % (16ull * kGs[gi] * lvk::U) == 0; };
+    if (forced >= 0) return fits(forced) ? forced : -1;
+    for (int gi : {2, 1, 0})
+        if (fits(gi)) return gi;
+    return -1;
+}
+
+template <int G>
+void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, uint32_t blen,
+                     uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t s) {
+    const uint64_t groups_per_wg = static_cast<uint64_t>(lvk::kWaves) * (64 / G);
+    uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
+    if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
+    if (grid == 0) grid = 1;
+    lvk::Params P;
+    P.base = reinterpret_cast<uint64_t>(base);
+    P.off = nullptr;
+    P.len = nullptr;
+    P.seed = seed;
+    P.out = out;
+    P.n = n;
+    P.stride = stride;
+    P.blen = blen;
+    P.flags = flags;
+    const uint32_t nb = static_cast<uint32_t>(blen / (16ull * G * lvk::U));
+    hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G>), dim3(static_cast<uint32_t>(grid)),
+                       dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
+}
+
+void launch_blocks(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, uint32_t blen,
+                   uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t s) {
+    switch (gi) {
+        case 0: launch_blocks_g<1>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
+        case 1: launch_blocks_g<4>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
+        case 2: launch_blocks_g<16>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
+        default: launch_blocks_g<64>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
     }
 }
 
@@ -463,6 +798,13 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     const int gi = forced_gi(flags);
+    // Aligned whole-batch blocks take the uniform-block kernel.
+    const int bgi = pick_block_gi(reinterpret_cast<uint64_t>(d_base), stride, block_len, gi);
+    if (bgi >= 0) {
+        launch_blocks(*c, bgi, d_base, stride, block_len, n, d_seed, d_out, flags,
+                      static_cast<hipStream_t>(stream));
+        return check_launch();
+    }
     launch_g<true>(*c, gi >= 0 ? gi : pick_gi(block_len), d_base, nullptr, nullptr, stride, block_len, d_seed,
                    d_out, n, flags, static_cast<hipStream_t>(stream));
     return check_launch();

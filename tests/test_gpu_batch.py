@@ -212,3 +212,28 @@ def test_bad_arguments_raise(torch_dev):
         lvgpu.lib()  # loads fine
         rc = lvgpu.lib().lv_crc32c_batch_device(None, None, None, None, None, 5, 0, None)
         lvgpu._check(rc)
+
+
+@pytest.mark.parametrize("group", [None, 1, 4, 16])
+@pytest.mark.parametrize("block_len,stride_pad,n", [
+    (64, 0, 1), (64, 16, 4097), (256, 0, 3001), (256, 48, 777), (1024, 0, 1025), (1024, 32, 64),
+    (4096, 0, 262), (4096, 4096, 100), (8192, 16, 513), (65536, 0, 37), (1048576, 0, 3)])
+@pytest.mark.parametrize("seeded", [False, True])
+def test_uniform_block_kernel(torch_dev, group, block_len, stride_pad, n, seeded):
+    """Aligned whole-batch blocks take the uniform-block kernel (SSTable
+    blocks); ragged block counts leave partially filled waves."""
+    torch, dev = torch_dev
+    if group is not None and block_len % (64 * group):
+        pytest.skip("block not a whole batch for this group size")
+    stride = block_len + stride_pad
+    rng = np.random.default_rng(block_len * 7 + n)
+    total = stride * n
+    t = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(t, 0, 0xB10C + n)
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out = lvgpu.batch_strided(t, stride, block_len, n, seed=sd, masked=seeded, group=group)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy().tobytes()
+    want = oracle_batch(host, np.arange(n, dtype=np.uint64) * stride, np.full(n, block_len, np.uint32), seeds, seeded)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
