@@ -274,7 +274,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 payload generated in HBM)",
             "config": {"workload": desc, "buffers_per_gpu": n, "bytes_per_gpu": nbytes,
-                       "api": "lv_crc32c_batch_strided" if args.api == "strided" else "lv_crc32c_batch_device",
+                       "api": ("lv_crc32c_batch_strided" if args.api == "strided" and args.workload in ("c3", "c5")
+                               else "lv_crc32c_batch_device"),
                        "parallelism": f"dp{world} (independent shards, no collective)"},
             "hbm_peak_frac": round(value * 2**30 / world / 1e9 / HBM_PEAK_GBS, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

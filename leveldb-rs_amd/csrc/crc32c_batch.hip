@@ -65,7 +65,7 @@ __shared__ __attribute__((aligned(16))) uint32_t g_lds[kImageWords];
 // state byte that indexes table k_i to bits 8..15 (v_perm selector: 0-3 = S1
 // bytes, 4-7 = S0 bytes, 12 = 0x00).
 struct Lut {
-    uint32_t lv, sel0, sel1, sel2, sel3, c4;
+    uint32_t lv, sel0, sel1, sel2, sel3;
 };
 
 __device__ __forceinline__ Lut make_lut(uint32_t lane) {
@@ -83,7 +83,6 @@ __device__ __forceinline__ Lut make_lut(uint32_t lane) {
     L.sel1 = sel[1];
     L.sel2 = sel[2];
     L.sel3 = sel[3];
-    L.c4 = 4u * c;
     return L;
 }
 
@@ -175,7 +174,8 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 }
 
 // One byte through T0 (this lane's copy): crc32c.rs:81.
-__device__ __forceinline__ uint32_t byte_step(uint32_t s, uint32_t b, uint32_t c4) {
+__device__ __forceinline__ uint32_t byte_step(uint32_t s, uint32_t b) {
+    const uint32_t c4 = (__lane_id() & 7u) * 4u;
     const uint32_t e = (s ^ b) & 0xffu;
     return g_lds[e * 64u + c4] ^ (s >> 8);
 }
@@ -220,6 +220,8 @@ struct Params {
     uint64_t stride;
     uint32_t blen;
     uint32_t flags;
+    const uint32_t *idx;    // optional: logical i -> buffer idx[i] (sorted list)
+    const uint32_t *count;  // optional: {start, -, -, -, count} of this class's slice
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of
@@ -228,6 +230,7 @@ struct Params {
 // Granule index g is expressed relative to g0 = a >> 4: d = g - g0.
 struct Geo {
     uint64_t abase;  // a & ~15 (address of granule g0)
+    uint32_t bid;    // buffer index (output slot)
     uint32_t len;
     uint32_t seed;
     uint32_t nb;     // batches, >= 1
@@ -253,12 +256,16 @@ __device__ __forceinline__ Geo make_geo(uint64_t a, uint32_t len, uint32_t seed)
 }
 
 template <int G, bool STRIDED>
-__device__ __forceinline__ Geo fetch_geo(const Params &P, uint64_t b) {
+__device__ __forceinline__ Geo fetch_geo(const Params &P, uint64_t i) {
+    const uint64_t b = P.idx ? P.idx[i] : i;
+    Geo q;
     if constexpr (STRIDED) {
-        return make_geo<G>(P.base + b * P.stride, P.blen, P.seed ? P.seed[b] : 0u);
+        q = make_geo<G>(P.base + b * P.stride, P.blen, P.seed ? P.seed[b] : 0u);
     } else {
-        return make_geo<G>(P.base + P.off[b], P.len[b], P.seed ? P.seed[b] : 0u);
+        q = make_geo<G>(P.base + P.off[b], P.len[b], P.seed ? P.seed[b] : 0u);
     }
+    q.bid = static_cast<uint32_t>(b);
+    return q;
 }
 
 // Batch j >= 1: all rows lie inside the buffer.
@@ -321,7 +328,7 @@ __device__ __forceinline__ void drop_pre_rows(const Geo &q, uint32_t gl, uint32_
 // Finish a buffer: merge the U row accumulators, combine the G lanes, fold
 // the tail bytes, apply the short-buffer seed and store (lane 0).
 template <int G>
-__device__ __forceinline__ void finish(const Params &P, uint64_t b, const Geo &q, const uint32_t (&A)[U],
+__device__ __forceinline__ void finish(const Params &P, const Geo &q, const uint32_t (&A)[U],
                                        const uint4 &tail, uint32_t gl, const Lut &L) {
     // X = W3(A0) ^ W2(A1) ^ W1(A2) ^ A3 = W2(W1(A0) ^ A1) ^ (W1(A2) ^ A3)
     const uint32_t x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
@@ -344,17 +351,17 @@ __device__ __forceinline__ void finish(const Params &P, uint64_t b, const Geo &q
             uint32_t by = (tw[i >> 2] >> (8u * (i & 3u))) & 0xffu;
             const uint32_t rel = tb + i - alow;
             if (rel < 4) by ^= (s0 >> (8u * rel)) & 0xffu;
-            X = byte_step(X, by, L.c4);
+            X = byte_step(X, by);
         }
         if (q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for the unseeded short path
             uint32_t s = ~q.seed;
-            for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u, L.c4);
+            for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u);
             X ^= s;
         }
     }
     if (gl == 0) {
         const uint32_t crc = ~X;
-        P.out[b] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+        P.out[q.bid] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
     }
 }
 
@@ -363,65 +370,76 @@ __device__ __forceinline__ void finish(const Params &P, uint64_t b, const Geo &q
 // buffer when j is the last batch.
 template <int G>
 struct Stream {
-    Geo q, qn;        // current / next buffer
-    uint64_t b, bn;   // their indices
+    Geo q, qn;        // current / next buffer (qn valid iff b + gstride < n)
+    uint64_t b;       // logical index of q
     uint4 tail;       // tail granule of q (lane 0 only)
     uint32_t A[U];
     uint32_t j;
-    bool has_next;
 };
 
 template <int G, bool STRIDED>
 __device__ __forceinline__ bool stream_step(const Params &P, uint64_t gstride, uint32_t gl, const Lut &L,
                                             Stream<G> &S, uint4 (&cur)[U], uint4 (&nxt)[U]) {
     const bool last = S.j + 1 == S.q.nb;
+    const bool has_next = S.b + gstride < P.n;
     if (!last)
         load_batch<G>(S.q, S.j + 1, gl, nxt);
-    else if (S.has_next)
+    else if (has_next)
         load_batch0<G>(S.qn, gl, nxt);
-    if (S.j == 0) {
+    // One fold variant for every batch (accumulators start at 0 and
+    // Shift(0) = 0), so groups of a wave at different batch indices never
+    // run two fold bodies; only the light head fix-up is divergent.
+    if (S.j == 0)
         fix_head<G>(S.q, 0, gl, cur);
-        fold_batch<true>(cur, S.A, L);
-        drop_pre_rows<G>(S.q, gl, S.A);
-    } else {
-        if (S.j == 1 && (S.q.alow & 16u)) fix_head<G>(S.q, 1, gl, cur);
-        fold_batch<false>(cur, S.A, L);
-    }
+    else if (S.j == 1 && (S.q.alow & 16u))
+        fix_head<G>(S.q, 1, gl, cur);
+    fold_batch<false>(cur, S.A, L);
+    if (S.j == 0) drop_pre_rows<G>(S.q, gl, S.A);
     if (!last) {
         ++S.j;
         return false;
     }
-    finish<G>(P, S.b, S.q, S.A, S.tail, gl, L);
-    if (!S.has_next) return true;
-    S.b = S.bn;
+    finish<G>(P, S.q, S.A, S.tail, gl, L);
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) S.A[i] = 0u;
+    if (!has_next) return true;
+    S.b += gstride;
     S.q = S.qn;
     S.tail = load_tail(S.q, gl);  // needed only at this buffer's finish
-    S.bn += gstride;
-    S.has_next = S.bn < P.n;
-    if (S.has_next) S.qn = fetch_geo<G, STRIDED>(P, S.bn);
+    if (S.b + gstride < P.n) S.qn = fetch_geo<G, STRIDED>(P, S.b + gstride);
     S.j = 0;
     return false;
 }
 
-// One group streams buffers gid, gid + gstride, ...; the two register slots
-// alternate roles (ping-pong), so no batch is ever copied between registers.
+// One group streams buffers gid, gid + gstride, ...  The loop shape is the
+// one that fits 128 VGPRs (16 waves/CU) without spills for each G: a
+// ping-pong of two register slots for G = 1, a copy of the prefetched batch
+// (16 moves) for G > 1, where the doubled inlined fold of a ping-pong spills.
 template <int G, bool STRIDED>
 __device__ __forceinline__ void group_stream(const Params &P, uint64_t gid, uint64_t gstride,
                                              uint32_t gl, const Lut &L) {
     if (gid >= P.n) return;
     Stream<G> S;
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) S.A[i] = 0u;
     S.b = gid;
     S.q = fetch_geo<G, STRIDED>(P, S.b);
-    S.bn = gid + gstride;
-    S.has_next = S.bn < P.n;
-    if (S.has_next) S.qn = fetch_geo<G, STRIDED>(P, S.bn);
+    if (gid + gstride < P.n) S.qn = fetch_geo<G, STRIDED>(P, gid + gstride);
     S.tail = load_tail(S.q, gl);
     S.j = 0;
-    uint4 slot0[U], slot1[U];
-    load_batch0<G>(S.q, gl, slot0);
-    for (;;) {
-        if (stream_step<G, STRIDED>(P, gstride, gl, L, S, slot0, slot1)) break;
-        if (stream_step<G, STRIDED>(P, gstride, gl, L, S, slot1, slot0)) break;
+    uint4 cur[U], nxt[U];
+    load_batch0<G>(S.q, gl, cur);
+    if constexpr (G == 1) {  // ping-pong: slots swap roles, no copies
+        for (;;) {
+            if (stream_step<G, STRIDED>(P, gstride, gl, L, S, cur, nxt)) break;
+            if (stream_step<G, STRIDED>(P, gstride, gl, L, S, nxt, cur)) break;
+        }
+    } else {
+        for (;;) {
+            if (stream_step<G, STRIDED>(P, gstride, gl, L, S, cur, nxt)) break;
+#pragma unroll
+            for (uint32_t i = 0; i < U; ++i) cur[i] = nxt[i];
+        }
     }
 }
 
@@ -449,6 +467,12 @@ __device__ __forceinline__ void stage_tables(const uint4 *__restrict__ image) {
 
 template <int G, bool STRIDED>
 __global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(Params P, const uint4 *__restrict__ image) {
+    if (P.count) {  // class slice of the sorted list: count[0] = start, count[4] = size
+        P.idx += P.count[0];
+        P.n = P.count[4];
+    }
+    // Workgroups without work leave before staging the tables (empty classes).
+    if (static_cast<uint64_t>(blockIdx.x) * kWaves * (64 / G) >= P.n) return;
     stage_tables(image);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
@@ -547,6 +571,85 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     }
 }
 
+// Length classes of the offsets API.  Buffers are counting-sorted by key =
+// (class, batches descending): each class runs with the group size that keeps
+// ~1-32 batches per buffer, and consecutive list entries -- the groups of one
+// wave -- have the same batch count, so they finish buffers in lockstep.
+constexpr uint32_t kBuckets = 64;                 // batch-count buckets per class
+constexpr uint32_t kKeys = 4 * kBuckets;
+constexpr uint32_t kSortThreads = 256;
+
+__device__ __forceinline__ uint32_t len_class(uint32_t len) {
+    return len <= 256u ? 0u : len <= 2048u ? 1u : len <= 32768u ? 2u : 3u;
+}
+
+__device__ __forceinline__ uint32_t sort_key(uint32_t len) {
+    const uint32_t c = len_class(len);
+    const uint32_t gu16 = 16u * U * (c == 0 ? 1u : c == 1 ? 4u : c == 2 ? 16u : 64u);
+    uint32_t nb = (len + gu16 - 1) / gu16;  // batches, ignoring start alignment
+    nb = nb < kBuckets - 1 ? nb : kBuckets - 1;
+    return c * kBuckets + (kBuckets - 1 - nb);
+}
+
+// Pass 1: per-workgroup LDS histogram over a contiguous chunk, one global
+// atomic per nonzero bin per workgroup.
+__global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__restrict__ len, uint64_t n,
+                                                          uint64_t chunk, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[kKeys];
+    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads) h[k] = 0;
+    __syncthreads();
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kSortThreads) atomicAdd(&h[sort_key(len[i])], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+
+// Pass 2 (one workgroup): exclusive scan of the key histogram into per-key
+// cursors, plus each class's [start, count) for the class launches.
+__global__ __launch_bounds__(kKeys) void sort_scan(uint32_t *__restrict__ hist, uint32_t *__restrict__ cls) {
+    __shared__ uint32_t v[kKeys];
+    const uint32_t t = threadIdx.x;
+    v[t] = hist[t];
+    __syncthreads();
+    for (uint32_t d = 1; d < kKeys; d <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t x = t >= d ? v[t - d] : 0u;
+        __syncthreads();
+        v[t] += x;
+        __syncthreads();
+    }
+    const uint32_t excl = v[t] - hist[t];
+    hist[t] = excl;  // becomes the global cursor of key t
+    if (t % kBuckets == 0) {
+        const uint32_t c = t / kBuckets;
+        cls[c] = excl;                                     // start
+        cls[4 + c] = v[t + kBuckets - 1] - excl;           // count
+    }
+}
+
+// Pass 3: same chunks as pass 1; each workgroup reserves its bins' ranges
+// with one atomic per bin, then places its buffers by LDS-atomic rank.
+__global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint32_t *__restrict__ len, uint64_t n,
+                                                             uint64_t chunk, uint32_t *__restrict__ cursor,
+                                                             uint32_t *__restrict__ list) {
+    __shared__ uint32_t h[kKeys];
+    __shared__ uint32_t base[kKeys];
+    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads) h[k] = 0;
+    __syncthreads();
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kSortThreads) atomicAdd(&h[sort_key(len[i])], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads) {
+        base[k] = h[k] ? atomicAdd(&cursor[k], h[k]) : 0u;
+        h[k] = 0;
+    }
+    __syncthreads();
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kSortThreads) {
+        const uint32_t k = sort_key(len[i]);
+        list[base[k] + atomicAdd(&h[k], 1u)] = static_cast<uint32_t>(i);
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -638,6 +741,9 @@ struct DevCtx {
     size_t d_meta_cap = 0;
     uint8_t *h_pinned = nullptr;
     size_t h_pinned_cap = 0;
+    // offsets-API workspace: 4 class counts + 4 index lists of n entries
+    uint8_t *ws = nullptr;
+    size_t ws_cap = 0;
     hipStream_t stream = nullptr;
 };
 
@@ -682,7 +788,8 @@ int forced_gi(uint32_t flags) {
 template <int G, bool STRIDED>
 void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off,
                 const uint32_t *len, uint64_t stride, uint32_t blen, const uint32_t *seed,
-                uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
+                uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s,
+                const uint32_t *idx = nullptr, const uint32_t *count = nullptr) {
     const uint64_t groups_per_wg = static_cast<uint64_t>(lvk::kWaves) * (64 / G);
     uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
     if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
@@ -697,6 +804,8 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
     P.stride = stride;
     P.blen = blen;
     P.flags = flags;
+    P.idx = idx;
+    P.count = count;
     hipLaunchKernelGGL((lvk::crc32c_batch_kernel<G, STRIDED>), dim3(static_cast<uint32_t>(grid)),
                        dim3(lvk::kThreads), 0, s, P, c.image[gi]);
 }
@@ -704,13 +813,50 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
 template <bool STRIDED>
 void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off,
               const uint32_t *len, uint64_t stride, uint32_t blen, const uint32_t *seed,
-              uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
+              uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s,
+              const uint32_t *idx = nullptr, const uint32_t *count = nullptr) {
     switch (gi) {
-        case 0: launch_one<1, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
-        case 1: launch_one<4, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
-        case 2: launch_one<16, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
-        default: launch_one<64, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
+        case 0: launch_one<1, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
+        case 1: launch_one<4, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
+        case 2: launch_one<16, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
+        default: launch_one<64, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
     }
+}
+
+// Length-sorted launch of the offsets API: histogram, scan and scatter over
+// len[] (one sorted index list), then one launch per class reading its slice
+// of the list and its count from device memory (no host sync).
+int launch_binned(DevCtx &c, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
+    const size_t meta = (lvk::kKeys + 8) * sizeof(uint32_t);
+    {
+        std::lock_guard<std::mutex> lk(c.m);
+        const size_t need = meta + n * sizeof(uint32_t);
+        if (c.ws_cap < need) {
+            if (c.ws) LV_HIP(hipFree(c.ws));
+            c.ws = nullptr;
+            c.ws_cap = 0;
+            LV_HIP(hipMalloc(&c.ws, need));
+            c.ws_cap = need;
+        }
+    }
+    uint32_t *hist = reinterpret_cast<uint32_t *>(c.ws);
+    uint32_t *cls = hist + lvk::kKeys;  // [start x4, count x4]
+    uint32_t *list = cls + 8;
+    LV_HIP(hipMemsetAsync(hist, 0, lvk::kKeys * sizeof(uint32_t), s));
+    uint64_t wgs = (n + 4095) / 4096;  // ~4096 buffers per sorting workgroup
+    if (wgs > 2048) wgs = 2048;
+    const uint64_t chunk = (n + wgs - 1) / wgs;
+    hipLaunchKernelGGL(lvk::sort_hist, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, len, n,
+                       chunk, hist);
+    hipLaunchKernelGGL(lvk::sort_scan, dim3(1), dim3(lvk::kKeys), 0, s, hist, cls);
+    hipLaunchKernelGGL(lvk::sort_scatter, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, len, n,
+                       chunk, hist, list);
+    // class k's slice starts at cls[k] (device memory): pass the list base and
+    // let the kernel add the start (ClassList indirection below).
+    for (int k = 0; k < 4; ++k)
+        launch_g<false>(c, k, arena, off, len, 0, 0, seed, out, n, flags, s, list, cls + k);
+    return 0;
 }
 
 // Group size for the uniform-block kernel, or -1 when the blocks are not
@@ -785,8 +931,12 @@ int lv_crc32c_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const 
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     const int gi = forced_gi(flags);
-    launch_g<false>(*c, gi >= 0 ? gi : 2, d_arena, d_off, d_len, 0, 0, d_seed, d_out, n, flags,
-                    static_cast<hipStream_t>(stream));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (gi >= 0) {
+        launch_g<false>(*c, gi, d_arena, d_off, d_len, 0, 0, d_seed, d_out, n, flags, s);
+    } else if (int rc = launch_binned(*c, d_arena, d_off, d_len, d_seed, d_out, n, flags, s)) {
+        return rc;
+    }
     return check_launch();
 }
 
@@ -862,7 +1012,7 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     std::memcpy(c->h_pinned, h_arena, arena_bytes);
     LV_HIP(hipMemcpyAsync(c->d_arena, c->h_pinned, arena_bytes, hipMemcpyHostToDevice, s));
     launch_g<false>(*c, 2, c->d_arena, d_off, d_len, 0, 0, h_seed ? d_seed : nullptr, d_out, n,
-                    flags, s);
+                    flags, s);  // host path: G = 16 (binning would need the shared workspace lock)
     if (int rc = check_launch()) return rc;
     LV_HIP(hipMemcpyAsync(c->h_pinned, d_out, n * 4, hipMemcpyDeviceToHost, s));
     LV_HIP(hipStreamSynchronize(s));
