@@ -67,6 +67,15 @@ int lv_crc32c_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const 
                            const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
                            void *stream);
 
+/* Same as lv_crc32c_batch_device with a caller-owned device workspace of at
+ * least lv_crc32c_workspace_bytes(n) bytes (the per-call length sort).  Use it
+ * for stream capture into a HIP graph, or to run concurrent calls on several
+ * streams without the library's per-stream workspace. */
+size_t lv_crc32c_workspace_bytes(size_t n);
+int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                              const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
+                              void *d_workspace, size_t workspace_bytes, void *stream);
+
 /* Fixed-stride form for table blocks: buffer i is
  * d_base[i*stride .. i*stride + block_len).  Same semantics as above. */
 int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t block_len, size_t n,

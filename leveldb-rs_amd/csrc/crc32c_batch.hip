@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -730,20 +731,22 @@ const std::vector<uint32_t> &host_image(int gi) {
 }
 
 struct DevCtx {
-    std::mutex m;
+    std::mutex m;  // one-time init
     bool ready = false;
     int cus = 0;
     uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
-    // host-path staging (grown on demand)
+    // offsets-API sort workspace, one per stream (calls on one stream are
+    // stream-ordered, so reusing its buffer is safe; different streams never share)
+    std::mutex ws_m;
+    std::map<hipStream_t, std::pair<uint8_t *, size_t>> ws;
+    // host-path staging (grown on demand), serialised by host_m
+    std::mutex host_m;
     uint8_t *d_arena = nullptr;
     size_t d_arena_cap = 0;
     uint8_t *d_meta = nullptr;
     size_t d_meta_cap = 0;
     uint8_t *h_pinned = nullptr;
     size_t h_pinned_cap = 0;
-    // offsets-API workspace: 4 class counts + 4 index lists of n entries
-    uint8_t *ws = nullptr;
-    size_t ws_cap = 0;
     hipStream_t stream = nullptr;
 };
 
@@ -823,24 +826,31 @@ void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off
     }
 }
 
+// Bytes of sort workspace the offsets API needs for n buffers.
+size_t sort_ws_bytes(uint64_t n) { return (lvk::kKeys + 8) * sizeof(uint32_t) + n * sizeof(uint32_t); }
+
+// The library-owned workspace of (device, stream), grown on demand.
+int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out) {
+    std::lock_guard<std::mutex> lk(c.ws_m);
+    auto &w = c.ws[s];
+    const size_t need = sort_ws_bytes(n);
+    if (w.second < need) {
+        if (w.first) LV_HIP(hipFree(w.first));
+        w.first = nullptr;
+        w.second = 0;
+        LV_HIP(hipMalloc(&w.first, need));
+        w.second = need;
+    }
+    *out = w.first;
+    return 0;
+}
+
 // Length-sorted launch of the offsets API: histogram, scan and scatter over
 // len[] (one sorted index list), then one launch per class reading its slice
 // of the list and its count from device memory (no host sync).
-int launch_binned(DevCtx &c, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+int launch_binned(DevCtx &c, uint8_t *ws, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                   const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
-    const size_t meta = (lvk::kKeys + 8) * sizeof(uint32_t);
-    {
-        std::lock_guard<std::mutex> lk(c.m);
-        const size_t need = meta + n * sizeof(uint32_t);
-        if (c.ws_cap < need) {
-            if (c.ws) LV_HIP(hipFree(c.ws));
-            c.ws = nullptr;
-            c.ws_cap = 0;
-            LV_HIP(hipMalloc(&c.ws, need));
-            c.ws_cap = need;
-        }
-    }
-    uint32_t *hist = reinterpret_cast<uint32_t *>(c.ws);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(ws);
     uint32_t *cls = hist + lvk::kKeys;  // [start x4, count x4]
     uint32_t *list = cls + 8;
     LV_HIP(hipMemsetAsync(hist, 0, lvk::kKeys * sizeof(uint32_t), s));
@@ -852,8 +862,6 @@ int launch_binned(DevCtx &c, const uint8_t *arena, const uint64_t *off, const ui
     hipLaunchKernelGGL(lvk::sort_scan, dim3(1), dim3(lvk::kKeys), 0, s, hist, cls);
     hipLaunchKernelGGL(lvk::sort_scatter, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, len, n,
                        chunk, hist, list);
-    // class k's slice starts at cls[k] (device memory): pass the list base and
-    // let the kernel add the start (ClassList indirection below).
     for (int k = 0; k < 4; ++k)
         launch_g<false>(c, k, arena, off, len, 0, 0, seed, out, n, flags, s, list, cls + k);
     return 0;
@@ -922,22 +930,44 @@ int lv_device_init(void) {
     return current_ctx(&c);
 }
 
-int lv_crc32c_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
-                           const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
-                           void *stream) {
+static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                             const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
+                             void *stream, uint8_t *d_ws, size_t ws_bytes) {
     g_err.clear();
     if (n == 0) return LV_OK;
     if (!d_arena || !d_off || !d_len || !d_out) return set_err(LV_ERR_INVALID, "null device pointer");
+    if (n > 0xffffffffull) return set_err(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     const int gi = forced_gi(flags);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (gi >= 0) {
         launch_g<false>(*c, gi, d_arena, d_off, d_len, 0, 0, d_seed, d_out, n, flags, s);
-    } else if (int rc = launch_binned(*c, d_arena, d_off, d_len, d_seed, d_out, n, flags, s)) {
+        return check_launch();
+    }
+    if (d_ws) {
+        if (ws_bytes < sort_ws_bytes(n)) return set_err(LV_ERR_INVALID, "workspace too small");
+    } else if (int rc = stream_ws(*c, s, n, &d_ws)) {
         return rc;
     }
+    if (int rc = launch_binned(*c, d_ws, d_arena, d_off, d_len, d_seed, d_out, n, flags, s)) return rc;
     return check_launch();
+}
+
+int lv_crc32c_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                           const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
+                           void *stream) {
+    return batch_device_impl(d_arena, d_off, d_len, d_seed, d_out, n, flags, stream, nullptr, 0);
+}
+
+size_t lv_crc32c_workspace_bytes(size_t n) { return sort_ws_bytes(n); }
+
+int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                              const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
+                              void *d_workspace, size_t workspace_bytes, void *stream) {
+    if (!d_workspace) return set_err(LV_ERR_INVALID, "null workspace");
+    return batch_device_impl(d_arena, d_off, d_len, d_seed, d_out, n, flags, stream,
+                             static_cast<uint8_t *>(d_workspace), workspace_bytes);
 }
 
 int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t block_len, size_t n,
@@ -972,7 +1002,7 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     LV_HIP(hipSetDevice(device));
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
-    std::lock_guard<std::mutex> lk(c->m);
+    std::lock_guard<std::mutex> lk(c->host_m);
     if (!c->stream) LV_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     const size_t meta = n * (8 + 4 + 4 + 4);
     const size_t need_dev = arena_bytes + 16;
@@ -1011,8 +1041,10 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     LV_HIP(hipStreamSynchronize(s));
     std::memcpy(c->h_pinned, h_arena, arena_bytes);
     LV_HIP(hipMemcpyAsync(c->d_arena, c->h_pinned, arena_bytes, hipMemcpyHostToDevice, s));
-    launch_g<false>(*c, 2, c->d_arena, d_off, d_len, 0, 0, h_seed ? d_seed : nullptr, d_out, n,
-                    flags, s);  // host path: G = 16 (binning would need the shared workspace lock)
+    uint8_t *ws = nullptr;
+    if (int rc = stream_ws(*c, s, n, &ws)) return rc;
+    if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s))
+        return rc;
     if (int rc = check_launch()) return rc;
     LV_HIP(hipMemcpyAsync(c->h_pinned, d_out, n * 4, hipMemcpyDeviceToHost, s));
     LV_HIP(hipStreamSynchronize(s));

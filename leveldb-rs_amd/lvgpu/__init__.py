@@ -56,6 +56,10 @@ def lib() -> ctypes.CDLL:
         getattr(L, f).argtypes = [u32]
     L.lv_crc32c_batch_device.restype = ctypes.c_int
     L.lv_crc32c_batch_device.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp]
+    L.lv_crc32c_workspace_bytes.restype = sz
+    L.lv_crc32c_workspace_bytes.argtypes = [sz]
+    L.lv_crc32c_batch_device_ws.restype = ctypes.c_int
+    L.lv_crc32c_batch_device_ws.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, sz, vp]
     L.lv_crc32c_batch_strided.restype = ctypes.c_int
     L.lv_crc32c_batch_strided.argtypes = [vp, u64, u32, sz, vp, vp, u32, vp]
     L.lv_crc32c_batch_host.restype = ctypes.c_int
@@ -162,6 +166,25 @@ def batch(arena, off, length, seed=None, out=None, masked=False, stream=None, gr
     _check(lib().lv_crc32c_batch_device(
         _dev_ptr(arena, "arena"), _dev_ptr(off, "off"), _dev_ptr(length, "length"),
         _dev_ptr(seed, "seed"), _dev_ptr(out, "out"), n, _flags(masked, group), _stream_ptr(stream)))
+    return out
+
+
+def workspace_bytes(n: int) -> int:
+    """Device workspace lv_crc32c_batch_device_ws needs for n buffers."""
+    return int(lib().lv_crc32c_workspace_bytes(n))
+
+
+def batch_ws(arena, off, length, workspace, seed=None, out=None, masked=False, stream=None):
+    """`batch` with a caller-owned uint8 device workspace (graph capture,
+    concurrent streams)."""
+    torch = _torch()
+    n = off.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=arena.device)
+    _check(lib().lv_crc32c_batch_device_ws(
+        _dev_ptr(arena, "arena"), _dev_ptr(off, "off"), _dev_ptr(length, "length"),
+        _dev_ptr(seed, "seed"), _dev_ptr(out, "out"), n, _flags(masked, None),
+        _dev_ptr(workspace, "workspace"), workspace.numel(), _stream_ptr(stream)))
     return out
 
 

@@ -237,3 +237,44 @@ def test_uniform_block_kernel(torch_dev, group, block_len, stride_pad, n, seeded
     host = t.cpu().numpy().tobytes()
     want = oracle_batch(host, np.arange(n, dtype=np.uint64) * stride, np.full(n, block_len, np.uint32), seeds, seeded)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+def test_all_length_classes_one_batch(torch_dev):
+    """One offsets-API call spanning every length class (<=256 B, <=2 KiB,
+    <=32 KiB, >32 KiB up to 300 KiB), shuffled, misaligned, seeded: exercises
+    the length sort and all four class launches together."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(44)
+    lens = np.concatenate([rng.integers(0, 257, 3000), rng.integers(257, 2049, 1500),
+                           rng.integers(2049, 32769, 600), rng.integers(32769, 300000, 40)]).astype(np.uint32)
+    rng.shuffle(lens)
+    gaps = rng.integers(0, 40, lens.size).astype(np.uint64)
+    offs = np.zeros(lens.size, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    total = int(offs[-1] + lens[-1]) + 16
+    t = torch.empty(total, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(t, 0, 0x5EED)
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    host = t.cpu().numpy().tobytes()
+    want = oracle_batch(host, offs, lens, seeds, True)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    got = lvgpu.batch(t, o, ln, sd, masked=True).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    # caller-owned workspace gives the same answer
+    ws = torch.empty(lvgpu.workspace_bytes(lens.size), dtype=torch.uint8, device=dev)
+    got2 = lvgpu.batch_ws(t, o, ln, ws, sd, masked=True).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got2, want)
+    # single buffer, and two streams back to back (per-stream workspaces)
+    one = lvgpu.batch(t, o[:1], ln[:1], sd[:1], masked=True).cpu().numpy().view(np.uint32)
+    assert one[0] == want[0]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s1):
+        r1 = lvgpu.batch(t, o, ln, sd, masked=True, stream=s1)
+    with torch.cuda.stream(s2):
+        r2 = lvgpu.batch(t, torch.flip(o, [0]), torch.flip(ln, [0]), torch.flip(sd, [0]), masked=True,
+                         stream=s2)
+    torch.cuda.synchronize()
+    assert np.array_equal(r1.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(r2.cpu().numpy().view(np.uint32), want[::-1])
