@@ -48,6 +48,8 @@ def parse():
                    help="force the kernel's lanes-per-buffer group size (tuning)")
     p.add_argument("--blocks", type=int, default=None, help="override the c3/c5 block count (diagnostics)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--e2e", action="store_true",
+                   help="time the host-memory path lv_crc32c_batch_host (pageable and pinned input) on C3")
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
                    help="auto: measure roofline.traffic in a child rocprofv3 --pmc FETCH_SIZE pass")
     return p.parse_args()
@@ -196,8 +198,45 @@ def cpu_baseline(torch, arena, nbytes_block, seconds):
                       f"crc32c.rs:86-118, 1 thread"}, crcs
 
 
+def e2e(args):
+    """End-to-end rate of the host-memory path (the reference's data lives in
+    host file buffers): H2D of the 1 GiB C3 arena + kernel + D2H of the CRCs,
+    synchronous per call.  Pageable input goes through the pipelined pinned
+    staging; pinned input is DMA'd directly."""
+    import numpy as np
+    import torch
+    import lvgpu
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    n, bl = (args.blocks or 262144), 4096
+    host = np.empty(n * bl, dtype=np.uint8)
+    W.lib().oracle_fill_splitmix(host.ctypes.data, 0, host.size, PAYLOAD_SEED)
+    off = np.arange(n, dtype=np.uint64) * bl
+    ln = np.full(n, bl, dtype=np.uint32)
+    pinned = torch.empty(host.size, dtype=torch.uint8, pin_memory=True)
+    pinned.numpy()[:] = host
+    res = {}
+    for name, arr in (("pageable", host), ("pinned", pinned.numpy())):
+        lvgpu.batch_host(arr, off, ln)  # warm: allocations, staging
+        ts = []
+        for _ in range(max(3, args.steps // 20)):
+            t0 = time.perf_counter()
+            out = lvgpu.batch_host(arr, off, ln)
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        med = ts[len(ts) // 2]
+        res[name] = {"GiB_per_s": round(n * bl / 2**30 / med, 2), "ms": round(med * 1e3, 2)}
+        want = np.zeros(1024, dtype=np.uint32)
+        W.lib().oracle_batch(host.ctypes.data, off.ctypes.data, ln.ctypes.data, None, want.ctypes.data, 1024, 0)
+        assert (out[:1024] == want).all(), "e2e parity check failed"
+    print(json.dumps({"metric": "end-to-end host-memory batched CRC32C (H2D + kernel + D2H), C3 1 GiB",
+                      "unit": "GiB/s", "results": res, "blocks": n, "block_bytes": bl}), flush=True)
+
+
 def main():
     args = parse()
+    if args.e2e:
+        return e2e(args)
     import torch
     import lvgpu
 

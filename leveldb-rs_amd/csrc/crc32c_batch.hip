@@ -36,6 +36,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -745,10 +746,65 @@ struct DevCtx {
     size_t d_arena_cap = 0;
     uint8_t *d_meta = nullptr;
     size_t d_meta_cap = 0;
-    uint8_t *h_pinned = nullptr;
-    size_t h_pinned_cap = 0;
+    uint8_t *h_meta = nullptr;
+    size_t h_meta_cap = 0;
+    uint8_t *h_stage[2] = {nullptr, nullptr};
+    size_t h_stage_cap[2] = {0, 0};
+    hipEvent_t ev[2] = {nullptr, nullptr};
     hipStream_t stream = nullptr;
 };
+
+constexpr size_t kStageBytes = 64ull << 20;  // pinned staging slot for pageable input
+
+int grow_dev(uint8_t **p, size_t *cap, size_t need) {
+    if (*cap >= need) return 0;
+    if (*p) LV_HIP(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    LV_HIP(hipMalloc(p, need));
+    *cap = need;
+    return 0;
+}
+
+int grow_pinned(uint8_t **p, size_t *cap, size_t need) {
+    if (*cap >= need) return 0;
+    if (*p) LV_HIP(hipHostFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    LV_HIP(hipHostMalloc(p, need, hipHostMallocDefault));
+    *cap = need;
+    return 0;
+}
+
+// True if p is page-locked host memory (hipHostMalloc / hipHostRegister).
+bool is_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error; clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// memcpy split over up to 8 host threads (pageable -> pinned staging).
+void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes) {
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt == 0 ? 1 : (nt > 8 ? 8 : nt);
+    if (bytes < (4u << 20) || nt == 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (bytes + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; ++t) {
+        const size_t lo = t * per;
+        if (lo >= bytes) break;
+        const size_t len = bytes - lo < per ? bytes - lo : per;
+        th.emplace_back([=] { std::memcpy(dst + lo, src + lo, len); });
+    }
+    for (auto &x : th) x.join();
+}
 
 DevCtx g_dev[64];
 
@@ -996,6 +1052,7 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     g_err.clear();
     if (n == 0) return LV_OK;
     if (!h_arena || !h_off || !h_len || !h_out) return set_err(LV_ERR_INVALID, "null host pointer");
+    if (n > 0xffffffffull) return set_err(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     for (size_t i = 0; i < n; ++i)
         if (h_off[i] > arena_bytes || h_len[i] > arena_bytes - h_off[i])
             return set_err(LV_ERR_INVALID, "buffer outside arena");
@@ -1004,51 +1061,50 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     if (int rc = current_ctx(&c)) return rc;
     std::lock_guard<std::mutex> lk(c->host_m);
     if (!c->stream) LV_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto &ev : c->ev)
+        if (!ev) LV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipStream_t s = c->stream;
     const size_t meta = n * (8 + 4 + 4 + 4);
-    const size_t need_dev = arena_bytes + 16;
-    if (c->d_arena_cap < need_dev) {
-        if (c->d_arena) LV_HIP(hipFree(c->d_arena));
-        c->d_arena = nullptr;
-        c->d_arena_cap = 0;
-        LV_HIP(hipMalloc(&c->d_arena, need_dev));
-        c->d_arena_cap = need_dev;
-    }
-    if (c->d_meta_cap < meta) {
-        if (c->d_meta) LV_HIP(hipFree(c->d_meta));
-        c->d_meta = nullptr;
-        c->d_meta_cap = 0;
-        LV_HIP(hipMalloc(&c->d_meta, meta));
-        c->d_meta_cap = meta;
-    }
-    const size_t need_pin = arena_bytes > meta ? arena_bytes : meta;
-    if (c->h_pinned_cap < need_pin) {
-        if (c->h_pinned) LV_HIP(hipHostFree(c->h_pinned));
-        c->h_pinned = nullptr;
-        c->h_pinned_cap = 0;
-        LV_HIP(hipHostMalloc(&c->h_pinned, need_pin, hipHostMallocDefault));
-        c->h_pinned_cap = need_pin;
-    }
+    if (int rc = grow_dev(&c->d_arena, &c->d_arena_cap, arena_bytes + 16)) return rc;
+    if (int rc = grow_dev(&c->d_meta, &c->d_meta_cap, meta)) return rc;
+    if (int rc = grow_pinned(&c->h_meta, &c->h_meta_cap, meta)) return rc;
     uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_meta);
     uint32_t *d_len = reinterpret_cast<uint32_t *>(d_off + n);
     uint32_t *d_seed = d_len + n;
     uint32_t *d_out = d_seed + n;
-    hipStream_t s = c->stream;
-    // metadata via pinned staging, then the payload
-    std::memcpy(c->h_pinned, h_off, n * 8);
-    std::memcpy(c->h_pinned + n * 8, h_len, n * 4);
-    if (h_seed) std::memcpy(c->h_pinned + n * 12, h_seed, n * 4);
-    LV_HIP(hipMemcpyAsync(d_off, c->h_pinned, n * (h_seed ? 16 : 12), hipMemcpyHostToDevice, s));
-    LV_HIP(hipStreamSynchronize(s));
-    std::memcpy(c->h_pinned, h_arena, arena_bytes);
-    LV_HIP(hipMemcpyAsync(c->d_arena, c->h_pinned, arena_bytes, hipMemcpyHostToDevice, s));
+
+    // metadata: one pinned staging copy, async
+    std::memcpy(c->h_meta, h_off, n * 8);
+    std::memcpy(c->h_meta + n * 8, h_len, n * 4);
+    if (h_seed) std::memcpy(c->h_meta + n * 12, h_seed, n * 4);
+    LV_HIP(hipMemcpyAsync(d_off, c->h_meta, n * (h_seed ? 16 : 12), hipMemcpyHostToDevice, s));
+
+    // payload: DMA straight from pinned/registered memory; otherwise a
+    // two-slot pipeline (parallel memcpy into one pinned slot while the other
+    // slot's H2D runs)
+    if (is_pinned(h_arena)) {
+        LV_HIP(hipMemcpyAsync(c->d_arena, h_arena, arena_bytes, hipMemcpyHostToDevice, s));
+    } else {
+        for (auto &st : c->h_stage)
+            if (int rc = grow_pinned(&st, &c->h_stage_cap[&st - c->h_stage], kStageBytes)) return rc;
+        size_t k = 0;
+        for (size_t pos = 0; pos < arena_bytes; pos += kStageBytes, ++k) {
+            const size_t len = arena_bytes - pos < kStageBytes ? arena_bytes - pos : kStageBytes;
+            const int slot = static_cast<int>(k & 1);
+            if (k >= 2) LV_HIP(hipEventSynchronize(c->ev[slot]));
+            par_memcpy(c->h_stage[slot], h_arena + pos, len);
+            LV_HIP(hipMemcpyAsync(c->d_arena + pos, c->h_stage[slot], len, hipMemcpyHostToDevice, s));
+            LV_HIP(hipEventRecord(c->ev[slot], s));
+        }
+    }
     uint8_t *ws = nullptr;
     if (int rc = stream_ws(*c, s, n, &ws)) return rc;
     if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s))
         return rc;
     if (int rc = check_launch()) return rc;
-    LV_HIP(hipMemcpyAsync(c->h_pinned, d_out, n * 4, hipMemcpyDeviceToHost, s));
+    LV_HIP(hipMemcpyAsync(c->h_meta, d_out, n * 4, hipMemcpyDeviceToHost, s));
     LV_HIP(hipStreamSynchronize(s));
-    std::memcpy(h_out, c->h_pinned, n * 4);
+    std::memcpy(h_out, c->h_meta, n * 4);
     return LV_OK;
 }
 
