@@ -42,6 +42,7 @@
 
 #include "../../include/lvgpu/crc32c.h"
 #include "crc32c_gf2.h"
+#include "wal_internal.h"
 
 namespace lvk {
 
@@ -974,6 +975,10 @@ int check_launch() {
 }
 
 }  // namespace
+
+namespace lvgpu_internal {
+int set_error(int code, const char *msg) { return set_err(code, msg); }
+}  // namespace lvgpu_internal
 
 extern "C" {
 

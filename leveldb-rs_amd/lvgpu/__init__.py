@@ -82,11 +82,15 @@ def _check(rc: int) -> None:
 
 
 def declared_symbols() -> list:
-    """Function names declared in include/lvgpu/crc32c.h."""
+    """Function names declared in include/lvgpu/*.h (crc32c.h, wal.h, ...)."""
+    import glob
     import re
-    with open(HEADER_PATH) as f:
-        text = f.read()
-    return re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s+\*?\s*(lv_[a-z0-9_]+)\s*\(", text, re.M)
+    names = []
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(HEADER_PATH), "*.h"))):
+        with open(path) as f:
+            text = f.read()
+        names += re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s+\*?\s*(lv_[a-z0-9_]+)\s*\(", text, re.M)
+    return names
 
 
 # ---- scalar drop-ins (crc32c.rs) -------------------------------------------

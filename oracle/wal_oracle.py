@@ -381,3 +381,31 @@ def wal_physical_records(log: bytes):
             out.append((pos, length, t))
         pos += HEADER_SIZE + length
     return out
+
+
+def scan_log(log: bytes):
+    """Restatement of the block framing of log_reader.rs:271-331 over a whole
+    log, as the GPU scan computes it: per 32 KiB block, walk the header chain
+    until < HEADER_SIZE bytes remain, a length overruns the block (status 1)
+    or a ZERO/0 header (status 2).  Returns (header offsets, value([type ||
+    payload]) or 0, info = type | status << 8 | length << 16)."""
+    offs, crcs, info = [], [], []
+    for start in range(0, len(log), BLOCK_SIZE):
+        blen = min(BLOCK_SIZE, len(log) - start)
+        pos = 0
+        while blen - pos >= HEADER_SIZE:
+            h = log[start + pos:start + pos + HEADER_SIZE]
+            length = h[4] | (h[5] << 8)
+            t = h[6]
+            status = 0
+            if HEADER_SIZE + length > blen - pos:
+                status = 1
+            elif t == ZERO and length == 0:
+                status = 2
+            offs.append(start + pos)
+            crcs.append(value(log[start + pos + 6:start + pos + 7 + length]) if status == 0 else 0)
+            info.append(t | (status << 8) | (length << 16))
+            if status:
+                break
+            pos += HEADER_SIZE + length
+    return offs, crcs, info

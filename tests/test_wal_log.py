@@ -1,7 +1,14 @@
 """Replays the reference WAL test-suite (src/log_writer.rs:460-838, the
-LogTest harness at :268-443) against the Python WAL restatement
-(oracle/wal_oracle.py), with the reference's own expected values.  This pins
-the WAL oracle the GPU verify/encode paths are checked against."""
+LogTest harness at :268-443) with the reference's own expected values against
+three readers/writers:
+
+  oracle  the Python restatement (oracle/wal_oracle.py) — pins the oracle;
+  native  the product's host Reader (csrc/wal_host.cc, lv_wal_reader_*) fed a
+          scan the oracle computed (lv_wal_scan_from_arrays) — runs on CPU;
+  gpu     writes through lv_wal_encode_host (header CRCs batched on the GPU)
+          and reads through lv_wal_scan_host (framing + CRCs on the GPU) and
+          the host Reader.
+"""
 import hashlib
 
 import pytest
@@ -12,28 +19,70 @@ B, H = W.BLOCK_SIZE, W.HEADER_SIZE
 
 
 class LogTest:
-    """log_writer.rs:268-443."""
+    """log_writer.rs:268-443, over one of the three backends."""
 
-    def __init__(self):
+    def __init__(self, backend="oracle"):
+        self.backend = backend
         self.dest = bytearray()
+        self.pending = []          # gpu backend: records not yet encoded
+        self.writer_base = 0       # dest length when the current Writer was made
         self.writer = W.Writer(self.dest)
         self.source = W.StringSource()
         self.reporter = W.ReportCollector()
         self.reading = False
-        self.reader = W.Reader(self.source, self.reporter, True, 0)
+        self.initial_offset = 0
+        self.reader = None
+        if backend == "oracle":
+            self.reader = W.Reader(self.source, self.reporter, True, 0)
 
-    def read(self):
-        if not self.reading:
-            self.reading = True
-            self.source.contents = bytes(self.dest)
-        r = self.reader.read_record()
-        return "EOF" if r is None else r.decode()
+    # -- writer side --
+    def _flush(self):
+        if self.pending:
+            import lvgpu.wal as LW
+            # the Writer's block offset is the bytes it has written itself
+            # (Writer::new_with_dest_length, log_writer.rs:48-56)
+            self.dest += LW.encode(self.pending, dest_length=len(self.dest) - self.writer_base)
+            self.pending = []
 
     def write(self, msg):
         assert not self.reading
-        self.writer.add_record(msg.encode())
+        if self.backend == "gpu":
+            self.pending.append(msg.encode())
+        else:
+            self.writer.add_record(msg.encode())
+
+    def reopen_for_append(self):  # log_writer.rs:326-329: Writer::new, block offset 0
+        self._flush()
+        self.writer = W.Writer(self.dest)
+        self.writer_base = len(self.dest)
+
+    # -- reader side --
+    def _native_reader(self, log, initial_offset):
+        import lvgpu.wal as LW
+        if self.backend == "gpu":
+            scan = LW.Scan.host(log)
+        else:
+            scan = LW.Scan.from_arrays(*W.scan_log(log))
+        return LW.Reader(log, scan, self.reporter, True, initial_offset)
+
+    def _start(self):
+        self._flush()
+        self.reading = True
+        self.source.contents = bytes(self.dest)
+        if self.backend != "oracle":
+            self.reader = self._native_reader(self.source.contents, self.initial_offset)
+
+    def read(self):
+        if not self.reading:
+            self._start()
+        r = self.reader.read_record()
+        return "EOF" if r is None else r.decode()
+
+    def last_record_offset(self, rd):
+        return rd.last_record_offset if self.backend == "oracle" else rd.last_record_offset()
 
     def written_bytes(self):
+        self._flush()
         return len(self.dest)
 
     def dropped_bytes(self):
@@ -42,30 +91,39 @@ class LogTest:
     def report_message(self):
         return self.reporter.message
 
-    def reopen_for_append(self):
-        self.writer = W.Writer(self.dest)
-
-    def force_error(self):
-        self.source.force_error = True
-
     def match_error(self, msg):
         return "OK" if msg in self.reporter.message else self.reporter.message
 
     def increment_bytes(self, off, delta):
+        self._flush()
         self.dest[off] = (self.dest[off] + delta) & 0xFF
 
     def fix_checksum(self, hoff, ln):
+        self._flush()
         c = W.mask(W.value(bytes(self.dest[hoff + 6:hoff + 7 + ln])))
         self.dest[hoff:hoff + 4] = W.encode_fixed_32(c)
 
     def shrink_size(self, n):
+        self._flush()
         del self.dest[len(self.dest) - n:]
 
     def set_byte(self, off, v):
+        self._flush()
         self.dest[off] = v
 
     def start_reading_at(self, off):
-        self.reader = W.Reader(self.source, self.reporter, True, off)
+        if self.backend == "oracle":
+            self.reader = W.Reader(self.source, self.reporter, True, off)
+        else:
+            self.initial_offset = off
+
+    def _reader_at(self, off):
+        self._flush()
+        self.reading = True
+        self.source.contents = bytes(self.dest)
+        if self.backend == "oracle":
+            return W.Reader(self.source, self.reporter, True, off)
+        return self._native_reader(self.source.contents, off)
 
     def write_initial_offset_log(self):
         for i in range(len(SIZES)):
@@ -73,23 +131,26 @@ class LogTest:
 
     def check_initial_offset_record(self, initial_offset, expected):
         self.write_initial_offset_log()
-        self.reading = True
-        self.source.contents = bytes(self.dest)
-        rd = W.Reader(self.source, self.reporter, True, initial_offset)
+        rd = self._reader_at(initial_offset)
         while expected < len(SIZES):
             rec = rd.read_record()
             assert rec is not None
             assert len(rec) == SIZES[expected]
-            assert rd.last_record_offset == OFFSETS[expected]
+            assert self.last_record_offset(rd) == OFFSETS[expected]
             assert rec[0] == ord("a") + expected
             expected += 1
 
     def check_offset_past_end_returns_no_records(self, past):
         self.write_initial_offset_log()
-        self.reading = True
-        self.source.contents = bytes(self.dest)
-        rd = W.Reader(self.source, self.reporter, True, self.written_bytes() + past)
+        rd = self._reader_at(self.written_bytes() + past)
         assert rd.read_record() is None
+
+
+@pytest.fixture(params=["oracle", "native", pytest.param("gpu", marks=pytest.mark.gpu)])
+def LogTest_(request):
+    if request.param == "gpu":
+        request.getfixturevalue("gpu")
+    return lambda: LogTest(request.param)
 
 
 SIZES = [10000, 10000, 2 * B - 1000, 1, 13716, B - H]  # log_writer.rs:246-253
@@ -97,26 +158,27 @@ OFFSETS = [0, H + 10000, 2 * (H + 10000), 2 * (H + 10000) + (2 * B - 1000) + 3 *
            2 * (H + 10000) + (2 * B - 1000) + 3 * H + H + 1, 3 * B]  # :255-266
 
 
-def test_empty():
-    assert LogTest().read() == "EOF"
+def test_empty(LogTest_):
+    assert LogTest_().read() == "EOF"
 
 
-def test_read_write():
-    t = LogTest()
+def test_read_write(LogTest_):
+    t = LogTest_()
     for m in ("foo", "bar", "", "xxxx"):
         t.write(m)
     assert t.read() == "foo"
 
 
-def test_add_record_foo_header_bytes():
-    t = LogTest()
+def test_add_record_foo_header_bytes(LogTest_):
+    t = LogTest_()
     t.write("foo")
+    assert t.written_bytes() == 10
     assert bytes(t.dest[:7]).hex() == "dd5fb37a030001"
 
 
 @pytest.mark.slow
-def test_many_blocks():
-    t = LogTest()
+def test_many_blocks(LogTest_):
+    t = LogTest_()
     for i in range(100000):
         t.write(str(i))
     for i in range(100000):
@@ -124,8 +186,8 @@ def test_many_blocks():
     assert t.read() == "EOF"
 
 
-def test_fragmentation():
-    t = LogTest()
+def test_fragmentation(LogTest_):
+    t = LogTest_()
     t.write("small")
     t.write(W.big_string("medium", 50000))
     t.write(W.big_string("large", 100000))
@@ -135,8 +197,8 @@ def test_fragmentation():
     assert t.read() == "EOF"
 
 
-def test_marginal_trailer():
-    t = LogTest()
+def test_marginal_trailer(LogTest_):
+    t = LogTest_()
     n = B - 2 * H
     t.write(W.big_string("foo", n))
     assert t.written_bytes() == B - H
@@ -148,8 +210,8 @@ def test_marginal_trailer():
     assert t.read() == "EOF"
 
 
-def test_marginal_trailer_2():
-    t = LogTest()
+def test_marginal_trailer_2(LogTest_):
+    t = LogTest_()
     n = B - 2 * H
     t.write(W.big_string("foo", n))
     assert t.written_bytes() == B - H
@@ -161,8 +223,8 @@ def test_marginal_trailer_2():
     assert t.report_message() == ""
 
 
-def test_short_trailer():
-    t = LogTest()
+def test_short_trailer(LogTest_):
+    t = LogTest_()
     n = B - 2 * H + 4
     t.write(W.big_string("foo", n))
     assert t.written_bytes() == B - H + 4
@@ -174,8 +236,8 @@ def test_short_trailer():
     assert t.read() == "EOF"
 
 
-def test_aligned_eof():
-    t = LogTest()
+def test_aligned_eof(LogTest_):
+    t = LogTest_()
     n = B - 2 * H + 4
     t.write(W.big_string("foo", n))
     assert t.written_bytes() == B - H + 4
@@ -183,8 +245,8 @@ def test_aligned_eof():
     assert t.read() == "EOF"
 
 
-def test_open_for_append():
-    t = LogTest()
+def test_open_for_append(LogTest_):
+    t = LogTest_()
     t.write("hello")
     t.reopen_for_append()
     t.write("world")
@@ -193,8 +255,8 @@ def test_open_for_append():
     assert t.read() == "EOF"
 
 
-def test_rand_read():
-    t = LogTest()
+def test_rand_read(LogTest_):
+    t = LogTest_()
     wr = W.Random(301)
     for i in range(500):
         t.write(W.random_skewed_string(i, wr))
@@ -204,8 +266,8 @@ def test_rand_read():
     assert t.read() == "EOF"
 
 
-def test_bad_record_type():
-    t = LogTest()
+def test_bad_record_type(LogTest_):
+    t = LogTest_()
     t.write("foo")
     t.increment_bytes(6, 100)
     t.fix_checksum(0, 3)
@@ -213,8 +275,8 @@ def test_bad_record_type():
     assert t.dropped_bytes() == 3
 
 
-def test_truncated_trailing_record_is_ignored():
-    t = LogTest()
+def test_truncated_trailing_record_is_ignored(LogTest_):
+    t = LogTest_()
     t.write("foo")
     t.shrink_size(4)
     assert t.read() == "EOF"
@@ -222,8 +284,8 @@ def test_truncated_trailing_record_is_ignored():
     assert t.report_message() == ""
 
 
-def test_bad_length():
-    t = LogTest()
+def test_bad_length(LogTest_):
+    t = LogTest_()
     t.write(W.big_string("bar", B - H))
     t.write("foo")
     t.increment_bytes(4, 1)
@@ -232,8 +294,8 @@ def test_bad_length():
     assert t.match_error("bad record length") == "OK"
 
 
-def test_bad_length_at_end_is_ignored():
-    t = LogTest()
+def test_bad_length_at_end_is_ignored(LogTest_):
+    t = LogTest_()
     t.write("foo")
     t.shrink_size(1)
     assert t.read() == "EOF"
@@ -241,8 +303,8 @@ def test_bad_length_at_end_is_ignored():
     assert t.report_message() == ""
 
 
-def test_checksum_mismatch():
-    t = LogTest()
+def test_checksum_mismatch(LogTest_):
+    t = LogTest_()
     t.write("foo")
     t.increment_bytes(0, 10)
     assert t.read() == "EOF"
@@ -251,8 +313,8 @@ def test_checksum_mismatch():
 
 
 @pytest.mark.parametrize("ty", [W.MIDDLE, W.LAST])
-def test_unexpected_middle_last_type(ty):
-    t = LogTest()
+def test_unexpected_middle_last_type(LogTest_, ty):
+    t = LogTest_()
     t.write("foo")
     t.set_byte(6, ty)
     t.fix_checksum(0, 3)
@@ -261,8 +323,8 @@ def test_unexpected_middle_last_type(ty):
     assert t.match_error("missing start") == "OK"
 
 
-def test_unexpected_full_type():
-    t = LogTest()
+def test_unexpected_full_type(LogTest_):
+    t = LogTest_()
     t.write("foo")
     t.write("bar")
     t.set_byte(6, W.FIRST)
@@ -273,8 +335,8 @@ def test_unexpected_full_type():
     assert t.match_error("partial record without end") == "OK"
 
 
-def test_unexpected_first_type():
-    t = LogTest()
+def test_unexpected_first_type(LogTest_):
+    t = LogTest_()
     t.write("foo")
     t.write(W.big_string("bar", 100000))
     t.set_byte(6, W.FIRST)
@@ -285,8 +347,8 @@ def test_unexpected_first_type():
     assert t.match_error("partial record without end") == "OK"
 
 
-def test_missing_last_is_ignored():
-    t = LogTest()
+def test_missing_last_is_ignored(LogTest_):
+    t = LogTest_()
     t.write(W.big_string("bar", B))
     t.shrink_size(14)
     assert t.read() == "EOF"
@@ -294,8 +356,8 @@ def test_missing_last_is_ignored():
     assert t.report_message() == ""
 
 
-def test_partial_last_is_ignored():
-    t = LogTest()
+def test_partial_last_is_ignored(LogTest_):
+    t = LogTest_()
     t.write(W.big_string("bar", B))
     t.shrink_size(1)
     assert t.read() == "EOF"
@@ -303,8 +365,8 @@ def test_partial_last_is_ignored():
     assert t.report_message() == ""
 
 
-def test_skip_into_multi_record():
-    t = LogTest()
+def test_skip_into_multi_record(LogTest_):
+    t = LogTest_()
     t.write(W.big_string("foo", 3 * B))
     t.write("correct")
     t.start_reading_at(B)
@@ -314,8 +376,8 @@ def test_skip_into_multi_record():
     assert t.read() == "EOF"
 
 
-def test_error_joins_record():
-    t = LogTest()
+def test_error_joins_record(LogTest_):
+    t = LogTest_()
     t.write(W.big_string("foo", B))
     t.write(W.big_string("bar", B))
     t.write("correct")
@@ -330,13 +392,13 @@ def test_error_joins_record():
     (0, 0), (1, 1), (10000, 1), (10007, 1), (10008, 2), (20014, 2), (20015, 3),
     (B - 4, 3), (B + 1, 3), (2 * B + 1, 3),
     (2 * (H + 10000) + (2 * B - 1000) + 3 * H, 3), (3 * B - 3, 5)])
-def test_initial_offsets(off, exp):
-    LogTest().check_initial_offset_record(off, exp)
+def test_initial_offsets(LogTest_, off, exp):
+    LogTest_().check_initial_offset_record(off, exp)
 
 
 @pytest.mark.parametrize("past", [0, 5])
-def test_offset_past_end(past):
-    LogTest().check_offset_past_end_returns_no_records(past)
+def test_offset_past_end(LogTest_, past):
+    LogTest_().check_offset_past_end_returns_no_records(past)
 
 
 def test_fixture_matches_oracle(wal_golden):
