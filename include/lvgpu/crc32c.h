@@ -57,6 +57,7 @@ uint32_t lv_crc32c_extend_hw(uint32_t crc, const uint8_t *data, size_t n);
 #define LV_OK 0
 #define LV_ERR_INVALID (-1) /* bad argument                                   */
 #define LV_ERR_NO_DEVICE (-2) /* no usable GPU / HIP runtime error at init     */
+#define LV_ERR_CORRUPTION (-3) /* malformed on-disk data (table format decode)  */
 
 /* out[i] = [mask](extend(seed ? seed[i] : 0, arena[off[i] .. off[i]+len[i])))
  * for i < n.  All pointers are device pointers; `d_seed` may be NULL (all
@@ -88,6 +89,19 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
 int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off,
                          const uint32_t *h_len, const uint32_t *h_seed, uint32_t *h_out, size_t n,
                          uint32_t flags, int device);
+
+/* Multi-GPU host batch: lv_crc32c_batch_host semantics, with
+ * the buffers split into contiguous ranges balanced by payload bytes, one per
+ * device (0..ngpu-1), one host thread per device; each device receives only
+ * its range's arena span.  No collective.  A device that is not present fails
+ * the call (lv_last_error names it). */
+int lv_crc32c_batch_multi(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off, const uint32_t *h_len,
+                          const uint32_t *h_seed, uint32_t *h_out, size_t n, uint32_t flags, int ngpu);
+/* The same over an explicit device list (a device may repeat: its ranges
+ * then run one after another). */
+int lv_crc32c_batch_multi_devices(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off,
+                                  const uint32_t *h_len, const uint32_t *h_seed, uint32_t *h_out, size_t n,
+                                  uint32_t flags, const int *devices, int ndev);
 
 /* ---- runtime ----------------------------------------------------------- */
 

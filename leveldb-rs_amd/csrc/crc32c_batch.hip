@@ -42,7 +42,7 @@
 
 #include "../../include/lvgpu/crc32c.h"
 #include "crc32c_gf2.h"
-#include "wal_internal.h"
+#include "lv_internal.h"
 
 namespace lvk {
 
@@ -978,6 +978,8 @@ int check_launch() {
 
 namespace lvgpu_internal {
 int set_error(int code, const char *msg) { return set_err(code, msg); }
+void clear_error() { g_err.clear(); }
+int launch_status() { return check_launch(); }
 }  // namespace lvgpu_internal
 
 extern "C" {

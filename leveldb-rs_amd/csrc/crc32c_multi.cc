@@ -1,0 +1,85 @@
+// Multi-GPU host batch (SURVEY 8b `lv_crc32c_batch_multi`, 8e): buffers are
+// independent, so the batch is split into contiguous buffer ranges balanced
+// by payload bytes (prefix sum of lengths), one range per device and one host
+// thread per device; each device receives only its range's arena span and
+// metadata and writes back its slice of out[].  No collective, no peer
+// traffic.
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/lvgpu/crc32c.h"
+#include "lv_internal.h"
+
+namespace {
+
+// Buffer-range boundaries b[0..k]: range r holds ~ total*r/k payload bytes.
+std::vector<size_t> byte_balanced(const uint32_t *len, size_t n, int k) {
+    std::vector<uint64_t> pre(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) pre[i + 1] = pre[i] + len[i];
+    std::vector<size_t> b(k + 1, n);
+    b[0] = 0;
+    for (int r = 1; r < k; ++r) {
+        const uint64_t target = pre[n] / k * r + (pre[n] % k) * r / k;
+        b[r] = static_cast<size_t>(std::lower_bound(pre.begin(), pre.end(), target) - pre.begin());
+        b[r] = std::max(b[r], b[r - 1]);
+    }
+    return b;
+}
+
+struct Shard {
+    int rc = LV_OK;
+    std::string err;
+};
+
+}  // namespace
+
+extern "C" {
+
+int lv_crc32c_batch_multi_devices(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off,
+                                  const uint32_t *h_len, const uint32_t *h_seed, uint32_t *h_out, size_t n,
+                                  uint32_t flags, const int *devices, int ndev) {
+    lvgpu_internal::clear_error();
+    if (n == 0) return LV_OK;
+    if (!h_arena || !h_off || !h_len || !h_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null host pointer");
+    if (!devices || ndev <= 0) return lvgpu_internal::set_error(LV_ERR_INVALID, "no devices");
+    for (size_t i = 0; i < n; ++i)
+        if (h_off[i] > arena_bytes || h_len[i] > arena_bytes - h_off[i])
+            return lvgpu_internal::set_error(LV_ERR_INVALID, "buffer outside arena");
+    const std::vector<size_t> b = byte_balanced(h_len, n, ndev);
+    std::vector<Shard> res(ndev);
+    std::vector<std::thread> th;
+    for (int r = 0; r < ndev; ++r) {
+        if (b[r] == b[r + 1]) continue;
+        th.emplace_back([&, r] {
+            const size_t lo = b[r], cnt = b[r + 1] - b[r];
+            uint64_t first = UINT64_MAX, last = 0;
+            for (size_t i = lo; i < lo + cnt; ++i) {
+                first = std::min(first, h_off[i]);
+                last = std::max(last, h_off[i] + h_len[i]);
+            }
+            std::vector<uint64_t> off(h_off + lo, h_off + lo + cnt);
+            for (auto &o : off) o -= first;  // this device's span starts at `first`
+            res[r].rc = lv_crc32c_batch_host(h_arena + first, last - first, off.data(), h_len + lo,
+                                             h_seed ? h_seed + lo : nullptr, h_out + lo, cnt, flags, devices[r]);
+            if (res[r].rc) res[r].err = lv_last_error();
+        });
+    }
+    for (auto &t : th) t.join();
+    for (int r = 0; r < ndev; ++r)
+        if (res[r].rc)
+            return lvgpu_internal::set_error(res[r].rc, ("device " + std::to_string(devices[r]) + ": " + res[r].err).c_str());
+    return LV_OK;
+}
+
+int lv_crc32c_batch_multi(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off, const uint32_t *h_len,
+                          const uint32_t *h_seed, uint32_t *h_out, size_t n, uint32_t flags, int ngpu) {
+    if (ngpu <= 0 || ngpu > 64) return lvgpu_internal::set_error(LV_ERR_INVALID, "ngpu must be in 1..64");
+    std::vector<int> dev(ngpu);
+    for (int i = 0; i < ngpu; ++i) dev[i] = i;
+    return lv_crc32c_batch_multi_devices(h_arena, arena_bytes, h_off, h_len, h_seed, h_out, n, flags, dev.data(),
+                                         ngpu);
+}
+
+}  // extern "C"

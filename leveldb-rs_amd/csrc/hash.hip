@@ -1,0 +1,120 @@
+// Batched leveldb hash (util/hash.rs:20-51) on MI355X, SURVEY 8f row 4.
+//
+// The hash is a serial, non-linear chain over 4-byte words
+// (h = ((h + w) * m) ^ (h >> 16)), so unlike CRC32C it cannot be split
+// inside a buffer: one lane owns one buffer.  Its keys are cache keys (tens of
+// bytes), so a launch is bound by metadata + key bytes through HBM; per lane
+// the words are read as dword-aligned 16-B loads funnel-shifted by the
+// buffer's byte misalignment (v_alignbyte_b32), never touching a dword past
+// the buffer's last byte.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "../../include/lvgpu/crc32c.h"
+#include "../../include/lvgpu/hash.h"
+#include "lv_internal.h"
+
+namespace lvh {
+
+constexpr uint32_t kM = 0xc6a4a793u;  // hash.rs:23
+
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ uint32_t mix(uint32_t h, uint32_t w) {  // hash.rs:31-35
+    h += w;
+    h *= kM;
+    return h ^ (h >> 16);
+}
+
+// bytes [bs, bs+4) of the 8-byte little-endian pair (lo, hi)
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t bs) {
+    return __builtin_amdgcn_alignbyte(hi, lo, bs);
+}
+
+__global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ base,
+                                                   const uint64_t *__restrict__ off,
+                                                   const uint32_t *__restrict__ len,
+                                                   const uint32_t *__restrict__ seed, uint32_t *__restrict__ out,
+                                                   uint32_t n, uint32_t flags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o = off[i];
+    const uint32_t L = len[i];
+    uint32_t h = (seed ? seed[i] : 0u) ^ (kM * L);  // hash.rs:25
+    if (L) {
+        const uint32_t bs = static_cast<uint32_t>(o & 3u);
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
+        const uint32_t nw = L >> 2;               // whole words, hash.rs:29
+        const uint32_t ndw = (bs + L + 3) >> 2;   // dwords covering the buffer
+        uint32_t cur = d[0];
+        uint32_t k = 0;
+        // 4 words per step from d[k+1 .. k+4], all inside the buffer's dwords
+        for (; k + 4 <= nw && k + 4 < ndw; k += 4) {
+            const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + k + 1);
+            h = mix(h, funnel(v.x, cur, bs));
+            h = mix(h, funnel(v.y, v.x, bs));
+            h = mix(h, funnel(v.z, v.y, bs));
+            h = mix(h, funnel(v.w, v.z, bs));
+            cur = v.w;
+        }
+        for (; k < nw; ++k) {
+            const uint32_t hi = k + 1 < ndw ? d[k + 1] : 0u;
+            h = mix(h, funnel(hi, cur, bs));
+            cur = hi;
+        }
+        const uint32_t diff = L - 4 * nw;          // hash.rs:38-48
+        if (diff) {
+            const uint32_t hi = nw + 1 < ndw ? d[nw + 1] : 0u;
+            const uint32_t t = funnel(hi, cur, bs);
+            if (diff >= 3) h += ((t >> 16) & 0xffu) << 16;
+            if (diff >= 2) h += ((t >> 8) & 0xffu) << 8;
+            h += t & 0xffu;
+            h *= kM;
+            h ^= h >> 24;
+        }
+    }
+    out[i] = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
+}
+
+}  // namespace lvh
+
+extern "C" {
+
+uint32_t lv_hash(const uint8_t *data, size_t n, uint32_t seed) {
+    uint32_t h = seed ^ (lvh::kM * static_cast<uint32_t>(n));
+    size_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        uint32_t w;
+        std::memcpy(&w, data + i, 4);  // decode_fixed_32 (little-endian host)
+        h += w;
+        h *= lvh::kM;
+        h ^= h >> 16;
+    }
+    const size_t diff = n - i;
+    if (diff >= 3) h += static_cast<uint32_t>(data[i + 2]) << 16;
+    if (diff >= 2) h += static_cast<uint32_t>(data[i + 1]) << 8;
+    if (diff >= 1) {
+        h += data[i];
+        h *= lvh::kM;
+        h ^= h >> 24;
+    }
+    return h;
+}
+
+uint32_t lv_cache_shard(uint32_t hash) { return hash >> 28; }
+
+int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                         const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags, void *stream) {
+    lvgpu_internal::clear_error();
+    if (n == 0) return LV_OK;
+    if (!d_arena || !d_off || !d_len || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
+    if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
+    if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
+    const uint32_t grid = static_cast<uint32_t>((n + 255) / 256);
+    hipLaunchKernelGGL(lvh::hash_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_arena, d_off,
+                       d_len, d_seed, d_out, static_cast<uint32_t>(n), flags);
+    return lvgpu_internal::launch_status();
+}
+
+}  // extern "C"

@@ -1,4 +1,5 @@
-// Internal: the scan object shared by the GPU scan and the host reader.
+// Internal declarations shared by the product sources: the WAL scan object
+// (GPU scan + host reader) and the lv_last_error plumbing.
 #pragma once
 #include <cstdint>
 #include <vector>
@@ -11,4 +12,6 @@ struct lv_wal_scan {
 
 namespace lvgpu_internal {
 int set_error(int code, const char *msg);  // lv_last_error plumbing (crc32c_batch.hip)
+void clear_error();
+int launch_status();                       // hipGetLastError -> LV status + message
 }

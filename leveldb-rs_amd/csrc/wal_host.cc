@@ -10,7 +10,7 @@
 
 #include "../../include/lvgpu/crc32c.h"
 #include "../../include/lvgpu/wal.h"
-#include "wal_internal.h"
+#include "lv_internal.h"
 
 namespace {
 

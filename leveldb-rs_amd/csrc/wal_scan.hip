@@ -20,7 +20,7 @@
 
 #include "../../include/lvgpu/crc32c.h"
 #include "../../include/lvgpu/wal.h"
-#include "wal_internal.h"
+#include "lv_internal.h"
 
 namespace lvw {
 

@@ -64,6 +64,10 @@ def lib() -> ctypes.CDLL:
     L.lv_crc32c_batch_strided.argtypes = [vp, u64, u32, sz, vp, vp, u32, vp]
     L.lv_crc32c_batch_host.restype = ctypes.c_int
     L.lv_crc32c_batch_host.argtypes = [vp, sz, vp, vp, vp, vp, sz, u32, ctypes.c_int]
+    L.lv_crc32c_batch_multi.restype = ctypes.c_int
+    L.lv_crc32c_batch_multi.argtypes = [vp, sz, vp, vp, vp, vp, sz, u32, ctypes.c_int]
+    L.lv_crc32c_batch_multi_devices.restype = ctypes.c_int
+    L.lv_crc32c_batch_multi_devices.argtypes = [vp, sz, vp, vp, vp, vp, sz, u32, vp, ctypes.c_int]
     L.lv_device_init.restype = ctypes.c_int
     L.lv_device_init.argtypes = []
     L.lv_last_error.restype = ctypes.c_char_p
@@ -220,6 +224,26 @@ def batch_host(arena: bytes, off, length, seed=None, masked=False, device: int =
         a.ctypes.data_as(ctypes.c_void_p), a.size, o.ctypes.data_as(ctypes.c_void_p),
         ln.ctypes.data_as(ctypes.c_void_p), None if sd is None else sd.ctypes.data_as(ctypes.c_void_p),
         out.ctypes.data_as(ctypes.c_void_p), n, MASK if masked else 0, device))
+    return out
+
+
+def batch_multi(arena: bytes, off, length, seed=None, masked=False, ngpu: int = None, devices=None):
+    """Host-memory batch split by payload bytes over devices 0..ngpu-1 (or an
+    explicit `devices` list, repeats allowed); returns np.uint32 array."""
+    import numpy as np
+    a = np.frombuffer(arena, dtype=np.uint8) if isinstance(arena, (bytes, bytearray)) else np.ascontiguousarray(arena, dtype=np.uint8)
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(length, dtype=np.uint32)
+    sd = None if seed is None else np.ascontiguousarray(seed, dtype=np.uint32)
+    out = np.empty(o.size, dtype=np.uint32)
+    vp = ctypes.c_void_p
+    args = (a.ctypes.data_as(vp), a.size, o.ctypes.data_as(vp), ln.ctypes.data_as(vp),
+            None if sd is None else sd.ctypes.data_as(vp), out.ctypes.data_as(vp), o.size, MASK if masked else 0)
+    if devices is not None:
+        d = np.ascontiguousarray(devices, dtype=np.int32)
+        _check(lib().lv_crc32c_batch_multi_devices(*args, d.ctypes.data_as(vp), d.size))
+    else:
+        _check(lib().lv_crc32c_batch_multi(*args, 1 if ngpu is None else ngpu))
     return out
 
 

@@ -11,6 +11,12 @@ Outputs (all data — inputs and expected outputs, no reference source):
   wal_scenarios.json  the reference LogTest WAL scenarios (log_writer.rs:460-838)
                     replayed through oracle/wal_oracle.py: log bytes digest,
                     every physical record's CRC unit and the reader outcome.
+  hash_kat.json     reference hash KATs (util/hash.rs:58-75) + seeded random
+                    (offset, length, seed) cases over the same arena.
+  table_format.json BlockHandle / Footer encodings (table/format.rs:107-147),
+                    varint cases (coding.rs:481-510) and block trailers over
+                    arena slices (trailer layout parity unpinned, see
+                    oracle/table_oracle.py).
 """
 import ctypes
 import hashlib
@@ -206,7 +212,76 @@ def wal_scenarios():
     return {"generator": "tests/golden/make_golden.py", "scenarios": scen}
 
 
+def hash_fixture():
+    L = W.lib()
+    L.oracle_hash.restype = ctypes.c_uint32
+    L.oracle_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
+    d5 = bytes([0x01, 0xc0] + [0] * 14 + [0x14, 0, 0, 0, 0, 0, 0x04, 0, 0, 0, 0, 0x14, 0, 0, 0, 0x18, 0x28]
+               + [0] * 7 + [0x02] + [0] * 7)
+    ref = [  # hash.rs:58-75, expected values from the reference test
+        ("empty", b"", 0xbc9f1d34, 0xbc9f1d34),
+        ("62", b"\x62", 0xbc9f1d34, 0xef1345c4),
+        ("c3 97", b"\xc3\x97", 0xbc9f1d34, 0x5b663814),
+        ("e2 99 a5", b"\xe2\x99\xa5", 0xbc9f1d34, 0x323c078f),
+        ("e1 80 b9 32", b"\xe1\x80\xb9\x32", 0xbc9f1d34, 0xed21633a),
+        ("48-byte data5", d5, 0x12345678, 0xf333dabb),
+    ]
+    kats = []
+    for name, data, seed, want in ref:
+        got = L.oracle_hash(data, len(data), seed)
+        assert got == want, (name, hex(got))
+        kats.append({"name": name, "hex": data.hex(), "seed": seed, "hash": want, "ref": "hash.rs:58-75"})
+    arena = arena_bytes()
+    rng = random.Random(0x4C564853)
+    cases = []
+    for i in range(800):
+        ln = rng.choice([rng.randrange(0, 17), rng.randrange(0, 129), rng.randrange(0, 8193)])
+        off = rng.randrange(0, ARENA_BYTES - ln + 1)
+        seed = rng.choice([0, 0xbc9f1d34, rng.getrandbits(32)])
+        cases.append([off, ln, seed, L.oracle_hash(arena[off:off + ln], ln, seed)])
+    return {"generator": "tests/golden/make_golden.py",
+            "arena": {"bytes": ARENA_BYTES, "seed": ARENA_SEED}, "kats": kats,
+            "cases_fields": ["offset", "length", "seed", "hash"], "cases": cases}
+
+
+def table_fixture():
+    import table_oracle as T
+    out = {"generator": "tests/golden/make_golden.py"}
+    b = bytearray()
+    T.BlockHandle(10, 20).encode_to(b)  # format.rs:107-123
+    out["block_handles"] = [{"offset": 10, "size": 20, "hex": bytes(b).hex(), "ref": "format.rs:107-123"}]
+    rng = random.Random(0x4C565442)
+    for _ in range(40):
+        o, sz = rng.getrandbits(rng.randrange(1, 65)), rng.getrandbits(rng.randrange(1, 65))
+        b = bytearray()
+        T.BlockHandle(o, sz).encode_to(b)
+        out["block_handles"].append({"offset": o, "size": sz, "hex": bytes(b).hex()})
+    f = bytearray()
+    T.Footer(T.BlockHandle(50, 100), T.BlockHandle(200, 400)).encode_to(f)  # format.rs:125-147
+    out["footers"] = [{"metaindex": [50, 100], "index": [200, 400], "hex": bytes(f).hex(), "ref": "format.rs:125-147"}]
+    big = bytearray()
+    T.Footer(T.BlockHandle(2**64 - 1, 2**64 - 1), T.BlockHandle(2**63, 1)).encode_to(big)
+    out["footers"].append({"metaindex": [2**64 - 1, 2**64 - 1], "index": [2**63, 1], "hex": bytes(big).hex()})
+    out["varints"] = [[v, T.encode_varint_64(v).hex()] for v in
+                      [0, 1, 127, 128, 1000, 16383, 16384, 1 << 60, 2**64 - 1]]  # coding.rs:481-510
+    arena = arena_bytes()
+    tr = []
+    for _ in range(60):
+        ln = rng.choice([0, 1, rng.randrange(0, 4097), rng.randrange(0, 70000)])
+        off = rng.randrange(0, ARENA_BYTES - ln + 1)
+        ctype = rng.choice([0, 1])
+        tr.append([off, ln, ctype, T.block_trailer(arena[off:off + ln], ctype).hex()])
+    out["trailers_fields"] = ["offset", "size", "type", "trailer_hex"]
+    out["trailers"] = tr
+    out["trailers_note"] = "type || LE32(mask(crc32c(contents || type))); parity unpinned beyond crc32c KATs"
+    return out
+
+
 def main():
+    with open(os.path.join(HERE, "hash_kat.json"), "w") as f:
+        json.dump(hash_fixture(), f, indent=0, separators=(",", ":"))
+    with open(os.path.join(HERE, "table_format.json"), "w") as f:
+        json.dump(table_fixture(), f, indent=0, separators=(",", ":"))
     kat = kat_fixture()
     with open(os.path.join(HERE, "crc32c_kat.json"), "w") as f:
         json.dump(kat, f, indent=0, separators=(",", ":"))

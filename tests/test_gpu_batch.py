@@ -278,3 +278,28 @@ def test_all_length_classes_one_batch(torch_dev):
     torch.cuda.synchronize()
     assert np.array_equal(r1.cpu().numpy().view(np.uint32), want)
     assert np.array_equal(r2.cpu().numpy().view(np.uint32), want[::-1])
+
+
+@pytest.mark.gpu
+def test_batch_multi_devices(gpu):
+    """lv_crc32c_batch_multi_devices: byte-balanced ranges over a device list
+    (device 0 repeated on a 1-GPU box) equal the oracle; ngpu beyond the
+    visible devices fails loudly."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(97)
+    n = 5000
+    lens = (32 * np.minimum(rng.zipf(1.1, size=n), 512)).astype(np.uint32)
+    arena_n = int(lens.sum()) + 4096
+    arena = rng.integers(0, 256, size=arena_n, dtype=np.uint8)
+    offs = rng.integers(0, arena_n - lens.astype(np.int64), dtype=np.int64).astype(np.uint64)
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    want = np.zeros(n, dtype=np.uint32)
+    W.lib().oracle_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, seeds.ctypes.data,
+                         want.ctypes.data, n, 1)
+    for devs in ([0], [0, 0], [0, 0, 0, 0, 0]):
+        got = lvgpu.batch_multi(arena, offs, lens, seeds, masked=True, devices=devs)
+        assert np.array_equal(got, want), devs
+    assert np.array_equal(lvgpu.batch_multi(arena, offs, lens, seeds, masked=True, ngpu=1), want)
+    with pytest.raises(lvgpu.LvError, match="device"):
+        lvgpu.batch_multi(arena, offs, lens, seeds, ngpu=torch.cuda.device_count() + 1)

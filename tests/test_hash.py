@@ -1,0 +1,118 @@
+"""util/hash.rs: the oracle and the product's host scalar against the
+reference KATs (hash.rs:58-75) and the seeded fixture; the GPU batch against
+the same fixture and random batches (gpu-marked)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import wal_oracle as W
+
+
+def _oracle():
+    L = W.lib()
+    L.oracle_hash.restype = ctypes.c_uint32
+    L.oracle_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
+    L.oracle_hash_batch.restype = None
+    L.oracle_hash_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t]
+    return L
+
+
+@pytest.fixture(scope="module")
+def hkat():
+    import json
+    import os
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "hash_kat.json")) as f:
+        return json.load(f)
+
+
+def test_oracle_reference_kats(hkat):
+    L = _oracle()
+    assert len(hkat["kats"]) == 6
+    for k in hkat["kats"]:
+        d = bytes.fromhex(k["hex"])
+        assert L.oracle_hash(d, len(d), k["seed"]) == k["hash"], k["name"]
+
+
+def test_scalar_matches_kats_and_cases(hkat, arena):
+    from lvgpu import hash as H
+    for k in hkat["kats"]:
+        assert H.hash(bytes.fromhex(k["hex"]), k["seed"]) == k["hash"], k["name"]
+    for off, ln, seed, want in hkat["cases"]:
+        assert H.hash(arena[off:off + ln], seed) == want
+    assert H.cache_shard(0xF0000000) == 15 and H.cache_shard(0x0FFFFFFF) == 0
+
+
+def _dev(gpu, arr, dtype):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(arr).astype(dtype)).to(gpu)
+
+
+@pytest.mark.gpu
+def test_gpu_fixture_cases(gpu, hkat, arena):
+    import torch
+    from lvgpu import hash as H
+    c = np.array(hkat["cases"], dtype=np.uint64)
+    a = torch.frombuffer(bytearray(arena), dtype=torch.uint8).to(gpu)
+    out = H.hash_batch(a, _dev(gpu, c[:, 0], np.int64), _dev(gpu, c[:, 1], np.int32),
+                       _dev(gpu, c[:, 2].astype(np.uint32).view(np.int32), np.int32))
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, c[:, 3].astype(np.uint32))
+    sh = H.hash_batch(a, _dev(gpu, c[:, 0], np.int64), _dev(gpu, c[:, 1], np.int32),
+                      _dev(gpu, c[:, 2].astype(np.uint32).view(np.int32), np.int32), shard=True)
+    assert np.array_equal(sh.cpu().numpy().view(np.uint32), c[:, 3].astype(np.uint32) >> 28)
+
+
+@pytest.mark.gpu
+def test_gpu_kats_every_alignment(gpu, hkat):
+    import torch
+    from lvgpu import hash as H
+    offs, lens, seeds, want, buf = [], [], [], [], bytearray()
+    for k in hkat["kats"]:
+        d = bytes.fromhex(k["hex"])
+        for a in range(16):
+            buf += bytes(a)
+            offs.append(len(buf))
+            lens.append(len(d))
+            seeds.append(k["seed"])
+            want.append(k["hash"])
+            buf += d
+    buf += bytes(16)
+    a = torch.frombuffer(buf, dtype=torch.uint8).to(gpu)
+    out = H.hash_batch(a, _dev(gpu, offs, np.int64), _dev(gpu, lens, np.int32),
+                       _dev(gpu, np.array(seeds, dtype=np.uint32).view(np.int32), np.int32))
+    assert out.cpu().numpy().view(np.uint32).tolist() == want
+
+
+@pytest.mark.gpu
+def test_gpu_random_lengths_and_arena_end(gpu):
+    """Every length 0..300 at every offset mod 16, including buffers that end
+    at the last byte of the allocation; seeds NULL (cache.rs uses 0)."""
+    import torch
+    from lvgpu import hash as H
+    L = _oracle()
+    rng = np.random.default_rng(41)
+    size = 1 << 16
+    arena = rng.integers(0, 256, size=size, dtype=np.uint8)
+    lens = np.repeat(np.arange(0, 301), 16).astype(np.uint32)
+    offs = (rng.integers(0, size - 400, size=lens.size) & ~15) + np.tile(np.arange(16), 301)
+    offs = np.concatenate([offs, size - np.arange(0, 64)]).astype(np.uint64)
+    lens = np.concatenate([lens, np.arange(0, 64)]).astype(np.uint32)
+    want = np.zeros(lens.size, dtype=np.uint32)
+    L.oracle_hash_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, want.ctypes.data, lens.size)
+    a = torch.from_numpy(arena).to(gpu)
+    out = H.hash_batch(a, _dev(gpu, offs, np.int64), _dev(gpu, lens.view(np.int32), np.int32))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.gpu
+def test_gpu_bad_args(gpu):
+    import torch
+    from lvgpu import LvError, hash as H
+    L = H._bind()
+    assert L.lv_hash_batch_device(None, None, None, None, None, 0, 0, None) == 0
+    assert L.lv_hash_batch_device(None, None, None, None, None, 5, 0, None) != 0
+    a = torch.zeros(16, dtype=torch.uint8, device=gpu)
+    with pytest.raises(LvError):
+        H.hash_batch(a, torch.zeros(3, dtype=torch.int64, device=gpu), torch.zeros(2, dtype=torch.int32, device=gpu))
