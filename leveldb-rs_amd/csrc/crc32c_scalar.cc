@@ -13,20 +13,37 @@ namespace {
 
 constexpr uint32_t kMaskDelta = 0xa282ead8u;  // crc32c.rs:23
 
+// Sixteen byte tables: t[k][e] = R(e, 0^k) — the CRC of byte e followed by
+// k zero bytes — so a 16-byte step is sixteen independent lookups.
 struct SliceTables {
-    uint32_t t[8][256];
+    uint32_t t[16][256];
     SliceTables() {
         uint32_t base[4][256];
         lvgpu::slice_tables(base);
         std::memcpy(t, base, sizeof(base));
-        for (int k = 4; k < 8; ++k)
+        for (int k = 4; k < 16; ++k)
             for (int e = 0; e < 256; ++e) t[k][e] = (t[k - 1][e] >> 8) ^ t[0][t[k - 1][e] & 0xffu];
     }
 };
 
-const SliceTables &tables() {
-    static const SliceTables tabs;  // thread-safe once-init (C++11 magic static)
-    return tabs;
+const SliceTables g_tabs;  // built at load time, read-only afterwards
+
+// Three-stream hardware path: a superblock of 3 x kLane bytes runs three
+// independent crc32q chains (the instruction's latency is 3 cycles, its
+// throughput 1/cycle) and merges them by linearity,
+// R(s, A||B||C) = Shift_2L(R(s, A)) ^ Shift_L(R(0, B)) ^ R(0, C).
+constexpr size_t kLane = 512;
+struct ShiftPair {
+    uint32_t l1[4][256], l2[4][256];  // Shift_kLane, Shift_2kLane as byte tables
+    ShiftPair() {
+        lvgpu::shift_tables(kLane, l1);
+        lvgpu::shift_tables(2 * kLane, l2);
+    }
+};
+const ShiftPair g_shift;
+
+inline uint32_t apply(const uint32_t (&t)[4][256], uint32_t s) {
+    return t[0][s & 0xff] ^ t[1][(s >> 8) & 0xff] ^ t[2][(s >> 16) & 0xff] ^ t[3][s >> 24];
 }
 
 inline uint32_t load32(const uint8_t *p) {
@@ -57,25 +74,38 @@ uint32_t lv_crc32c_unmask(uint32_t masked_crc) {
     return (r >> 17) | (r << 15);
 }
 
-// Slice-by-8: fold 8 bytes per step through eight byte tables.
+// Software path (the twin of crc32c.rs:65-84, same value): slice-by-16, the
+// state xored into the first word, the other 12 bytes indexed directly.
 uint32_t lv_crc32c_extend_sw(uint32_t crc, const uint8_t *data, size_t n) {
-    const auto &T = tables().t;
+    const uint32_t(*T)[256] = g_tabs.t;
     uint32_t s = ~crc;
-    for (; n >= 8; n -= 8, data += 8) {
-        const uint32_t lo = s ^ load32(data);
-        const uint32_t hi = load32(data + 4);
-        s = T[7][lo & 0xff] ^ T[6][(lo >> 8) & 0xff] ^ T[5][(lo >> 16) & 0xff] ^ T[4][lo >> 24] ^
-            T[3][hi & 0xff] ^ T[2][(hi >> 8) & 0xff] ^ T[1][(hi >> 16) & 0xff] ^ T[0][hi >> 24];
+    for (; n >= 16; n -= 16, data += 16) {
+        const uint32_t w = s ^ load32(data);
+        s = T[15][w & 0xff] ^ T[14][(w >> 8) & 0xff] ^ T[13][(w >> 16) & 0xff] ^ T[12][w >> 24] ^
+            T[11][data[4]] ^ T[10][data[5]] ^ T[9][data[6]] ^ T[8][data[7]] ^
+            T[7][data[8]] ^ T[6][data[9]] ^ T[5][data[10]] ^ T[4][data[11]] ^
+            T[3][data[12]] ^ T[2][data[13]] ^ T[1][data[14]] ^ T[0][data[15]];
     }
     while (n--) s = T[0][(s ^ *data++) & 0xff] ^ (s >> 8);
     return ~s;
 }
 
-// SSE4.2 crc32 instruction over 8-byte words.  The CRC is independent of
-// address alignment, so unlike crc32c.rs:97-102 no byte prologue is needed.
+// SSE4.2 crc32 instruction over 8-byte words (the twin of crc32c.rs:86-118,
+// same value).  The CRC is independent of address alignment, so no byte
+// prologue is needed; long buffers run three chains per superblock.
 __attribute__((target("sse4.2"))) uint32_t lv_crc32c_extend_hw(uint32_t crc, const uint8_t *data,
                                                                 size_t n) {
     uint64_t s = ~crc;
+    for (; n >= 3 * kLane; n -= 3 * kLane, data += 3 * kLane) {
+        uint64_t a = s, b = 0, c = 0;
+        for (size_t k = 0; k < kLane; k += 8) {
+            a = _mm_crc32_u64(a, load64(data + k));
+            b = _mm_crc32_u64(b, load64(data + kLane + k));
+            c = _mm_crc32_u64(c, load64(data + 2 * kLane + k));
+        }
+        s = apply(g_shift.l2, static_cast<uint32_t>(a)) ^ apply(g_shift.l1, static_cast<uint32_t>(b)) ^
+            static_cast<uint32_t>(c);
+    }
     for (; n >= 8; n -= 8, data += 8) s = _mm_crc32_u64(s, load64(data));
     uint32_t s32 = static_cast<uint32_t>(s);
     if (n >= 4) {

@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box pass of every bench line and kernel profile for the round:
+#   bench.py default (C3 strided, headline), C3 offsets, C2, C4, C5,
+#   the C1 CPU sweep, the host-memory E2E path, and rocprofv3 kernel-trace
+#   stats for C3 (strided) / C2 / C4.  Every GPU step has its own timeout and
+#   the chain stops at the first failure.
+# usage: tools/measure_round.sh OUTDIR
+set -o pipefail
+out=${1:-gpurun_out/round}
+mkdir -p "$out"
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$root"
+export TMPDIR=/tmp
+b() { local name=$1; shift; timeout -k 10 400 python3 bench.py "$@" > "$out/$name.json" 2> "$out/$name.err"; }
+p() { local name=$1; shift
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_$name" -o "$name" -- \
+         python3 "$root/bench.py" --steps 50 --warmup 100 --cpu-seconds 0 --traffic off "$@") > "$out/prof_$name.log" 2>&1; }
+b default &&
+b c3_offsets --workload c3 --api offsets --cpu-seconds 5 &&
+b c2 --workload c2 --api offsets --cpu-seconds 5 &&
+b c4 --workload c4 --api offsets --cpu-seconds 5 &&
+b c5 --workload c5 --cpu-seconds 5 &&
+timeout -k 10 200 python3 bench.py --e2e > "$out/e2e.json" 2> "$out/e2e.err" &&
+timeout -k 10 300 python3 bench.py --c1 > "$out/c1.json" 2> "$out/c1.err" &&
+p c3 &&
+p c2 --workload c2 --api offsets &&
+p c4 --workload c4 --api offsets &&
+echo "all steps done"

@@ -13,7 +13,7 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
            "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --pmc $set --output-format csv -d "$out/p$i" -o pmc -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 "$@" > "$out/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$out/p$i.log"; }
+  timeout -k 10 180 rocprofv3 --pmc $set --output-format csv -d "$out/p$i" -o pmc -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --traffic off "$@" > "$out/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$out/p$i.log"; }
 done
 python3 - "$out" <<'PY'
 import csv, glob, os, sys, collections
@@ -21,10 +21,12 @@ out = sys.argv[1]
 agg = collections.defaultdict(list)
 for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
-        if "crc32c_batch_kernel" in row.get("Kernel_Name", ""):
-            agg[row["Counter_Name"]].append(float(row["Counter_Value"]))
+        name = row.get("Kernel_Name", "")
+        if "lvk::" in name and "fill_" not in name:
+            short = name.split("(")[0].replace("void ", "")
+            agg[(short, row["Counter_Name"])].append(float(row["Counter_Value"]))
 with open(os.path.join(out, "summary.txt"), "w") as fo:
     for k in sorted(agg):
-        v = sorted(agg[k]); line = f"{k:28s} median {v[len(v)//2]:.6g}  n={len(v)}"
+        v = sorted(agg[k]); line = f"{k[0]:44s} {k[1]:24s} median {v[len(v)//2]:.6g}  n={len(v)}"
         print(line); fo.write(line + "\n")
 PY
