@@ -33,6 +33,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -223,8 +224,7 @@ struct Params {
     uint64_t stride;
     uint32_t blen;
     uint32_t flags;
-    const uint32_t *idx;    // optional: logical i -> buffer idx[i] (sorted list)
-    const uint32_t *count;  // optional: {start, -, -, -, count} of this class's slice
+    const uint4 *ent;       // optional: sorted entries {off lo, off hi, len, buffer index}
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of
@@ -260,10 +260,14 @@ __device__ __forceinline__ Geo make_geo(uint64_t a, uint32_t len, uint32_t seed)
 
 template <int G, bool STRIDED>
 __device__ __forceinline__ Geo fetch_geo(const Params &P, uint64_t i) {
-    const uint64_t b = P.idx ? P.idx[i] : i;
     Geo q;
+    uint64_t b = i;
     if constexpr (STRIDED) {
         q = make_geo<G>(P.base + b * P.stride, P.blen, P.seed ? P.seed[b] : 0u);
+    } else if (P.ent) {  // one sequential 16-B load instead of idx -> off/len
+        const uint4 e = P.ent[i];
+        b = e.w;
+        q = make_geo<G>(P.base + ((static_cast<uint64_t>(e.y) << 32) | e.x), e.z, P.seed ? P.seed[b] : 0u);
     } else {
         q = make_geo<G>(P.base + P.off[b], P.len[b], P.seed ? P.seed[b] : 0u);
     }
@@ -470,10 +474,6 @@ __device__ __forceinline__ void stage_tables(const uint4 *__restrict__ image) {
 
 template <int G, bool STRIDED>
 __global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(Params P, const uint4 *__restrict__ image) {
-    if (P.count) {  // class slice of the sorted list: count[0] = start, count[4] = size
-        P.idx += P.count[0];
-        P.n = P.count[4];
-    }
     // Workgroups without work leave before staging the tables (empty classes).
     if (static_cast<uint64_t>(blockIdx.x) * kWaves * (64 / G) >= P.n) return;
     stage_tables(image);
@@ -581,6 +581,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
 constexpr uint32_t kBuckets = 64;                 // batch-count buckets per class
 constexpr uint32_t kKeys = 4 * kBuckets;
 constexpr uint32_t kSortThreads = 256;
+constexpr uint32_t kSortE = 16;  // elements per thread per register block in the sort passes
 
 __device__ __forceinline__ uint32_t len_class(uint32_t len) {
     return len <= 256u ? 0u : len <= 2048u ? 1u : len <= 32768u ? 2u : 3u;
@@ -588,68 +589,288 @@ __device__ __forceinline__ uint32_t len_class(uint32_t len) {
 
 __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     const uint32_t c = len_class(len);
-    const uint32_t gu16 = 16u * U * (c == 0 ? 1u : c == 1 ? 4u : c == 2 ? 16u : 64u);
+    const uint32_t gu16 = 16u * U * (c == 0 ? 1u : c == 1 ? 4u : 16u);
     uint32_t nb = (len + gu16 - 1) / gu16;  // batches, ignoring start alignment
     nb = nb < kBuckets - 1 ? nb : kBuckets - 1;
     return c * kBuckets + (kBuckets - 1 - nb);
 }
 
-// Pass 1: per-workgroup LDS histogram over a contiguous chunk, one global
-// atomic per nonzero bin per workgroup.
-__global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__restrict__ len, uint64_t n,
-                                                          uint64_t chunk, uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[kKeys];
-    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads) h[k] = 0;
-    __syncthreads();
-    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kSortThreads) atomicAdd(&h[sort_key(len[i])], 1u);
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads)
-        if (h[k]) atomicAdd(&hist[k], h[k]);
+// Sort workspace, 16-B aligned.  Header (u32 words): [0, 256) key
+// histogram -> cursors; [256, 264) class start x4, count x4; [264, 272) class
+// payload bytes, 4 x u64; [272] hist-pass ticket; [273] class-kernel exit
+// ticket; [274, 288) reserved.  Then n sorted 16-B entries.  Every header word
+// is zero between calls: the hist pass resets its ticket, the class kernel the
+// histogram (at its start) and, in its last workgroup out, the byte sums and
+// its ticket.
+constexpr uint32_t kWsCls = kKeys;
+constexpr uint32_t kWsBytes = kKeys + 8;
+constexpr uint32_t kWsTicket = kKeys + 16;
+constexpr uint32_t kWsDone = kKeys + 17;
+constexpr uint32_t kWsHeader = kKeys + 32;
+
+// h[k] += 1 for each valid lane's key k, aggregated per wave: up to four
+// passes over the wave's distinct keys (one LDS atomic per key) -- a uniform
+// batch has one key, and thousands of same-address LDS atomics serialize --
+// then plain per-lane atomics for whatever keys remain.
+__device__ __forceinline__ void wave_count(uint32_t *h, uint32_t k, bool valid, uint32_t lane) {
+    uint64_t rem = __ballot(valid);
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+        if (!rem) return;  // wave-uniform
+        const int leader = __ffsll(static_cast<long long>(rem)) - 1;
+        const uint32_t kl = __shfl(k, leader);
+        const uint64_t m = __ballot(valid && k == kl);
+        if (static_cast<int>(lane) == leader) atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(m)));
+        rem &= ~m;
+    }
+    if ((rem >> lane) & 1ull) atomicAdd(&h[k], 1u);
 }
 
-// Pass 2 (one workgroup): exclusive scan of the key histogram into per-key
-// cursors, plus each class's [start, count) for the class launches.
-__global__ __launch_bounds__(kKeys) void sort_scan(uint32_t *__restrict__ hist, uint32_t *__restrict__ cls) {
-    __shared__ uint32_t v[kKeys];
+// Sum of v over the wave (butterfly), in every lane.
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+// Pass 1: per-workgroup LDS histogram over a contiguous chunk (one global
+// atomic per nonzero bin per workgroup) plus per-class payload bytes; the
+// last workgroup to finish (ticket) scans the histogram into per-key
+// cursors and each class's [start, count).
+__global__ __launch_bounds__(kSortThreads) void sort_hist_scan(const uint32_t *__restrict__ len, uint64_t n,
+                                                               uint64_t chunk, uint32_t *__restrict__ ws) {
+    static_assert(kSortThreads == kKeys, "one thread per key in the scan");
+    __shared__ uint32_t h[kKeys];
+    __shared__ unsigned long long cb[4];
+    __shared__ bool last;
+    uint32_t *hist = ws;
     const uint32_t t = threadIdx.x;
-    v[t] = hist[t];
+    h[t] = 0;
+    if (t < 4) cb[t] = 0;
     __syncthreads();
-    for (uint32_t d = 1; d < kKeys; d <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t x = t >= d ? v[t - d] : 0u;
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    const uint32_t lane = t & 63u;
+    unsigned long long cls_bytes[4] = {0, 0, 0, 0};  // this lane's payload bytes per class
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads * kSortE) {
+        uint32_t l[kSortE];  // all loads of the block first: one memory latency, not kSortE
+#pragma unroll
+        for (uint32_t e = 0; e < kSortE; ++e) {
+            const uint64_t i = b0 + e * kSortThreads + t;
+            l[e] = i < hi ? len[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t e = 0; e < kSortE; ++e) {
+            if (b0 + e * kSortThreads >= hi) break;  // block-uniform
+            const bool valid = b0 + e * kSortThreads + t < hi;
+            wave_count(h, sort_key(l[e]), valid, lane);
+            if (valid) {
+                const uint32_t c = len_class(l[e]);
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) cls_bytes[q] += q == c ? l[e] : 0u;
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const unsigned long long tot = wave_sum64(cls_bytes[q]);
+        if (lane == 0 && tot) atomicAdd(&cb[q], tot);
+    }
+    __syncthreads();
+    if (h[t]) atomicAdd(&hist[t], h[t]);
+    if (t < 4 && cb[t]) atomicAdd(reinterpret_cast<unsigned long long *>(ws + kWsBytes) + t, cb[t]);
+    __threadfence();
+    __syncthreads();
+    if (t == 0) last = atomicAdd(&ws[kWsTicket], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    // Hillis-Steele inclusive scan of the (now complete) histogram
+    const uint32_t mine = __hip_atomic_load(&hist[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h[t] = mine;
+    __syncthreads();
+    for (uint32_t d = 1; d < kKeys; d <<= 1) {
+        const uint32_t x = t >= d ? h[t - d] : 0u;
         __syncthreads();
-        v[t] += x;
+        h[t] += x;
         __syncthreads();
     }
-    const uint32_t excl = v[t] - hist[t];
+    const uint32_t excl = h[t] - mine;
     hist[t] = excl;  // becomes the global cursor of key t
     if (t % kBuckets == 0) {
         const uint32_t c = t / kBuckets;
-        cls[c] = excl;                                     // start
-        cls[4 + c] = v[t + kBuckets - 1] - excl;           // count
+        ws[kWsCls + c] = excl;                            // start
+        ws[kWsCls + 4 + c] = h[t + kBuckets - 1] - excl;  // count
+    }
+    if (t == 0) ws[kWsTicket] = 0;
+}
+
+// Pass 2: same chunks as pass 1.  Each workgroup reserves its keys' ranges
+// (one atomic per nonzero key), then places its buffers STABLY -- input order
+// within a key -- in rounds of 256: a buffer's slot is its key's running
+// position + same-key buffers of earlier waves in the round + its rank among
+// same-key lanes of its wave (ballot over the wave's distinct keys).  Stable
+// order keeps a class's metadata reads and CRC stores sequential (a uniform
+// batch sorts to the identity).  Entries carry off/len/index so the CRC
+// kernel reads one sequential 16-B record per buffer.
+__global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__restrict__ off,
+                                                             const uint32_t *__restrict__ len, uint64_t n,
+                                                             uint64_t chunk, uint32_t *__restrict__ cursor,
+                                                             uint4 *__restrict__ ent) {
+    constexpr uint32_t kW = kSortThreads / 64;
+    __shared__ uint32_t h[kKeys];       // chunk counts, then running slot per key
+    __shared__ uint32_t wc[kW][kKeys];  // per-wave key counts of the current round
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    h[t] = 0;
+    for (uint32_t v = 0; v < kW; ++v) wc[v][t] = 0;
+    __syncthreads();
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads * kSortE) {
+        uint32_t l[kSortE];
+#pragma unroll
+        for (uint32_t e = 0; e < kSortE; ++e) {
+            const uint64_t i = b0 + e * kSortThreads + t;
+            l[e] = i < hi ? len[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t e = 0; e < kSortE; ++e) {
+            if (b0 + e * kSortThreads >= hi) break;  // block-uniform
+            const bool valid = b0 + e * kSortThreads + t < hi;
+            wave_count(h, sort_key(l[e]), valid, t & 63u);
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = h[t];
+    h[t] = cnt ? atomicAdd(&cursor[t], cnt) : 0u;
+    __syncthreads();
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads * kSortE) {
+      // this block's lengths and offsets, all loads issued before any use
+      uint32_t lb[kSortE];
+      uint64_t ob[kSortE];
+#pragma unroll
+      for (uint32_t e = 0; e < kSortE; ++e) {
+          const uint64_t i = b0 + e * kSortThreads + t;
+          lb[e] = i < hi ? len[i] : 0u;
+          ob[e] = i < hi ? off[i] : 0u;
+      }
+#pragma unroll
+      for (uint32_t e = 0; e < kSortE; ++e) {
+        const uint64_t r0 = b0 + e * kSortThreads;
+        if (r0 >= hi) break;  // block-uniform
+        const uint64_t i = r0 + t;
+        const bool valid = i < hi;
+        const uint32_t l = lb[e];
+        const uint32_t k = valid ? sort_key(l) : 0u;
+        uint64_t rem = __ballot(valid);
+        uint32_t rank = 0;
+        while (rem) {  // wave-uniform: one pass per distinct key in the wave
+            const int leader = __ffsll(static_cast<long long>(rem)) - 1;
+            const uint32_t kl = __shfl(k, leader);
+            const uint64_t m = __ballot(valid && k == kl);
+            if (valid && k == kl) rank = __popcll(m & ((1ull << lane) - 1ull));
+            if (static_cast<int>(lane) == leader) wc[w][kl] = __popcll(m);
+            rem &= ~m;
+        }
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = h[k] + rank;
+            for (uint32_t v = 0; v < w; ++v) pos += wc[v][k];
+            const uint64_t o = ob[e];
+            ent[pos] = make_uint4(static_cast<uint32_t>(o), static_cast<uint32_t>(o >> 32), l,
+                                  static_cast<uint32_t>(i));
+        }
+        __syncthreads();
+        uint32_t add = 0;
+        for (uint32_t v = 0; v < kW; ++v) {
+            add += wc[v][t];
+            wc[v][t] = 0;
+        }
+        h[t] += add;
+        __syncthreads();
+      }
     }
 }
 
-// Pass 3: same chunks as pass 1; each workgroup reserves its bins' ranges
-// with one atomic per bin, then places its buffers by LDS-atomic rank.
-__global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint32_t *__restrict__ len, uint64_t n,
-                                                             uint64_t chunk, uint32_t *__restrict__ cursor,
-                                                             uint32_t *__restrict__ list) {
-    __shared__ uint32_t h[kKeys];
-    __shared__ uint32_t base[kKeys];
-    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads) h[k] = 0;
-    __syncthreads();
-    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kSortThreads) atomicAdd(&h[sort_key(len[i])], 1u);
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kKeys; k += kSortThreads) {
-        base[k] = h[k] ? atomicAdd(&cursor[k], h[k]) : 0u;
-        h[k] = 0;
+// Length classes of the offsets API in ONE persistent launch.  The sorted
+// entries hold class 0..3 runs (G = 1, 4, 16, 16).  Each workgroup takes the
+// class given by a static split of the grid proportional to each class's
+// estimated work (payload bytes + buf_cost per buffer; every nonempty class
+// gets at least one workgroup), stages that class's LDS image and walks the
+// class exactly as a standalone launch of its share would (the entries are
+// sorted by batch count within a class, so the round-robin is balanced).
+// Small, latency-bound classes thus run beside the bandwidth-bound ones
+// instead of in launches of their own.  (Letting a workgroup move on to
+// another class once its own runs dry needs the class bodies inside a loop,
+// which costs ~30 spilled VGPRs; per-slice atomic work grabbing measured
+// slower: 4096 waves contending on one counter.)
+constexpr uint32_t kBufCost = 2048;  // default bytes-equivalent cost of one buffer
+
+struct Images {
+    const uint4 *img[4];
+    uint32_t buf_cost;
+};
+
+template <int G>
+__device__ __forceinline__ void run_class(const Params &P0, uint32_t start, uint32_t count, uint32_t r,
+                                          uint32_t nwg, uint32_t lane, const Lut &L) {
+    constexpr uint32_t kGroups = 64 / G;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    Params P = P0;
+    P.ent = P0.ent + start;
+    P.n = count;
+    const uint64_t gid = (static_cast<uint64_t>(r) * kWaves + wave) * kGroups + lane / G;
+    const uint64_t gstride = static_cast<uint64_t>(nwg) * kWaves * kGroups;
+    group_stream<G, false>(P, gid, gstride, lane % G, L);
+}
+
+__global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, Images im, uint32_t *ws) {
+    const uint32_t *cls = ws + kWsCls;
+    const unsigned long long *cbytes = reinterpret_cast<const unsigned long long *>(ws + kWsBytes);
+    if (blockIdx.x == 0 && threadIdx.x < kKeys) ws[threadIdx.x] = 0;  // histogram, for the next call
+    uint64_t w[4], W = 0;
+    int nz = 0;
+    for (int k = 0; k < 4; ++k) {
+        w[k] = cls[4 + k] ? cbytes[k] + static_cast<uint64_t>(cls[4 + k]) * im.buf_cost : 0;
+        W += w[k];
+        nz += cls[4 + k] ? 1 : 0;
+    }
+    const uint32_t grid = gridDim.x;
+    const uint32_t spare = grid > static_cast<uint32_t>(nz) ? grid - nz : 0;
+    uint32_t nwg[4], assigned = 0;
+    int big = -1;
+    for (int k = 0; k < 4; ++k) {
+        nwg[k] = cls[4 + k] ? 1 + static_cast<uint32_t>(static_cast<double>(spare) * static_cast<double>(w[k]) / W)
+                            : 0;
+        assigned += nwg[k];
+        if (cls[4 + k] && (big < 0 || w[k] > w[big])) big = k;
+    }
+    if (big >= 0) nwg[big] += grid - assigned;  // rounding leftovers: the class with the most work
+    int c = -1;
+    uint32_t first = 0, r = 0;
+    for (int k = 0; k < 4 && c < 0; ++k) {
+        if (blockIdx.x < first + nwg[k]) {
+            c = k;
+            r = blockIdx.x - first;
+        }
+        first += nwg[k];
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const Lut L = make_lut(lane);
+    if (c >= 0) {
+        stage_tables(im.img[c]);
+        const uint32_t start = cls[c], count = cls[4 + c];
+        switch (c) {
+            case 0: run_class<1>(P, start, count, r, nwg[0], lane, L); break;
+            case 1: run_class<4>(P, start, count, r, nwg[1], lane, L); break;
+            default: run_class<16>(P, start, count, r, nwg[c], lane, L); break;
+        }
     }
     __syncthreads();
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kSortThreads) {
-        const uint32_t k = sort_key(len[i]);
-        list[base[k] + atomicAdd(&h[k], 1u)] = static_cast<uint32_t>(i);
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&ws[kWsDone], 1u) == grid - 1) {  // last workgroup out
+            unsigned long long *cb = reinterpret_cast<unsigned long long *>(ws + kWsBytes);
+            for (int k = 0; k < 4; ++k) cb[k] = 0;
+            ws[kWsDone] = 0;
+        }
     }
 }
 
@@ -737,6 +958,7 @@ struct DevCtx {
     bool ready = false;
     int cus = 0;
     uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t buf_cost = lvk::kBufCost;  // class-split cost per buffer (LVGPU_BUF_COST overrides, tuning)
     // offsets-API sort workspace, one per stream (calls on one stream are
     // stream-ordered, so reusing its buffer is safe; different streams never share)
     std::mutex ws_m;
@@ -820,6 +1042,7 @@ int current_ctx(DevCtx **out) {
         hipDeviceProp_t prop;
         LV_HIP(hipGetDeviceProperties(&prop, dev));
         c.cus = prop.multiProcessorCount;
+        if (const char *e = std::getenv("LVGPU_BUF_COST")) c.buf_cost = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
         for (int i = 0; i < 4; ++i) {
             const auto &im = host_image(i);
             LV_HIP(hipMalloc(&c.image[i], im.size() * 4));
@@ -848,8 +1071,7 @@ int forced_gi(uint32_t flags) {
 template <int G, bool STRIDED>
 void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off,
                 const uint32_t *len, uint64_t stride, uint32_t blen, const uint32_t *seed,
-                uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s,
-                const uint32_t *idx = nullptr, const uint32_t *count = nullptr) {
+                uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
     const uint64_t groups_per_wg = static_cast<uint64_t>(lvk::kWaves) * (64 / G);
     uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
     if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
@@ -864,8 +1086,7 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
     P.stride = stride;
     P.blen = blen;
     P.flags = flags;
-    P.idx = idx;
-    P.count = count;
+    P.ent = nullptr;
     hipLaunchKernelGGL((lvk::crc32c_batch_kernel<G, STRIDED>), dim3(static_cast<uint32_t>(grid)),
                        dim3(lvk::kThreads), 0, s, P, c.image[gi]);
 }
@@ -873,20 +1094,20 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
 template <bool STRIDED>
 void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off,
               const uint32_t *len, uint64_t stride, uint32_t blen, const uint32_t *seed,
-              uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s,
-              const uint32_t *idx = nullptr, const uint32_t *count = nullptr) {
+              uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
     switch (gi) {
-        case 0: launch_one<1, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
-        case 1: launch_one<4, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
-        case 2: launch_one<16, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
-        default: launch_one<64, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s, idx, count); break;
+        case 0: launch_one<1, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
+        case 1: launch_one<4, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
+        case 2: launch_one<16, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
+        default: launch_one<64, STRIDED>(c, gi, arena, off, len, stride, blen, seed, out, n, flags, s); break;
     }
 }
 
 // Bytes of sort workspace the offsets API needs for n buffers.
-size_t sort_ws_bytes(uint64_t n) { return (lvk::kKeys + 8) * sizeof(uint32_t) + n * sizeof(uint32_t); }
+size_t sort_ws_bytes(uint64_t n) { return lvk::kWsHeader * sizeof(uint32_t) + n * sizeof(uint4); }
 
-// The library-owned workspace of (device, stream), grown on demand.
+// The library-owned workspace of (device, stream), grown on demand; its
+// header is zeroed when allocated and every call leaves it zero again.
 int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out) {
     std::lock_guard<std::mutex> lk(c.ws_m);
     auto &w = c.ws[s];
@@ -896,31 +1117,43 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out) {
         w.first = nullptr;
         w.second = 0;
         LV_HIP(hipMalloc(&w.first, need));
+        LV_HIP(hipMemsetAsync(w.first, 0, lvk::kWsHeader * sizeof(uint32_t), s));
         w.second = need;
     }
     *out = w.first;
     return 0;
 }
 
-// Length-sorted launch of the offsets API: histogram, scan and scatter over
-// len[] (one sorted index list), then one launch per class reading its slice
-// of the list and its count from device memory (no host sync).
-int launch_binned(DevCtx &c, uint8_t *ws, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+// Length-sorted launch of the offsets API, three kernels and no host sync:
+// histogram + scan (last workgroup), stable scatter into sorted entries, then
+// the persistent class kernel over all four length classes.
+int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                   const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
-    uint32_t *hist = reinterpret_cast<uint32_t *>(ws);
-    uint32_t *cls = hist + lvk::kKeys;  // [start x4, count x4]
-    uint32_t *list = cls + 8;
-    LV_HIP(hipMemsetAsync(hist, 0, lvk::kKeys * sizeof(uint32_t), s));
-    uint64_t wgs = (n + 4095) / 4096;  // ~4096 buffers per sorting workgroup
-    if (wgs > 2048) wgs = 2048;
+    uint32_t *ws = reinterpret_cast<uint32_t *>(ws_bytes);
+    uint4 *ent = reinterpret_cast<uint4 *>(ws + lvk::kWsHeader);
+    uint64_t wgs = (n + 2047) / 2048;  // ~2048 buffers per sorting workgroup: 8 per thread
+    if (wgs > 4096) wgs = 4096;
     const uint64_t chunk = (n + wgs - 1) / wgs;
-    hipLaunchKernelGGL(lvk::sort_hist, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, len, n,
-                       chunk, hist);
-    hipLaunchKernelGGL(lvk::sort_scan, dim3(1), dim3(lvk::kKeys), 0, s, hist, cls);
-    hipLaunchKernelGGL(lvk::sort_scatter, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, len, n,
-                       chunk, hist, list);
-    for (int k = 0; k < 4; ++k)
-        launch_g<false>(c, k, arena, off, len, 0, 0, seed, out, n, flags, s, list, cls + k);
+    hipLaunchKernelGGL(lvk::sort_hist_scan, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, len,
+                       n, chunk, ws);
+    hipLaunchKernelGGL(lvk::sort_scatter, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, off, len,
+                       n, chunk, ws, ent);
+    lvk::Params P;
+    P.base = reinterpret_cast<uint64_t>(arena);
+    P.off = off;
+    P.len = len;
+    P.seed = seed;
+    P.out = out;
+    P.n = n;
+    P.stride = 0;
+    P.blen = 0;
+    P.flags = flags;
+    P.ent = ent;
+    lvk::Images im;
+    for (int k = 0; k < 4; ++k) im.img[k] = c.image[k < 3 ? k : 2];  // class 3 runs with G = 16
+    im.buf_cost = c.buf_cost;
+    hipLaunchKernelGGL(lvk::crc32c_classes_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0, s, P,
+                       im, ws);
     return 0;
 }
 
@@ -1010,6 +1243,8 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
     }
     if (d_ws) {
         if (ws_bytes < sort_ws_bytes(n)) return set_err(LV_ERR_INVALID, "workspace too small");
+        if (reinterpret_cast<uintptr_t>(d_ws) % 16) return set_err(LV_ERR_INVALID, "workspace must be 16-byte aligned");
+        LV_HIP(hipMemsetAsync(d_ws, 0, lvk::kWsHeader * sizeof(uint32_t), s));  // caller's header: any state
     } else if (int rc = stream_ws(*c, s, n, &d_ws)) {
         return rc;
     }
