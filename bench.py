@@ -77,8 +77,13 @@ def build_workload(torch, lvgpu, name, dev, rank, blocks=None):
         desc = f"{name}: {n} x {bl} B SSTable blocks per GPU ({n * bl / 2**30:.0f} GiB), offsets i*{bl}, seed 0"
         return arena, off, ln, n * bl, desc
     rng = np.random.default_rng(0xC0FFEE + rank)
-    if name == "c4":  # Zipf(1.1) multiples of 32 B on 1..2048, shuffled
-        k = np.minimum(rng.zipf(1.1, size=1048576), 2048)
+    if name == "c4":  # Zipf(1.1) multiples of 32 B, truncated to 1..2048 (not clipped:
+        # clipping rng.zipf at 2048 would pile ~44% of the mass onto 64 KiB)
+        kk = np.arange(1, 2049, dtype=np.float64)
+        cdf = np.cumsum(kk ** -1.1)
+        cdf /= cdf[-1]
+        k = np.searchsorted(cdf, rng.random(1048576), side="right") + 1
+        k = np.minimum(k, 2048)
         lens = (32 * k).astype(np.uint32)
         desc = "c4: 1,048,576 buffers, L = 32*k, k ~ Zipf(1.1) on 1..2048, byte-packed"
     else:  # c2: WAL physical records from Random(301).skewed(17) record sizes

@@ -94,6 +94,20 @@ __device__ __forceinline__ uint32_t lds_word(uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(g_lds) + byte_addr);
 }
 
+// a ^ b ^ c in ONE v_bitop3_b32 (gfx950; truth table 0x96).  The lookup XOR
+// trees are most of the kernel's VALU work, and VALU issue (4 cycles per
+// wave64 instruction per SIMD) is one of the resources that bound it.
+#ifndef LVK_XOR3
+#define LVK_XOR3 1
+#endif
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if LVK_XOR3
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 // XOR of the four Latin tables at byte offset OFF indexed by the bytes of s.
 // OFF = 0 is one slice-by-4 step T3[b0]^T2[b1]^T1[b2]^T0[b3]; the shift
 // regions hold S[3-k] at table slot k so the same selectors index them.
@@ -103,15 +117,25 @@ __device__ __forceinline__ uint32_t lookup4(uint32_t s, const Lut &L) {
     const uint32_t a1 = __builtin_amdgcn_perm(s, L.lv, L.sel1);
     const uint32_t a2 = __builtin_amdgcn_perm(s, L.lv, L.sel2);
     const uint32_t a3 = __builtin_amdgcn_perm(s, L.lv, L.sel3);
-    return lds_word(a0 + OFF) ^ lds_word(a1 + OFF) ^ lds_word(a2 + OFF) ^ lds_word(a3 + OFF);
+    return xor3(lds_word(a0 + OFF), lds_word(a1 + OFF), lds_word(a2 + OFF)) ^ lds_word(a3 + OFF);
+}
+
+// lookup4 ^ x with two 3-input XORs.
+template <uint32_t OFF>
+__device__ __forceinline__ uint32_t lookup4x(uint32_t s, uint32_t x, const Lut &L) {
+    const uint32_t a0 = __builtin_amdgcn_perm(s, L.lv, L.sel0);
+    const uint32_t a1 = __builtin_amdgcn_perm(s, L.lv, L.sel1);
+    const uint32_t a2 = __builtin_amdgcn_perm(s, L.lv, L.sel2);
+    const uint32_t a3 = __builtin_amdgcn_perm(s, L.lv, L.sel3);
+    return xor3(xor3(lds_word(a0 + OFF), lds_word(a1 + OFF), lds_word(a2 + OFF)), lds_word(a3 + OFF), x);
 }
 
 // R(0, 16 bytes of v): four slice-by-4 steps.
 __device__ __forceinline__ uint32_t r0_granule(uint4 v, const Lut &L) {
-    uint32_t s = lookup4<kRegionA>(v.x, L);
-    s = lookup4<kRegionA>(s ^ v.y, L);
-    s = lookup4<kRegionA>(s ^ v.z, L);
-    return lookup4<kRegionA>(s ^ v.w, L);
+    uint32_t s = lookup4x<kRegionA>(v.x, v.y, L);
+    s = lookup4x<kRegionA>(s, v.z, L);
+    s = lookup4x<kRegionA>(s, v.w, L);
+    return lookup4<kRegionA>(s, L);
 }
 
 // Address of lookup i of state s (one v_perm_b32).
@@ -128,7 +152,7 @@ __device__ __forceinline__ uint32_t lut_addr(uint32_t s, const Lut &L) {
 // (or A[i] = p[i] when FIRST).
 template <bool FIRST>
 __device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U], const Lut &L) {
-    uint32_t s[U], w[U];
+    uint32_t s[U], w[U], w3[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) s[i] = v[i].x;
     if constexpr (!FIRST) {
@@ -141,9 +165,11 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U]
             aa[i][3] = lut_addr<3>(A[i], L);
         }
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i)
-            w[i] = lds_word(aa[i][0] + kRegionA + kHalf) ^ lds_word(aa[i][1] + kRegionA + kHalf) ^
-                   lds_word(aa[i][2] + kRegionA + kHalf) ^ lds_word(aa[i][3] + kRegionA + kHalf);
+        for (uint32_t i = 0; i < U; ++i) {
+            w[i] = xor3(lds_word(aa[i][0] + kRegionA + kHalf), lds_word(aa[i][1] + kRegionA + kHalf),
+                        lds_word(aa[i][2] + kRegionA + kHalf));
+            w3[i] = lds_word(aa[i][3] + kRegionA + kHalf);
+        }
     }
 #pragma unroll
     for (uint32_t step = 0; step < 4; ++step) {
@@ -162,12 +188,17 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U]
             for (uint32_t k = 0; k < 4; ++k) t[i][k] = lds_word(ad[i][k] + kRegionA);
 #pragma unroll
         for (uint32_t i = 0; i < U; ++i) {
-            const uint32_t nw = step == 0 ? v[i].y : step == 1 ? v[i].z : step == 2 ? v[i].w : 0u;
-            s[i] = (t[i][0] ^ t[i][1]) ^ (t[i][2] ^ t[i][3]) ^ nw;
+            const uint32_t x = xor3(t[i][0], t[i][1], t[i][2]);
+            if (step < 3) {
+                const uint32_t nw = step == 0 ? v[i].y : step == 1 ? v[i].z : v[i].w;
+                s[i] = xor3(x, t[i][3], nw);
+            } else if constexpr (FIRST) {
+                A[i] = x ^ t[i][3];
+            } else {  // A = W4(A) ^ R(0, granule): 8 terms in four ops
+                A[i] = x ^ xor3(t[i][3], w[i], w3[i]);
+            }
         }
     }
-#pragma unroll
-    for (uint32_t i = 0; i < U; ++i) A[i] = FIRST ? s[i] : (w[i] ^ s[i]);
 }
 
 // Shift_{16*2^k}(a) from the plain combine tables.
@@ -210,6 +241,22 @@ __device__ __forceinline__ uint4 load16(uint64_t addr) {
     return to_uint4(__builtin_nontemporal_load(reinterpret_cast<g_u32x4 *>(addr)));
 }
 
+// Default-policy (L2-allocating) 16-B load.
+__device__ __forceinline__ uint4 load16_rt(uint64_t addr) {
+    return to_uint4(*reinterpret_cast<g_u32x4 *>(addr));
+}
+
+// Row loads of the general kernels: non-temporal, except the last row of a
+// batch, whose last 128-B line the next batch's first row shares when the
+// buffer end is not line aligned (rows are aligned to the buffer END): a
+// default-policy load keeps that line in L2 for the second reader (C2 HBM
+// traffic 1.146x -> 1.045x of the payload).
+template <uint32_t I>
+__device__ __forceinline__ uint4 load_row(uint64_t addr) {
+    if constexpr (I == U - 1) return load16_rt(addr);
+    return load16(addr);
+}
+
 __device__ __forceinline__ uint32_t mask_crc(uint32_t c) {  // crc32c.rs:54-57
     return ((c >> 15) | (c << 17)) + 0xa282ead8u;
 }
@@ -225,6 +272,7 @@ struct Params {
     uint32_t blen;
     uint32_t flags;
     const uint4 *ent;       // optional: sorted entries {off lo, off hi, len, buffer index}
+    const uint32_t *sseed;  // optional: seeds in sorted-entry order
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of
@@ -280,8 +328,10 @@ template <int G>
 __device__ __forceinline__ void load_batch(const Geo &q, uint32_t j, uint32_t gl, uint4 (&v)[U]) {
     const int32_t d = q.hoff + static_cast<int32_t>(G * U * j + gl);
     const uint64_t p = q.abase + (static_cast<int64_t>(d) << 4);
-#pragma unroll
-    for (uint32_t i = 0; i < U; ++i) v[i] = load16(p + 16u * G * i);
+    v[0] = load_row<0>(p);
+    v[1] = load_row<1>(p + 16u * G);
+    v[2] = load_row<2>(p + 32u * G);
+    v[3] = load_row<3>(p + 48u * G);
 }
 
 // Batch 0: rows before the buffer are clamped to granule g0 (a valid
@@ -292,7 +342,8 @@ __device__ __forceinline__ void load_batch0(const Geo &q, uint32_t gl, uint4 (&v
     for (uint32_t i = 0; i < U; ++i) {
         int32_t d = q.hoff + static_cast<int32_t>(G * i + gl);
         d = d < 0 ? 0 : d;
-        v[i] = load16(q.abase + (static_cast<uint32_t>(d) << 4));
+        const uint64_t a = q.abase + (static_cast<uint32_t>(d) << 4);
+        v[i] = i == U - 1 ? load16_rt(a) : load16(a);
     }
 }
 
@@ -595,18 +646,20 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     return c * kBuckets + (kBuckets - 1 - nb);
 }
 
-// Sort workspace, 16-B aligned.  Header (u32 words): [0, 256) key
-// histogram -> cursors; [256, 264) class start x4, count x4; [264, 272) class
-// payload bytes, 4 x u64; [272] hist-pass ticket; [273] class-kernel exit
-// ticket; [274, 288) reserved.  Then n sorted 16-B entries.  Every header word
-// is zero between calls: the hist pass resets its ticket, the class kernel the
-// histogram (at its start) and, in its last workgroup out, the byte sums and
-// its ticket.
+// Sort workspace, 16-B aligned.  Header (u32 words): [0, 256) key start
+// (cursor base) per key; [256, 264) class start x4, count x4; [264, 520)
+// per-key totals; [520] scan ticket (zero between calls: the last scan
+// workgroup resets it).  Then the per-workgroup histogram matrix M[wgs][256],
+// then n sorted 16-B entries, then n seeds in entry order.
 constexpr uint32_t kWsCls = kKeys;
-constexpr uint32_t kWsBytes = kKeys + 8;
-constexpr uint32_t kWsTicket = kKeys + 16;
-constexpr uint32_t kWsDone = kKeys + 17;
-constexpr uint32_t kWsHeader = kKeys + 32;
+constexpr uint32_t kWsTot = kKeys + 8;
+constexpr uint32_t kWsTicket = kWsTot + kKeys;
+constexpr uint32_t kWsHeader = kWsTicket + 8;  // 528 words, 16-B multiple
+constexpr uint32_t kSortChunk = kSortThreads * kSortE;  // elements per sorting workgroup (n <= 4M)
+constexpr uint32_t kSortMaxWgs = 1024;
+constexpr uint32_t kScanWgs = kKeys / 16;  // 16 keys per scan workgroup
+constexpr uint32_t kScanThreads = 1024;    // 16 keys x 64 row ranges
+static_assert(kSortMaxWgs <= 64 * 16, "scan: 64 row ranges of <= 16 rows");
 
 // h[k] += 1 for each valid lane's key k, aggregated per wave: up to four
 // passes over the wave's distinct keys (one LDS atomic per key) -- a uniform
@@ -626,32 +679,39 @@ __device__ __forceinline__ void wave_count(uint32_t *h, uint32_t k, bool valid, 
     if ((rem >> lane) & 1ull) atomicAdd(&h[k], 1u);
 }
 
-// Sum of v over the wave (butterfly), in every lane.
-__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+// Like wave_count, but returns each valid lane's claimed slot h[k]++.
+__device__ __forceinline__ uint32_t wave_claim(uint32_t *h, uint32_t k, bool valid, uint32_t lane) {
+    uint64_t rem = __ballot(valid);
+    uint32_t pos = 0;
+    const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d);
-    return v;
+    for (int pass = 0; pass < 4; ++pass) {
+        if (!rem) return pos;  // wave-uniform
+        const int leader = __ffsll(static_cast<long long>(rem)) - 1;
+        const uint32_t kl = __shfl(k, leader);
+        const uint64_t m = __ballot(valid && k == kl);
+        uint32_t base = 0;
+        if (static_cast<int>(lane) == leader) base = atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(m)));
+        base = __shfl(base, leader);
+        if (valid && k == kl) pos = base + static_cast<uint32_t>(__popcll(m & below));
+        rem &= ~m;
+    }
+    if ((rem >> lane) & 1ull) pos = atomicAdd(&h[k], 1u);
+    return pos;
 }
 
-// Pass 1: per-workgroup LDS histogram over a contiguous chunk (one global
-// atomic per nonzero bin per workgroup) plus per-class payload bytes; the
-// last workgroup to finish (ticket) scans the histogram into per-key
-// cursors and each class's [start, count).
-__global__ __launch_bounds__(kSortThreads) void sort_hist_scan(const uint32_t *__restrict__ len, uint64_t n,
-                                                               uint64_t chunk, uint32_t *__restrict__ ws) {
-    static_assert(kSortThreads == kKeys, "one thread per key in the scan");
+// Pass 1: per-workgroup key histogram of a contiguous chunk, in LDS, stored
+// as row blockIdx.x of M.  No global atomics: same-address device atomics
+// from hundreds of workgroups serialize (one key for a uniform batch).
+__global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__restrict__ len, uint64_t n,
+                                                          uint64_t chunk, uint32_t *__restrict__ M) {
+    static_assert(kSortThreads == kKeys, "one thread per key");
     __shared__ uint32_t h[kKeys];
-    __shared__ unsigned long long cb[4];
-    __shared__ bool last;
-    uint32_t *hist = ws;
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = t & 63u;
     h[t] = 0;
-    if (t < 4) cb[t] = 0;
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    const uint32_t lane = t & 63u;
-    unsigned long long cls_bytes[4] = {0, 0, 0, 0};  // this lane's payload bytes per class
-    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads * kSortE) {
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortChunk) {
         uint32_t l[kSortE];  // all loads of the block first: one memory latency, not kSortE
 #pragma unroll
         for (uint32_t e = 0; e < kSortE; ++e) {
@@ -661,216 +721,421 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist_scan(const uint32_t *_
 #pragma unroll
         for (uint32_t e = 0; e < kSortE; ++e) {
             if (b0 + e * kSortThreads >= hi) break;  // block-uniform
-            const bool valid = b0 + e * kSortThreads + t < hi;
-            wave_count(h, sort_key(l[e]), valid, lane);
-            if (valid) {
-                const uint32_t c = len_class(l[e]);
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) cls_bytes[q] += q == c ? l[e] : 0u;
-            }
+            wave_count(h, sort_key(l[e]), b0 + e * kSortThreads + t < hi, lane);
         }
     }
+    __syncthreads();
+    M[static_cast<uint64_t>(blockIdx.x) * kKeys + t] = h[t];
+}
+
+// Pass 2: column scan of M.  Workgroup b owns keys [16b, 16b+16); thread
+// (sub, kl) sums rows [sub*R, sub*R+R) of key 16b+kl, the 64 partial sums
+// are scanned in LDS, and M[w][k] becomes the offset of workgroup w's first
+// key-k entry within key k.  The last workgroup (ticket; 16 arrivals) scans
+// the key totals into key starts and per-class [start, count).
+__global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__ M, uint32_t wgs,
+                                                          uint32_t *__restrict__ ws) {
+    __shared__ uint32_t part[64][16];
+    __shared__ uint32_t sc[kKeys];
+    __shared__ bool last;
+    const uint32_t t = threadIdx.x, kl = t & 15u, sub = t >> 4;
+    const uint32_t k = blockIdx.x * 16u + kl;
+    const uint32_t R = (wgs + 63u) / 64u;  // <= 16
+    const uint32_t r0 = sub * R;
+    uint32_t v[16];
+    uint32_t sum = 0;
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const unsigned long long tot = wave_sum64(cls_bytes[q]);
-        if (lane == 0 && tot) atomicAdd(&cb[q], tot);
+    for (uint32_t r = 0; r < 16; ++r) {
+        v[r] = (r < R && r0 + r < wgs) ? M[static_cast<uint64_t>(r0 + r) * kKeys + k] : 0u;
+        sum += v[r];
+    }
+    part[sub][kl] = sum;
+    __syncthreads();
+    if (sub == 0) {
+        uint32_t run = 0;
+        for (uint32_t q = 0; q < 64; ++q) {
+            const uint32_t x = part[q][kl];
+            part[q][kl] = run;
+            run += x;
+        }
+        ws[kWsTot + k] = run;
     }
     __syncthreads();
-    if (h[t]) atomicAdd(&hist[t], h[t]);
-    if (t < 4 && cb[t]) atomicAdd(reinterpret_cast<unsigned long long *>(ws + kWsBytes) + t, cb[t]);
+    uint32_t run = part[sub][kl];
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r) {
+        if (r < R && r0 + r < wgs) M[static_cast<uint64_t>(r0 + r) * kKeys + k] = run;
+        run += v[r];
+    }
     __threadfence();
     __syncthreads();
     if (t == 0) last = atomicAdd(&ws[kWsTicket], 1u) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
-    // Hillis-Steele inclusive scan of the (now complete) histogram
-    const uint32_t mine = __hip_atomic_load(&hist[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h[t] = mine;
+    __threadfence();
+    uint32_t mine = 0;
+    if (t < kKeys) {
+        mine = __hip_atomic_load(&ws[kWsTot + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sc[t] = mine;
+    }
     __syncthreads();
-    for (uint32_t d = 1; d < kKeys; d <<= 1) {
-        const uint32_t x = t >= d ? h[t - d] : 0u;
+    for (uint32_t d = 1; d < kKeys; d <<= 1) {  // Hillis-Steele inclusive scan
+        uint32_t x = 0;
+        if (t < kKeys && t >= d) x = sc[t - d];
         __syncthreads();
-        h[t] += x;
+        if (t < kKeys) sc[t] += x;
         __syncthreads();
     }
-    const uint32_t excl = h[t] - mine;
-    hist[t] = excl;  // becomes the global cursor of key t
-    if (t % kBuckets == 0) {
-        const uint32_t c = t / kBuckets;
-        ws[kWsCls + c] = excl;                            // start
-        ws[kWsCls + 4 + c] = h[t + kBuckets - 1] - excl;  // count
+    if (t < kKeys) {
+        const uint32_t excl = sc[t] - mine;
+        ws[t] = excl;
+        if (t % kBuckets == 0) {
+            const uint32_t c = t / kBuckets;
+            ws[kWsCls + c] = excl;                             // start
+            ws[kWsCls + 4 + c] = sc[t + kBuckets - 1] - excl;  // count
+        }
     }
     if (t == 0) ws[kWsTicket] = 0;
 }
 
-// Pass 2: same chunks as pass 1.  Each workgroup reserves its keys' ranges
-// (one atomic per nonzero key), then places its buffers STABLY -- input order
-// within a key -- in rounds of 256: a buffer's slot is its key's running
-// position + same-key buffers of earlier waves in the round + its rank among
-// same-key lanes of its wave (ballot over the wave's distinct keys).  Stable
-// order keeps a class's metadata reads and CRC stores sequential (a uniform
-// batch sorts to the identity).  Entries carry off/len/index so the CRC
-// kernel reads one sequential 16-B record per buffer.
+// Pass 3: same chunks as pass 1.  Workgroup w's slots for key k start at
+// key_start[k] + M[w][k]; buffers claim them with wave-aggregated LDS
+// atomics (order within a workgroup's run is not stable, which keeps metadata
+// reads and CRC stores within one 4096-buffer window).  Entries carry
+// off/len/index so the CRC kernel reads one 16-B record per buffer; seeds are
+// permuted alongside.
 __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__restrict__ off,
                                                              const uint32_t *__restrict__ len, uint64_t n,
-                                                             uint64_t chunk, uint32_t *__restrict__ cursor,
-                                                             uint4 *__restrict__ ent) {
-    constexpr uint32_t kW = kSortThreads / 64;
-    __shared__ uint32_t h[kKeys];       // chunk counts, then running slot per key
-    __shared__ uint32_t wc[kW][kKeys];  // per-wave key counts of the current round
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    h[t] = 0;
-    for (uint32_t v = 0; v < kW; ++v) wc[v][t] = 0;
+                                                             uint64_t chunk, const uint32_t *__restrict__ ws,
+                                                             const uint32_t *__restrict__ M,
+                                                             uint4 *__restrict__ ent,
+                                                             const uint32_t *__restrict__ seed,
+                                                             uint32_t *__restrict__ sseed) {
+    __shared__ uint32_t cur[kKeys];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    cur[t] = ws[t] + M[static_cast<uint64_t>(blockIdx.x) * kKeys + t];
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads * kSortE) {
-        uint32_t l[kSortE];
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortChunk) {
+        uint32_t lb[kSortE];
+        uint64_t ob[kSortE];
 #pragma unroll
         for (uint32_t e = 0; e < kSortE; ++e) {
             const uint64_t i = b0 + e * kSortThreads + t;
-            l[e] = i < hi ? len[i] : 0u;
+            lb[e] = i < hi ? len[i] : 0u;
+            ob[e] = i < hi ? off[i] : 0u;
         }
 #pragma unroll
         for (uint32_t e = 0; e < kSortE; ++e) {
-            if (b0 + e * kSortThreads >= hi) break;  // block-uniform
-            const bool valid = b0 + e * kSortThreads + t < hi;
-            wave_count(h, sort_key(l[e]), valid, t & 63u);
+            const uint64_t r0 = b0 + e * kSortThreads;
+            if (r0 >= hi) break;  // block-uniform
+            const uint64_t i = r0 + t;
+            const bool valid = i < hi;
+            const uint32_t pos = wave_claim(cur, sort_key(lb[e]), valid, lane);
+            if (valid) {
+                ent[pos] = make_uint4(static_cast<uint32_t>(ob[e]), static_cast<uint32_t>(ob[e] >> 32), lb[e],
+                                      static_cast<uint32_t>(i));
+                if (seed) sseed[pos] = seed[i];
+            }
         }
-    }
-    __syncthreads();
-    const uint32_t cnt = h[t];
-    h[t] = cnt ? atomicAdd(&cursor[t], cnt) : 0u;
-    __syncthreads();
-    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads * kSortE) {
-      // this block's lengths and offsets, all loads issued before any use
-      uint32_t lb[kSortE];
-      uint64_t ob[kSortE];
-#pragma unroll
-      for (uint32_t e = 0; e < kSortE; ++e) {
-          const uint64_t i = b0 + e * kSortThreads + t;
-          lb[e] = i < hi ? len[i] : 0u;
-          ob[e] = i < hi ? off[i] : 0u;
-      }
-#pragma unroll
-      for (uint32_t e = 0; e < kSortE; ++e) {
-        const uint64_t r0 = b0 + e * kSortThreads;
-        if (r0 >= hi) break;  // block-uniform
-        const uint64_t i = r0 + t;
-        const bool valid = i < hi;
-        const uint32_t l = lb[e];
-        const uint32_t k = valid ? sort_key(l) : 0u;
-        uint64_t rem = __ballot(valid);
-        uint32_t rank = 0;
-        while (rem) {  // wave-uniform: one pass per distinct key in the wave
-            const int leader = __ffsll(static_cast<long long>(rem)) - 1;
-            const uint32_t kl = __shfl(k, leader);
-            const uint64_t m = __ballot(valid && k == kl);
-            if (valid && k == kl) rank = __popcll(m & ((1ull << lane) - 1ull));
-            if (static_cast<int>(lane) == leader) wc[w][kl] = __popcll(m);
-            rem &= ~m;
-        }
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = h[k] + rank;
-            for (uint32_t v = 0; v < w; ++v) pos += wc[v][k];
-            const uint64_t o = ob[e];
-            ent[pos] = make_uint4(static_cast<uint32_t>(o), static_cast<uint32_t>(o >> 32), l,
-                                  static_cast<uint32_t>(i));
-        }
-        __syncthreads();
-        uint32_t add = 0;
-        for (uint32_t v = 0; v < kW; ++v) {
-            add += wc[v][t];
-            wc[v][t] = 0;
-        }
-        h[t] += add;
-        __syncthreads();
-      }
     }
 }
 
-// Length classes of the offsets API in ONE persistent launch.  The sorted
-// entries hold class 0..3 runs (G = 1, 4, 16, 16).  Each workgroup takes the
-// class given by a static split of the grid proportional to each class's
-// estimated work (payload bytes + buf_cost per buffer; every nonempty class
-// gets at least one workgroup), stages that class's LDS image and walks the
-// class exactly as a standalone launch of its share would (the entries are
-// sorted by batch count within a class, so the round-robin is balanced).
-// Small, latency-bound classes thus run beside the bandwidth-bound ones
-// instead of in launches of their own.  (Letting a workgroup move on to
-// another class once its own runs dry needs the class bodies inside a loop,
-// which costs ~30 spilled VGPRs; per-slice atomic work grabbing measured
-// slower: 4096 waves contending on one counter.)
-constexpr uint32_t kBufCost = 2048;  // default bytes-equivalent cost of one buffer
-
+// Length classes of the offsets API in ONE persistent launch: every
+// workgroup walks every class (sorted runs of G = 1, 4, 16, 16), smallest
+// buffers first, each class spread over all waves of the grid, so no class
+// leaves CUs idle while another still has work.  (A static split of the grid
+// by estimated class work measured 3-8 % slower: the estimate is never
+// exact, and a class that finishes early idles its CUs.)
 struct Images {
-    const uint4 *img[4];
-    uint32_t buf_cost;
+    const uint4 *img[3];  // G = 1, 4, 16
 };
 
-template <int G>
-__device__ __forceinline__ void run_class(const Params &P0, uint32_t start, uint32_t count, uint32_t r,
-                                          uint32_t nwg, uint32_t lane, const Lut &L) {
-    constexpr uint32_t kGroups = 64 / G;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    Params P = P0;
-    P.ent = P0.ent + start;
-    P.n = count;
-    const uint64_t gid = (static_cast<uint64_t>(r) * kWaves + wave) * kGroups + lane / G;
-    const uint64_t gstride = static_cast<uint64_t>(nwg) * kWaves * kGroups;
-    group_stream<G, false>(P, gid, gstride, lane % G, L);
+// ---------------------------------------------------------------------------
+// Wave-uniform walk of length-sorted entries (offsets API).  The K = 64/G
+// groups of a wave take K consecutive sorted entries per round; sorting by
+// (class, batch count) makes their batch counts (nearly) equal, so the wave
+// runs max_i(nb_i) batches for all of them under SCALAR control -- the
+// uniform-block kernel's loop shape, ping-pong register slots and all.  A
+// group with fewer batches starts early: its granules before the buffer start
+// load from a clamped address and are zeroed in registers (leading zeros
+// leave a zero CRC register unchanged).  The bytes after the last whole
+// granule fold in as ONE granule (seed trick, below) instead of bytewise.
+struct RGeo {
+    uint64_t a;     // buffer start address (an empty buffer: the arena start)
+    uint32_t len;
+    uint32_t seed;
+    uint32_t bid;   // output slot, or ~0u for a lane past the end of the list
+    __device__ __forceinline__ uint64_t abase() const { return a & ~static_cast<uint64_t>(15); }
+    __device__ __forceinline__ uint32_t alow() const { return static_cast<uint32_t>(a) & 15u; }
+    __device__ __forceinline__ uint32_t ng() const { return (alow() + len) >> 4; }  // whole granules from g0
+};
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int from) {
+    for (int m = from; m < 64; m <<= 1) {
+        const uint32_t o = __shfl_xor(v, m);
+        v = o > v ? o : v;
+    }
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
-__global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, Images im, uint32_t *ws) {
-    const uint32_t *cls = ws + kWsCls;
-    const unsigned long long *cbytes = reinterpret_cast<const unsigned long long *>(ws + kWsBytes);
-    if (blockIdx.x == 0 && threadIdx.x < kKeys) ws[threadIdx.x] = 0;  // histogram, for the next call
-    uint64_t w[4], W = 0;
-    int nz = 0;
-    for (int k = 0; k < 4; ++k) {
-        w[k] = cls[4 + k] ? cbytes[k] + static_cast<uint64_t>(cls[4 + k]) * im.buf_cost : 0;
-        W += w[k];
-        nz += cls[4 + k] ? 1 : 0;
+// Geometry of sorted entry e (clamped to the last entry for lanes past the
+// end, so every address stays valid).  Seeds come pre-sorted (sort_scatter),
+// so no load depends on another.
+__device__ __forceinline__ RGeo load_rgeo(const Params &P, uint64_t e) {
+    const bool valid = e < P.n;
+    const uint64_t ec = valid ? e : P.n - 1;
+    const uint4 v = P.ent[ec];
+    RGeo q;
+    // an empty buffer reads nothing of its own: point it at the arena start
+    // so its (masked) loads stay inside the caller's allocation
+    q.a = v.z ? P.base + ((static_cast<uint64_t>(v.y) << 32) | v.x) : P.base;
+    q.len = v.z;
+    q.seed = P.sseed ? P.sseed[ec] : 0u;
+    q.bid = valid ? v.w : 0xffffffffu;
+    return q;
+}
+
+// Wave max of the groups' batch counts (>= 1).
+template <int G>
+__device__ __forceinline__ uint32_t round_nbw(const RGeo &q) {
+    constexpr uint32_t GU = G * U;
+    const uint32_t nb = (q.ng() + GU - 1) / GU;
+    return wave_max_u32(nb < 1u ? 1u : nb, G);
+}
+
+// Last batch index that holds head granules (d <= 1) for any group.
+template <int G>
+__device__ __forceinline__ uint32_t round_jfix(const RGeo &q, uint32_t nbw) {
+    constexpr uint32_t GU = G * U;
+    const uint32_t ng = q.ng();
+    const uint32_t jh = (GU * nbw - ng) / GU + ((q.alow() > 12u && ng >= 2u) ? 1u : 0u);
+    return wave_max_u32(jh, G);
+}
+
+// d (granule index relative to g0) of batch j, row 0, this lane.
+template <int G>
+__device__ __forceinline__ int32_t row_d(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl) {
+    return static_cast<int32_t>(q.ng()) - static_cast<int32_t>(G * U * (nbw - j)) + static_cast<int32_t>(gl);
+}
+
+// Batch j of a round: rows before the buffer clamp to granule g0.
+template <int G>
+__device__ __forceinline__ void load_rbatch(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl, uint4 (&v)[U]) {
+    const int32_t d0 = row_d<G>(q, nbw, j, gl);
+    const uint64_t ab = q.abase();
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+        int32_t d = d0 + static_cast<int32_t>(G * i);
+        d = d < 0 ? 0 : d;
+        const uint64_t ad = ab + (static_cast<uint32_t>(d) << 4);
+        // the last row's 128-B line is shared with the next batch's first
+        // row when the buffer end is not line aligned: keep it in L2
+        v[i] = i == U - 1 ? load16_rt(ad) : load16(ad);
     }
-    const uint32_t grid = gridDim.x;
-    const uint32_t spare = grid > static_cast<uint32_t>(nz) ? grid - nz : 0;
-    uint32_t nwg[4], assigned = 0;
-    int big = -1;
-    for (int k = 0; k < 4; ++k) {
-        nwg[k] = cls[4 + k] ? 1 + static_cast<uint32_t>(static_cast<double>(spare) * static_cast<double>(w[k]) / W)
-                            : 0;
-        assigned += nwg[k];
-        if (cls[4 + k] && (big < 0 || w[k] > w[big])) big = k;
-    }
-    if (big >= 0) nwg[big] += grid - assigned;  // rounding leftovers: the class with the most work
-    int c = -1;
-    uint32_t first = 0, r = 0;
-    for (int k = 0; k < 4 && c < 0; ++k) {
-        if (blockIdx.x < first + nwg[k]) {
-            c = k;
-            r = blockIdx.x - first;
+}
+
+// Head fix-up of batch j: zero granules before the buffer (d < 0), clear the
+// pre-buffer bytes of g0 and xor the seed into buffer bytes 0..3.
+template <int G>
+__device__ __forceinline__ void fix_rbatch(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl, uint4 (&v)[U]) {
+    const uint32_t s0 = q.len >= 4 ? ~q.seed : 0u;
+    const int32_t alow = static_cast<int32_t>(q.alow());
+    const int32_t d0 = row_d<G>(q, nbw, j, gl);
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+        const int32_t d = d0 + static_cast<int32_t>(G * i);
+        if (d < 0) {
+            v[i] = make_uint4(0, 0, 0, 0);
+        } else if (d == 0 || (d == 1 && alow > 12)) {
+            const int32_t rel = d * 16 - alow;
+            v[i].x = fix_word(v[i].x, rel, s0);
+            v[i].y = fix_word(v[i].y, rel + 4, s0);
+            v[i].z = fix_word(v[i].z, rel + 8, s0);
+            v[i].w = fix_word(v[i].w, rel + 12, s0);
         }
-        first += nwg[k];
     }
+}
+
+// The granule after the last whole granule (k = (alow+len) & 15 bytes of it
+// belong to the buffer).
+__device__ __forceinline__ uint4 load_rtail(const RGeo &q, uint32_t gl) {
+    if (gl == 0 && ((q.alow() + q.len) & 15u)) return load16_rt(q.abase() + (static_cast<uint64_t>(q.ng()) << 4));
+    return make_uint4(0, 0, 0, 0);
+}
+
+// X = R(X, tail bytes).  With V the tail granule (pre-buffer bytes zeroed,
+// seed applied, bytes >= k zeroed) and k >= 4:
+//   R(X, V[0..k)) = R(0, V'[0..k)) with V'.x = V.x ^ X      (seed trick)
+//                 = R(0, 0^(16-k) || V'[0..k))              (leading zeros)
+// i.e. one granule fold of V' shifted up by 16-k bytes.  k < 4 goes bytewise.
+__device__ __forceinline__ uint32_t fold_tail(uint32_t X, uint4 V, const RGeo &q, const Lut &L) {
+    const uint32_t alow = q.alow();
+    const uint32_t end = alow + q.len;
+    const uint32_t k = end & 15u;
+    if (k == 0) return X;
+    const uint32_t s0 = q.len >= 4 ? ~q.seed : 0u;
+    const int32_t rel = static_cast<int32_t>(end & ~15u) - static_cast<int32_t>(alow);
+    uint32_t w[4] = {fix_word(V.x, rel, s0), fix_word(V.y, rel + 4, s0), fix_word(V.z, rel + 8, s0),
+                     fix_word(V.w, rel + 12, s0)};
+#pragma unroll
+    for (uint32_t m = 0; m < 4; ++m) {  // zero bytes >= k
+        const int32_t nb = static_cast<int32_t>(k) - static_cast<int32_t>(4 * m);
+        w[m] &= nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : (0xffffffffu >> (32 - 8 * nb)));
+    }
+    if (k >= 4) {
+        w[0] ^= X;
+        const uint64_t lo = (static_cast<uint64_t>(w[1]) << 32) | w[0];
+        const uint64_t hi = (static_cast<uint64_t>(w[3]) << 32) | w[2];
+        const uint32_t b = 8u * (16u - k);  // 8 .. 96
+        uint64_t h2, l2;
+        if (b >= 64) {
+            h2 = lo << (b - 64);
+            l2 = 0;
+        } else {
+            h2 = (hi << b) | (lo >> (64 - b));
+            l2 = lo << b;
+        }
+        return r0_granule(make_uint4(static_cast<uint32_t>(l2), static_cast<uint32_t>(l2 >> 32),
+                                     static_cast<uint32_t>(h2), static_cast<uint32_t>(h2 >> 32)),
+                          L);
+    }
+    for (uint32_t i = 0; i < k; ++i) X = byte_step(X, (w[0] >> (8u * i)) & 0xffu);
+    return X;
+}
+
+template <int G>
+__device__ __forceinline__ void finish_round(const Params &P, const RGeo &q, const uint32_t (&A)[U],
+                                             const uint4 &tail, uint32_t gl, const Lut &L) {
+    const uint32_t x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
+    const uint32_t x23 = lookup4<kRegionB>(A[2], L) ^ A[3];
+    uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+#pragma unroll
+    for (int k = 0; (1 << k) < G; ++k) {
+        const uint32_t other = __shfl_down(X, 1u << k, G);
+        X = comb_shift(X, k) ^ other;
+    }
+    X = fold_tail(X, tail, q, L);
+    if (gl == 0 && q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for short buffers
+        uint32_t s = ~q.seed;
+        for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u);
+        X ^= s;
+    }
+    if (gl == 0 && q.bid != 0xffffffffu) {
+        const uint32_t crc = ~X;
+        P.out[q.bid] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+    }
+}
+
+// One wave walks rounds r = 0, 1, ... of its entries: entries of round r are
+// (wave_id + r*nwaves)*K + group.  Batches are prefetched one ahead, across
+// rounds, in two ping-pong register slots; all control is wave-uniform.
+template <int G>
+__device__ __forceinline__ void sorted_stream(const Params &P, uint64_t wave_id, uint64_t nwaves, uint32_t lane,
+                                              const Lut &L) {
+    constexpr uint32_t K = 64 / G;
+    const uint32_t gl = lane % G;
+    const uint64_t w0 = wave_id * K;
+    if (w0 >= P.n) return;
+    const uint64_t rstride = nwaves * K;
+    const uint64_t R = (P.n - 1 - w0) / rstride + 1;  // rounds (wave-uniform)
+    const uint64_t e0 = w0 + lane / G;
+
+    RGeo q = load_rgeo(P, e0);
+    uint32_t nbw = round_nbw<G>(q);
+    uint32_t jfix = round_jfix<G>(q, nbw);
+    RGeo qn = q;
+    if (R > 1) qn = load_rgeo(P, e0 + rstride);
+    uint32_t nbwn = 0;
+    uint4 tail;
+    uint4 slot0[U], slot1[U];
+    load_rbatch<G>(q, nbw, 0, gl, slot0);
+    uint32_t A[U];
+    uint64_t r = 0;
+    uint32_t j = 0;
+
+    auto step = [&](uint4(&cur)[U], uint4(&nxt)[U]) -> bool {
+        const bool lastj = j + 1 == nbw;
+        if (!lastj) {
+            load_rbatch<G>(q, nbw, j + 1, gl, nxt);
+        } else {
+            tail = load_rtail(q, gl);  // consumed after this batch's fold
+            if (r + 1 < R) {
+                nbwn = round_nbw<G>(qn);
+                load_rbatch<G>(qn, nbwn, 0, gl, nxt);
+            }
+        }
+        if (j <= jfix) fix_rbatch<G>(q, nbw, j, gl, cur);
+        if (j == 0)
+            fold_batch<true>(cur, A, L);
+        else
+            fold_batch<false>(cur, A, L);
+        if (!lastj) {
+            ++j;
+            return false;
+        }
+        finish_round<G>(P, q, A, tail, gl, L);
+        if (++r == R) return true;
+        q = qn;
+        nbw = nbwn;
+        jfix = round_jfix<G>(q, nbw);
+        if (r + 1 < R) qn = load_rgeo(P, e0 + (r + 1) * rstride);
+        j = 0;
+        return false;
+    };
+    for (;;) {
+        if (step(slot0, slot1)) break;
+        if (step(slot1, slot0)) break;
+    }
+}
+
+#ifndef LVK_WALK
+#define LVK_WALK 1  // 0: per-group streams (group_stream), 1: wave-uniform rounds (sorted_stream)
+#endif
+// Walk entries [start, start+count) of the sorted list as wave wave_id of
+// nwaves.
+template <int G>
+__device__ __forceinline__ void run_class(const Params &P0, uint32_t start, uint32_t count, uint64_t wave_id,
+                                          uint64_t nwaves, uint32_t lane, const Lut &L) {
+    Params P = P0;
+    P.ent = P0.ent + start;
+    P.sseed = P0.sseed ? P0.sseed + start : nullptr;
+    P.n = count;
+#if LVK_WALK
+    sorted_stream<G>(P, wave_id, nwaves, lane, L);
+#else
+    constexpr uint32_t kGroups = 64 / G;
+    group_stream<G, false>(P, wave_id * kGroups + lane / G, nwaves * kGroups, lane % G, L);
+#endif
+}
+
+__global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, Images im, const uint32_t *ws) {
+    const uint32_t *cls = ws + kWsCls;
     const uint32_t lane = threadIdx.x & 63u;
     const Lut L = make_lut(lane);
-    if (c >= 0) {
-        stage_tables(im.img[c]);
-        const uint32_t start = cls[c], count = cls[4 + c];
-        switch (c) {
-            case 0: run_class<1>(P, start, count, r, nwg[0], lane, L); break;
-            case 1: run_class<4>(P, start, count, r, nwg[1], lane, L); break;
-            default: run_class<16>(P, start, count, r, nwg[c], lane, L); break;
-        }
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t wave_id = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWaves;
+    // Classes 2 and 3 share G = 16 and one image: one contiguous list.  The
+    // LDS image is restaged per G after a barrier (every wave of the
+    // workgroup is done with the previous one).
+    const uint32_t n0 = cls[4], n1 = cls[5], n23 = cls[6] + cls[7];
+    bool staged = false;
+    if (n0) {
+        stage_tables(im.img[0]);
+        staged = true;
+        run_class<1>(P, cls[0], n0, wave_id, nwaves, lane, L);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&ws[kWsDone], 1u) == grid - 1) {  // last workgroup out
-            unsigned long long *cb = reinterpret_cast<unsigned long long *>(ws + kWsBytes);
-            for (int k = 0; k < 4; ++k) cb[k] = 0;
-            ws[kWsDone] = 0;
-        }
+    if (n1) {
+        if (staged) __syncthreads();
+        stage_tables(im.img[1]);
+        staged = true;
+        run_class<4>(P, cls[1], n1, wave_id, nwaves, lane, L);
+    }
+    if (n23) {
+        if (staged) __syncthreads();
+        stage_tables(im.img[2]);
+        run_class<16>(P, cls[6] ? cls[2] : cls[3], n23, wave_id, nwaves, lane, L);
     }
 }
 
@@ -958,7 +1223,6 @@ struct DevCtx {
     bool ready = false;
     int cus = 0;
     uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
-    uint32_t buf_cost = lvk::kBufCost;  // class-split cost per buffer (LVGPU_BUF_COST overrides, tuning)
     // offsets-API sort workspace, one per stream (calls on one stream are
     // stream-ordered, so reusing its buffer is safe; different streams never share)
     std::mutex ws_m;
@@ -1042,7 +1306,6 @@ int current_ctx(DevCtx **out) {
         hipDeviceProp_t prop;
         LV_HIP(hipGetDeviceProperties(&prop, dev));
         c.cus = prop.multiProcessorCount;
-        if (const char *e = std::getenv("LVGPU_BUF_COST")) c.buf_cost = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
         for (int i = 0; i < 4; ++i) {
             const auto &im = host_image(i);
             LV_HIP(hipMalloc(&c.image[i], im.size() * 4));
@@ -1087,6 +1350,7 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
     P.blen = blen;
     P.flags = flags;
     P.ent = nullptr;
+    P.sseed = nullptr;
     hipLaunchKernelGGL((lvk::crc32c_batch_kernel<G, STRIDED>), dim3(static_cast<uint32_t>(grid)),
                        dim3(lvk::kThreads), 0, s, P, c.image[gi]);
 }
@@ -1104,7 +1368,22 @@ void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off
 }
 
 // Bytes of sort workspace the offsets API needs for n buffers.
-size_t sort_ws_bytes(uint64_t n) { return lvk::kWsHeader * sizeof(uint32_t) + n * sizeof(uint4); }
+// Sorting workgroups and elements per workgroup for n buffers.
+uint64_t sort_wgs(uint64_t n, uint64_t *chunk) {
+    uint64_t wgs = (n + lvk::kSortChunk - 1) / lvk::kSortChunk;
+    if (wgs > lvk::kSortMaxWgs) wgs = lvk::kSortMaxWgs;
+    if (wgs == 0) wgs = 1;
+    *chunk = (n + wgs - 1) / wgs;
+    return wgs;
+}
+
+// Header, histogram matrix, n sorted 16-B entries, then n seeds in entry order.
+size_t sort_ws_bytes(uint64_t n) {
+    uint64_t chunk = 0;
+    const uint64_t wgs = sort_wgs(n, &chunk);
+    return lvk::kWsHeader * sizeof(uint32_t) + wgs * lvk::kKeys * sizeof(uint32_t) +
+           n * (sizeof(uint4) + sizeof(uint32_t));
+}
 
 // The library-owned workspace of (device, stream), grown on demand; its
 // header is zeroed when allocated and every call leaves it zero again.
@@ -1124,20 +1403,22 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out) {
     return 0;
 }
 
-// Length-sorted launch of the offsets API, three kernels and no host sync:
-// histogram + scan (last workgroup), stable scatter into sorted entries, then
-// the persistent class kernel over all four length classes.
+// Length-sorted launch of the offsets API, four kernels and no host sync:
+// per-workgroup histograms, their column scan (+ key starts), the scatter
+// into sorted entries, then the persistent class kernel.
 int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                   const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
     uint32_t *ws = reinterpret_cast<uint32_t *>(ws_bytes);
-    uint4 *ent = reinterpret_cast<uint4 *>(ws + lvk::kWsHeader);
-    uint64_t wgs = (n + 2047) / 2048;  // ~2048 buffers per sorting workgroup: 8 per thread
-    if (wgs > 4096) wgs = 4096;
-    const uint64_t chunk = (n + wgs - 1) / wgs;
-    hipLaunchKernelGGL(lvk::sort_hist_scan, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, len,
-                       n, chunk, ws);
-    hipLaunchKernelGGL(lvk::sort_scatter, dim3(static_cast<uint32_t>(wgs)), dim3(lvk::kSortThreads), 0, s, off, len,
-                       n, chunk, ws, ent);
+    uint64_t chunk = 0;
+    const uint64_t wgs = sort_wgs(n, &chunk);
+    uint32_t *M = ws + lvk::kWsHeader;
+    uint4 *ent = reinterpret_cast<uint4 *>(M + wgs * lvk::kKeys);
+    uint32_t *sseed = reinterpret_cast<uint32_t *>(ent + n);
+    const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
+    hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M);
+    hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
+                       static_cast<uint32_t>(wgs), ws);
+    hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed);
     lvk::Params P;
     P.base = reinterpret_cast<uint64_t>(arena);
     P.off = off;
@@ -1149,9 +1430,9 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     P.blen = 0;
     P.flags = flags;
     P.ent = ent;
+    P.sseed = seed ? sseed : nullptr;
     lvk::Images im;
-    for (int k = 0; k < 4; ++k) im.img[k] = c.image[k < 3 ? k : 2];  // class 3 runs with G = 16
-    im.buf_cost = c.buf_cost;
+    for (int k = 0; k < 3; ++k) im.img[k] = c.image[k];
     hipLaunchKernelGGL(lvk::crc32c_classes_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0, s, P,
                        im, ws);
     return 0;
@@ -1185,6 +1466,8 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
     P.stride = stride;
     P.blen = blen;
     P.flags = flags;
+    P.ent = nullptr;
+    P.sseed = nullptr;
     const uint32_t nb = static_cast<uint32_t>(blen / (16ull * G * lvk::U));
     hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G>), dim3(static_cast<uint32_t>(grid)),
                        dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);

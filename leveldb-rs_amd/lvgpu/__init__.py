@@ -18,7 +18,8 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "liblvgpu.so")
+# LVGPU_LIB selects another build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("LVGPU_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "liblvgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "lvgpu", "crc32c.h")
 
 MASK = 0x1  # LV_CRC_MASK

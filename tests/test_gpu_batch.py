@@ -303,3 +303,33 @@ def test_batch_multi_devices(gpu):
     assert np.array_equal(lvgpu.batch_multi(arena, offs, lens, seeds, masked=True, ngpu=1), want)
     with pytest.raises(lvgpu.LvError, match="device"):
         lvgpu.batch_multi(arena, offs, lens, seeds, ngpu=torch.cuda.device_count() + 1)
+
+
+def test_sorted_walk_edges(torch_dev, arena):
+    """Offsets API edge geometry for the wave-uniform walk: lengths at the
+    class edges (256/257, 2048/2049, 32768/32769) and at batch-count edges of
+    each class (k*64, k*256, k*1024 +-1), every start alignment mod 16, seeded;
+    empty buffers at the arena's first and last byte; one call holding them
+    all shuffled, so waves mix batch counts that differ by one."""
+    torch, dev = torch_dev
+    rng = random.Random(2024)
+    edges = {0, 1, 3, 4, 5, 15, 16, 17, 255, 256, 257, 2047, 2048, 2049, 32767, 32768, 32769, 65536}
+    for unit in (64, 256, 1024):
+        for k in range(1, 9):
+            edges |= {k * unit - 1, k * unit, k * unit + 1}
+    offs, lens = [], []
+    for ln in sorted(edges):
+        for mis in range(16):
+            offs.append(4096 * rng.randrange(1, 150) + mis)
+            lens.append(ln)
+    offs += [0, len(arena), len(arena) - 1]
+    lens += [0, 0, 1]
+    order = list(range(len(offs)))
+    rng.shuffle(order)
+    offs = [offs[i] for i in order]
+    lens = [lens[i] for i in order]
+    seeds = [rng.getrandbits(32) for _ in offs]
+    want = oracle_batch(arena, offs, lens, seeds, True)
+    got = gpu_batch(torch, dev, arena, offs, lens, seeds, True)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(offs[i], lens[i]) for i in bad[:10]]
