@@ -64,6 +64,16 @@ constexpr int kImageWords = (131072 + 6 * 4 * 1024) / 4;  // 38912 dwords = 152 
 
 __shared__ __attribute__((aligned(16))) uint32_t g_lds[kImageWords];
 
+// Per-wave output staging (8 KiB; with the image, exactly the 160 KiB of a
+// CU).  Results go to LDS and leave in one global store per wave every few
+// rounds.  A global store in the batch loop costs a pipeline drain: on gfx9
+// stores count in vmcnt, the register allocator soon reuses the store's
+// registers, and waiting for the store waits (in order) for every prefetch
+// load issued before it.
+__shared__ uint32_t g_oidx[kWaves][64];
+__shared__ uint32_t g_ocrc[kWaves][64];
+static_assert(sizeof(uint32_t) * (kImageWords + 2 * kWaves * 64) <= 163840, "LDS budget");
+
 // Per-lane lookup constants: lv byte i = 4*beta_i (dword of the lane's table
 // copy for lookup instruction i); sel_i moves that byte to bits 0..7 and the
 // state byte that indexes table k_i to bits 8..15 (v_perm selector: 0-3 = S1
@@ -543,9 +553,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(Params P, const 
 // of a wave walks the same (block round, batch) sequence: the batch control
 // is wave-uniform (scalar), there is no head/tail work, and the seed enters
 // as lane 0's first word.
+// Merge the U row accumulators and the G lanes of a group; lane 0 of the
+// group returns the (optionally masked) CRC.
 template <int G>
-__device__ __forceinline__ void finish_block(const Params &P, uint64_t blk, const uint32_t (&A)[U],
-                                             uint32_t gl, const Lut &L) {
+__device__ __forceinline__ uint32_t merge_group(const uint32_t (&A)[U], const Lut &L) {
     const uint32_t x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
     const uint32_t x23 = lookup4<kRegionB>(A[2], L) ^ A[3];
     uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
@@ -554,13 +565,22 @@ __device__ __forceinline__ void finish_block(const Params &P, uint64_t blk, cons
         const uint32_t other = __shfl_down(X, 1u << k, G);
         X = comb_shift(X, k) ^ other;
     }
-    if (gl == 0) {
-        const uint32_t crc = ~X;
-        P.out[blk] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
-    }
+    return X;
 }
 
-template <int G>
+__device__ __forceinline__ uint32_t final_crc(const Params &P, uint32_t X) {
+    const uint32_t crc = ~X;
+    return (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+}
+
+// Every step issues the SAME loads (next batch, and for seeded calls the
+// next block's seed) whether or not a next batch exists -- the last one
+// re-reads the current batch.  The compiler's s_waitcnt counts are static:
+// if one path through a step skips the prefetch, the fold of the current
+// batch waits with the count of that path (vmcnt(2)..(0) after a 4-load
+// prefetch) and so for the prefetch itself, serialising load and compute in
+// every step.
+template <int G, bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint32_t nb,
                                                                  const uint4 *__restrict__ image) {
     stage_tables(image);
@@ -579,24 +599,31 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     if (wblk0 >= P.n) return;
     const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
     auto block_ptr = [&](uint64_t k) { return P.base + (k < P.n ? k : 0) * P.stride + 16u * gl; };
-    auto block_s0 = [&](uint64_t k) { return P.seed && k < P.n ? ~P.seed[k] : 0xffffffffu; };
+    auto seed_ld = [&](uint64_t k) { return ~P.seed[k < P.n ? k : 0]; };
 
     uint64_t ptr = block_ptr(blk);
-    uint32_t s0 = block_s0(blk);
+    uint32_t s0 = SEEDED ? seed_ld(blk) : 0xffffffffu;
+    uint32_t s0n = s0;
     uint4 slot0[U], slot1[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) slot0[i] = load16(ptr + kRow * i);
     uint32_t A[U];
+    // The flush store's operands live in registers of their own for the whole
+    // loop (kept live past it below), so no loop temporary reuses them: a
+    // write to a pending store's source register waits for the store, i.e.
+    // (vmcnt is in order) for every prefetch load issued before it.
+    uint32_t st_val = 0;
+    uint64_t st_ptr = 0;
 
-    // one batch: fold `cur`, prefetch the next batch into `nxt`
+    // one batch: prefetch the next batch into `nxt`, fold `cur`
     auto step = [&](uint64_t r, uint32_t j, uint4(&cur)[U], uint4(&nxt)[U]) {
         const bool lastj = j + 1 == nb;
         const bool more = !lastj || r + 1 < rounds;
         const uint64_t nptr = lastj ? block_ptr(blk + gstride) : ptr + kBatch;
-        if (more) {
+        const uint64_t lptr = more ? nptr : ptr;  // no next batch: re-read this one
+        if constexpr (SEEDED) s0n = seed_ld(blk + gstride);
 #pragma unroll
-            for (uint32_t i = 0; i < U; ++i) nxt[i] = load16(nptr + kRow * i);
-        }
+        for (uint32_t i = 0; i < U; ++i) nxt[i] = load16(lptr + kRow * i);
         if (j == 0) {
             if (gl == 0) cur[0].x ^= s0;
             fold_batch<true>(cur, A, L);
@@ -604,9 +631,21 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
             fold_batch<false>(cur, A, L);
         }
         if (lastj) {
-            if (blk < P.n) finish_block<G>(P, blk, A, gl, L);
+            // round r's K results -> LDS slot (r % G)*K + group; one store of
+            // the wave's 64 slots every G rounds (and after the last round)
+            const uint32_t X = merge_group<G>(A, L);
+            if (gl == 0) g_ocrc[wave][(r % G) * kGroups + lane / G] = final_crc(P, X);
+            if ((r + 1) % G == 0 || r + 1 == rounds) {
+                __builtin_amdgcn_wave_barrier();
+                const uint64_t r0 = r - r % G;
+                const uint64_t k = wblk0 + (r0 + lane / kGroups) * gstride + lane % kGroups;
+                st_val = g_ocrc[wave][lane];
+                st_ptr = reinterpret_cast<uint64_t>(P.out + (k < P.n ? k : 0));
+                if (lane < (r - r0 + 1) * kGroups && k < P.n) *reinterpret_cast<uint32_t *>(st_ptr) = st_val;
+                __builtin_amdgcn_wave_barrier();
+            }
             blk += gstride;
-            s0 = block_s0(blk);
+            if constexpr (SEEDED) s0 = s0n;
         }
         ptr = nptr;
     };
@@ -623,6 +662,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         if (++t == total) break;
         if (++j == nb) { j = 0; ++r; }
     }
+    asm volatile("" ::"v"(st_val), "v"(st_ptr));
 }
 
 // Length classes of the offsets API.  Buffers are counting-sorted by key =
@@ -882,6 +922,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int from) {
 // Geometry of sorted entry e (clamped to the last entry for lanes past the
 // end, so every address stays valid).  Seeds come pre-sorted (sort_scatter),
 // so no load depends on another.
+template <bool SEEDED>
 __device__ __forceinline__ RGeo load_rgeo(const Params &P, uint64_t e) {
     const bool valid = e < P.n;
     const uint64_t ec = valid ? e : P.n - 1;
@@ -891,7 +932,7 @@ __device__ __forceinline__ RGeo load_rgeo(const Params &P, uint64_t e) {
     // so its (masked) loads stay inside the caller's allocation
     q.a = v.z ? P.base + ((static_cast<uint64_t>(v.y) << 32) | v.x) : P.base;
     q.len = v.z;
-    q.seed = P.sseed ? P.sseed[ec] : 0u;
+    q.seed = SEEDED ? P.sseed[ec] : 0u;
     q.bid = valid ? v.w : 0xffffffffu;
     return q;
 }
@@ -1005,47 +1046,42 @@ __device__ __forceinline__ uint32_t fold_tail(uint32_t X, uint4 V, const RGeo &q
 }
 
 template <int G>
-__device__ __forceinline__ void finish_round(const Params &P, const RGeo &q, const uint32_t (&A)[U],
-                                             const uint4 &tail, uint32_t gl, const Lut &L) {
-    const uint32_t x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
-    const uint32_t x23 = lookup4<kRegionB>(A[2], L) ^ A[3];
-    uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
-#pragma unroll
-    for (int k = 0; (1 << k) < G; ++k) {
-        const uint32_t other = __shfl_down(X, 1u << k, G);
-        X = comb_shift(X, k) ^ other;
-    }
+__device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q, const uint32_t (&A)[U],
+                                                 const uint4 &tail, uint32_t gl, const Lut &L) {
+    uint32_t X = merge_group<G>(A, L);
     X = fold_tail(X, tail, q, L);
     if (gl == 0 && q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for short buffers
         uint32_t s = ~q.seed;
         for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u);
         X ^= s;
     }
-    if (gl == 0 && q.bid != 0xffffffffu) {
-        const uint32_t crc = ~X;
-        P.out[q.bid] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
-    }
+    return final_crc(P, X);
 }
 
 // One wave walks rounds r = 0, 1, ... of its entries: entries of round r are
 // (wave_id + r*nwaves)*K + group.  Batches are prefetched one ahead, across
 // rounds, in two ping-pong register slots; all control is wave-uniform.
-template <int G>
+// Results are staged in LDS (g_oidx/g_ocrc) and stored every G rounds.
+// (Issuing the same loads in every step -- entries and tail re-read each
+// batch -- measured 4-5 % slower here: the extra loads and spills cost more
+// than the conservative wait counts they remove.)
+template <int G, bool SEEDED>
 __device__ __forceinline__ void sorted_stream(const Params &P, uint64_t wave_id, uint64_t nwaves, uint32_t lane,
                                               const Lut &L) {
     constexpr uint32_t K = 64 / G;
     const uint32_t gl = lane % G;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t w0 = wave_id * K;
     if (w0 >= P.n) return;
     const uint64_t rstride = nwaves * K;
     const uint64_t R = (P.n - 1 - w0) / rstride + 1;  // rounds (wave-uniform)
     const uint64_t e0 = w0 + lane / G;
 
-    RGeo q = load_rgeo(P, e0);
+    RGeo q = load_rgeo<SEEDED>(P, e0);
     uint32_t nbw = round_nbw<G>(q);
     uint32_t jfix = round_jfix<G>(q, nbw);
     RGeo qn = q;
-    if (R > 1) qn = load_rgeo(P, e0 + rstride);
+    if (R > 1) qn = load_rgeo<SEEDED>(P, e0 + rstride);
     uint32_t nbwn = 0;
     uint4 tail;
     uint4 slot0[U], slot1[U];
@@ -1074,12 +1110,23 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint64_t wave_id,
             ++j;
             return false;
         }
-        finish_round<G>(P, q, A, tail, gl, L);
+        const uint32_t crc = finish_round<G>(P, q, A, tail, gl, L);
+        const uint32_t slot = static_cast<uint32_t>(r % G) * K + lane / G;
+        if (gl == 0) {
+            g_oidx[wave][slot] = q.bid;
+            g_ocrc[wave][slot] = crc;
+        }
+        if ((r + 1) % G == 0 || r + 1 == R) {
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t bi = g_oidx[wave][lane], c = g_ocrc[wave][lane];
+            if (lane < (r % G + 1) * K && bi != 0xffffffffu) P.out[bi] = c;
+            __builtin_amdgcn_wave_barrier();
+        }
         if (++r == R) return true;
         q = qn;
         nbw = nbwn;
         jfix = round_jfix<G>(q, nbw);
-        if (r + 1 < R) qn = load_rgeo(P, e0 + (r + 1) * rstride);
+        if (r + 1 < R) qn = load_rgeo<SEEDED>(P, e0 + (r + 1) * rstride);
         j = 0;
         return false;
     };
@@ -1094,7 +1141,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint64_t wave_id,
 #endif
 // Walk entries [start, start+count) of the sorted list as wave wave_id of
 // nwaves.
-template <int G>
+template <int G, bool SEEDED>
 __device__ __forceinline__ void run_class(const Params &P0, uint32_t start, uint32_t count, uint64_t wave_id,
                                           uint64_t nwaves, uint32_t lane, const Lut &L) {
     Params P = P0;
@@ -1102,13 +1149,14 @@ __device__ __forceinline__ void run_class(const Params &P0, uint32_t start, uint
     P.sseed = P0.sseed ? P0.sseed + start : nullptr;
     P.n = count;
 #if LVK_WALK
-    sorted_stream<G>(P, wave_id, nwaves, lane, L);
+    sorted_stream<G, SEEDED>(P, wave_id, nwaves, lane, L);
 #else
     constexpr uint32_t kGroups = 64 / G;
     group_stream<G, false>(P, wave_id * kGroups + lane / G, nwaves * kGroups, lane % G, L);
 #endif
 }
 
+template <bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, Images im, const uint32_t *ws) {
     const uint32_t *cls = ws + kWsCls;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1119,23 +1167,29 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, Imag
     // Classes 2 and 3 share G = 16 and one image: one contiguous list.  The
     // LDS image is restaged per G after a barrier (every wave of the
     // workgroup is done with the previous one).
-    const uint32_t n0 = cls[4], n1 = cls[5], n23 = cls[6] + cls[7];
+#ifndef LVK_CLASSMASK
+#define LVK_CLASSMASK 7  // experiment knob: bit c runs class c (bit 2: classes 2+3)
+#endif
+    const uint32_t n0 = (LVK_CLASSMASK & 1) ? cls[4] : 0u, n1 = (LVK_CLASSMASK & 2) ? cls[5] : 0u,
+                   n23 = (LVK_CLASSMASK & 4) ? cls[6] + cls[7] : 0u;
     bool staged = false;
     if (n0) {
         stage_tables(im.img[0]);
         staged = true;
-        run_class<1>(P, cls[0], n0, wave_id, nwaves, lane, L);
+#ifndef LVK_EXP_STAGEONLY
+        run_class<1, SEEDED>(P, cls[0], n0, wave_id, nwaves, lane, L);
+#endif
     }
     if (n1) {
         if (staged) __syncthreads();
         stage_tables(im.img[1]);
         staged = true;
-        run_class<4>(P, cls[1], n1, wave_id, nwaves, lane, L);
+        run_class<4, SEEDED>(P, cls[1], n1, wave_id, nwaves, lane, L);
     }
     if (n23) {
         if (staged) __syncthreads();
         stage_tables(im.img[2]);
-        run_class<16>(P, cls[6] ? cls[2] : cls[3], n23, wave_id, nwaves, lane, L);
+        run_class<16, SEEDED>(P, cls[6] ? cls[2] : cls[3], n23, wave_id, nwaves, lane, L);
     }
 }
 
@@ -1433,8 +1487,12 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     P.sseed = seed ? sseed : nullptr;
     lvk::Images im;
     for (int k = 0; k < 3; ++k) im.img[k] = c.image[k];
-    hipLaunchKernelGGL(lvk::crc32c_classes_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0, s, P,
-                       im, ws);
+    if (seed)
+        hipLaunchKernelGGL(lvk::crc32c_classes_kernel<true>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0,
+                           s, P, im, ws);
+    else
+        hipLaunchKernelGGL(lvk::crc32c_classes_kernel<false>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads),
+                           0, s, P, im, ws);
     return 0;
 }
 
@@ -1469,8 +1527,12 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
     P.ent = nullptr;
     P.sseed = nullptr;
     const uint32_t nb = static_cast<uint32_t>(blen / (16ull * G * lvk::U));
-    hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G>), dim3(static_cast<uint32_t>(grid)),
-                       dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
+    if (seed)
+        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G, true>), dim3(static_cast<uint32_t>(grid)),
+                           dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
+    else
+        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G, false>), dim3(static_cast<uint32_t>(grid)),
+                           dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
 }
 
 void launch_blocks(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, uint32_t blen,
