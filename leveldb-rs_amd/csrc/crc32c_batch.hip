@@ -155,17 +155,33 @@ __device__ __forceinline__ uint32_t lut_addr(uint32_t s, const Lut &L) {
     return __builtin_amdgcn_perm(s, L.lv, sel);
 }
 
+// Shift_{16*2^k}(a) from the plain combine tables.
+__device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
+    const uint32_t *t = g_lds + (kComb / 4) + k * 1024;
+    return t[a & 0xffu] ^ t[256 + ((a >> 8) & 0xffu)] ^ t[512 + ((a >> 16) & 0xffu)] ^
+           t[768 + (a >> 24)];
+}
+
 // The U granules of a batch folded step-major: every slice-by-4 step issues
 // the 4U lookups of all U chains (plus, in step 0, the U row-shift lookups of
 // the accumulators) before consuming any, so 4U+ LDS reads are in flight per
 // wave instead of one chain's 4.  p[i] = R(0, v[i]); A[i] = W4(A[i]) ^ p[i]
 // (or A[i] = p[i] when FIRST).
-template <bool FIRST>
+// W4K < 0: W4 = the Latin half of region A (Shift_{64G} for the image's G);
+// W4K = k >= 0: W4 = plain combine table k (Shift_{16*2^k}) -- how groups of
+// G = 1 and 4 run on a G = 16 image (Shift_64 = k 2, Shift_256 = k 4).
+template <bool FIRST, int W4K = -1>
 __device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U], const Lut &L) {
     uint32_t s[U], w[U], w3[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) s[i] = v[i].x;
-    if constexpr (!FIRST) {
+    if constexpr (!FIRST && W4K >= 0) {
+#pragma unroll
+        for (uint32_t i = 0; i < U; ++i) {
+            w[i] = comb_shift(A[i], W4K);
+            w3[i] = 0u;
+        }
+    } else if constexpr (!FIRST) {
         uint32_t aa[U][4];
 #pragma unroll
         for (uint32_t i = 0; i < U; ++i) {
@@ -211,12 +227,6 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U]
     }
 }
 
-// Shift_{16*2^k}(a) from the plain combine tables.
-__device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
-    const uint32_t *t = g_lds + (kComb / 4) + k * 1024;
-    return t[a & 0xffu] ^ t[256 + ((a >> 8) & 0xffu)] ^ t[512 + ((a >> 16) & 0xffu)] ^
-           t[768 + (a >> 24)];
-}
 
 // One byte through T0 (this lane's copy): crc32c.rs:81.
 __device__ __forceinline__ uint32_t byte_step(uint32_t s, uint32_t b) {
@@ -555,11 +565,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(Params P, const 
 // as lane 0's first word.
 // Merge the U row accumulators and the G lanes of a group; lane 0 of the
 // group returns the (optionally masked) CRC.
-template <int G>
+// W1K/W2K < 0: the image's Latin W1/W2 (region B); k >= 0: plain combine
+// table k (for G = 1, 4 on a G = 16 image: Shift_16G, Shift_32G).
+template <int G, int W1K = -1, int W2K = -1>
 __device__ __forceinline__ uint32_t merge_group(const uint32_t (&A)[U], const Lut &L) {
-    const uint32_t x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
-    const uint32_t x23 = lookup4<kRegionB>(A[2], L) ^ A[3];
-    uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+    uint32_t x01, x23, X;
+    if constexpr (W1K >= 0) {
+        x01 = comb_shift(A[0], W1K) ^ A[1];
+        x23 = comb_shift(A[2], W1K) ^ A[3];
+    } else {
+        x01 = lookup4<kRegionB>(A[0], L) ^ A[1];
+        x23 = lookup4<kRegionB>(A[2], L) ^ A[3];
+    }
+    if constexpr (W2K >= 0)
+        X = comb_shift(x01, W2K) ^ x23;
+    else
+        X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
 #pragma unroll
     for (int k = 0; (1 << k) < G; ++k) {
         const uint32_t other = __shfl_down(X, 1u << k, G);
@@ -887,9 +908,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
 // leaves CUs idle while another still has work.  (A static split of the grid
 // by estimated class work measured 3-8 % slower: the estimate is never
 // exact, and a class that finishes early idles its CUs.)
-struct Images {
-    const uint4 *img[3];  // G = 1, 4, 16
-};
+
 
 // ---------------------------------------------------------------------------
 // Wave-uniform walk of length-sorted entries (offsets API).  The K = 64/G
@@ -1045,10 +1064,8 @@ __device__ __forceinline__ uint32_t fold_tail(uint32_t X, uint4 V, const RGeo &q
     return X;
 }
 
-template <int G>
-__device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q, const uint32_t (&A)[U],
-                                                 const uint4 &tail, uint32_t gl, const Lut &L) {
-    uint32_t X = merge_group<G>(A, L);
+__device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q, uint32_t X, const uint4 &tail,
+                                                 uint32_t gl, const Lut &L) {
     X = fold_tail(X, tail, q, L);
     if (gl == 0 && q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for short buffers
         uint32_t s = ~q.seed;
@@ -1058,75 +1075,83 @@ __device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q,
     return final_crc(P, X);
 }
 
-// One wave walks rounds r = 0, 1, ... of its entries: entries of round r are
-// (wave_id + r*nwaves)*K + group.  Batches are prefetched one ahead, across
-// rounds, in two ping-pong register slots; all control is wave-uniform.
-// Results are staged in LDS (g_oidx/g_ocrc) and stored every G rounds.
-// (Issuing the same loads in every step -- entries and tail re-read each
-// batch -- measured 4-5 % slower here: the extra loads and spills cost more
-// than the conservative wait counts they remove.)
-template <int G, bool SEEDED>
-__device__ __forceinline__ void sorted_stream(const Params &P, uint64_t wave_id, uint64_t nwaves, uint32_t lane,
-                                              const Lut &L) {
+// One wave walks rounds of the sorted list: round rho holds entries
+// rho*K + group (K = 64/G groups).  The rounds come from `next()` (a static
+// stride, or a workgroup's shared pool) until it returns rho >= nr.  Batches
+// are prefetched one ahead, across rounds, in two ping-pong register slots;
+// all control is wave-uniform.  Results are staged in LDS (g_oidx/g_ocrc)
+// and stored every G rounds.  (Issuing the same loads in every step --
+// entries and tail re-read each batch -- measured 4-5 % slower: the extra
+// loads and spills cost more than the conservative wait counts they remove.)
+// The image is always the G = 16 one: groups of G = 1 and 4 take their
+// row-shift and merge tables from the plain combine tables.
+template <int G, bool SEEDED, class Next>
+__device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, const Lut &L, uint64_t rho,
+                                              Next next) {
     constexpr uint32_t K = 64 / G;
-    const uint32_t gl = lane % G;
+    constexpr int W4K = G == 16 ? -1 : (G == 4 ? 4 : 2);  // Shift_{64G}
+    constexpr int W1K = G == 16 ? -1 : (G == 4 ? 2 : 0);  // Shift_{16G}
+    constexpr int W2K = G == 16 ? -1 : (G == 4 ? 3 : 1);  // Shift_{32G}
+    const uint32_t gl = lane % G, grp = lane / G;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t w0 = wave_id * K;
-    if (w0 >= P.n) return;
-    const uint64_t rstride = nwaves * K;
-    const uint64_t R = (P.n - 1 - w0) / rstride + 1;  // rounds (wave-uniform)
-    const uint64_t e0 = w0 + lane / G;
+    const uint64_t nr = (P.n + K - 1) / K;  // rounds in the list
+    if (rho >= nr) return;
+    uint64_t rhon = next();
 
-    RGeo q = load_rgeo<SEEDED>(P, e0);
+    RGeo q = load_rgeo<SEEDED>(P, rho * K + grp);
     uint32_t nbw = round_nbw<G>(q);
     uint32_t jfix = round_jfix<G>(q, nbw);
     RGeo qn = q;
-    if (R > 1) qn = load_rgeo<SEEDED>(P, e0 + rstride);
+    if (rhon < nr) qn = load_rgeo<SEEDED>(P, rhon * K + grp);
     uint32_t nbwn = 0;
     uint4 tail;
     uint4 slot0[U], slot1[U];
     load_rbatch<G>(q, nbw, 0, gl, slot0);
     uint32_t A[U];
-    uint64_t r = 0;
+    uint32_t c = 0;  // rounds finished (output staging slot)
     uint32_t j = 0;
 
     auto step = [&](uint4(&cur)[U], uint4(&nxt)[U]) -> bool {
         const bool lastj = j + 1 == nbw;
+        const bool more = rhon < nr;
         if (!lastj) {
             load_rbatch<G>(q, nbw, j + 1, gl, nxt);
         } else {
             tail = load_rtail(q, gl);  // consumed after this batch's fold
-            if (r + 1 < R) {
+            if (more) {
                 nbwn = round_nbw<G>(qn);
                 load_rbatch<G>(qn, nbwn, 0, gl, nxt);
             }
         }
         if (j <= jfix) fix_rbatch<G>(q, nbw, j, gl, cur);
         if (j == 0)
-            fold_batch<true>(cur, A, L);
+            fold_batch<true, W4K>(cur, A, L);
         else
-            fold_batch<false>(cur, A, L);
+            fold_batch<false, W4K>(cur, A, L);
         if (!lastj) {
             ++j;
             return false;
         }
-        const uint32_t crc = finish_round<G>(P, q, A, tail, gl, L);
-        const uint32_t slot = static_cast<uint32_t>(r % G) * K + lane / G;
+        uint32_t X = merge_group<G, W1K, W2K>(A, L);
+        const uint32_t crc = finish_round(P, q, X, tail, gl, L);
+        const uint32_t slot = (c % G) * K + grp;
         if (gl == 0) {
             g_oidx[wave][slot] = q.bid;
             g_ocrc[wave][slot] = crc;
         }
-        if ((r + 1) % G == 0 || r + 1 == R) {
+        if ((c + 1) % G == 0 || !more) {
             __builtin_amdgcn_wave_barrier();
-            const uint32_t bi = g_oidx[wave][lane], c = g_ocrc[wave][lane];
-            if (lane < (r % G + 1) * K && bi != 0xffffffffu) P.out[bi] = c;
+            const uint32_t bi = g_oidx[wave][lane], cv = g_ocrc[wave][lane];
+            if (lane < (c % G + 1) * K && bi != 0xffffffffu) P.out[bi] = cv;
             __builtin_amdgcn_wave_barrier();
         }
-        if (++r == R) return true;
+        if (!more) return true;
+        ++c;
         q = qn;
         nbw = nbwn;
         jfix = round_jfix<G>(q, nbw);
-        if (r + 1 < R) qn = load_rgeo<SEEDED>(P, e0 + (r + 1) * rstride);
+        rhon = next();
+        if (rhon < nr) qn = load_rgeo<SEEDED>(P, rhon * K + grp);
         j = 0;
         return false;
     };
@@ -1136,60 +1161,70 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint64_t wave_id,
     }
 }
 
-#ifndef LVK_WALK
-#define LVK_WALK 1  // 0: per-group streams (group_stream), 1: wave-uniform rounds (sorted_stream)
-#endif
-// Walk entries [start, start+count) of the sorted list as wave wave_id of
-// nwaves.
-template <int G, bool SEEDED>
-__device__ __forceinline__ void run_class(const Params &P0, uint32_t start, uint32_t count, uint64_t wave_id,
-                                          uint64_t nwaves, uint32_t lane, const Lut &L) {
+// The sorted sub-list [start, start+count).
+__device__ __forceinline__ Params sub_list(const Params &P0, uint32_t start, uint32_t count) {
     Params P = P0;
     P.ent = P0.ent + start;
     P.sseed = P0.sseed ? P0.sseed + start : nullptr;
     P.n = count;
-#if LVK_WALK
-    sorted_stream<G, SEEDED>(P, wave_id, nwaves, lane, L);
-#else
-    constexpr uint32_t kGroups = 64 / G;
-    group_stream<G, false>(P, wave_id * kGroups + lane / G, nwaves * kGroups, lane % G, L);
-#endif
+    return P;
 }
 
+// Waves per workgroup that walk the small classes (<= 2 KiB) before joining
+// the large-buffer pool.  Measured on C2/C4: class 0 runs as fast on 4 waves
+// per CU as on 16 (it is bound by per-buffer VALU work and random line
+// reads, not latency), and classes 2+3 run FASTER on 12 waves than on 16.
+#ifndef LVK_SMALL_WAVES
+#define LVK_SMALL_WAVES 4
+#endif
+constexpr uint32_t kSmallWaves = LVK_SMALL_WAVES;
+
+// Next round of the workgroup's large-buffer share: a word of combine table
+// k = 5 (Shift_512), which no group of the class kernel uses, since the LDS
+// is full (image + output staging = 160 KiB).
+constexpr uint32_t kPoolWord = (kComb + 5 * 4096) / 4;
+
+// The offsets API in ONE persistent launch over the length-sorted list, on
+// the G = 16 table image (staged once).  Waves [0, kSmallWaves) of every
+// workgroup walk class 0 (G = 1) and then class 1 (G = 4), each class spread
+// over those waves of the whole grid; meanwhile the other waves stream
+// classes 2+3 (G = 16; one contiguous list).  Workgroup b owns the large
+// rounds rho = b + k*grid, which its waves take from an LDS counter, so the
+// small-class waves join the large work when they are done and no wave idles
+// while its workgroup has rounds left.  (Earlier: a static split of the grid
+// by class, 3-8 % slower -- a class that finishes early idles its CUs; then
+// every workgroup walking every class in turn, with the image restaged per
+// G -- the small classes ran alone, latency- and VALU-bound, for ~100 us of
+// C2's 1.2 ms.)
 template <bool SEEDED>
-__global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, Images im, const uint32_t *ws) {
+__global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, const uint4 *__restrict__ image,
+                                                                  const uint32_t *ws) {
     const uint32_t *cls = ws + kWsCls;
+    stage_tables(image);
+    if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const Lut L = make_lut(lane);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t wave_id = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-    const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWaves;
-    // Classes 2 and 3 share G = 16 and one image: one contiguous list.  The
-    // LDS image is restaged per G after a barrier (every wave of the
-    // workgroup is done with the previous one).
-#ifndef LVK_CLASSMASK
-#define LVK_CLASSMASK 7  // experiment knob: bit c runs class c (bit 2: classes 2+3)
-#endif
-    const uint32_t n0 = (LVK_CLASSMASK & 1) ? cls[4] : 0u, n1 = (LVK_CLASSMASK & 2) ? cls[5] : 0u,
-                   n23 = (LVK_CLASSMASK & 4) ? cls[6] + cls[7] : 0u;
-    bool staged = false;
-    if (n0) {
-        stage_tables(im.img[0]);
-        staged = true;
-#ifndef LVK_EXP_STAGEONLY
-        run_class<1, SEEDED>(P, cls[0], n0, wave_id, nwaves, lane, L);
-#endif
+    const uint64_t grid = gridDim.x;
+    if (wave < kSmallWaves) {
+        const uint64_t sw = blockIdx.x * kSmallWaves + wave, nsw = grid * kSmallWaves;
+        uint64_t k = 0;
+        auto stride = [&]() { return sw + (++k) * nsw; };
+        if (cls[4]) {
+            sorted_stream<1, SEEDED>(sub_list(P, cls[0], cls[4]), lane, L, sw, stride);
+            k = 0;
+        }
+        if (cls[5]) sorted_stream<4, SEEDED>(sub_list(P, cls[1], cls[5]), lane, L, sw, stride);
     }
-    if (n1) {
-        if (staged) __syncthreads();
-        stage_tables(im.img[1]);
-        staged = true;
-        run_class<4, SEEDED>(P, cls[1], n1, wave_id, nwaves, lane, L);
-    }
+    const uint32_t n23 = cls[6] + cls[7];
     if (n23) {
-        if (staged) __syncthreads();
-        stage_tables(im.img[2]);
-        run_class<16, SEEDED>(P, cls[6] ? cls[2] : cls[3], n23, wave_id, nwaves, lane, L);
+        auto pool = [&]() -> uint64_t {
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
+            return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+        };
+        sorted_stream<16, SEEDED>(sub_list(P, cls[6] ? cls[2] : cls[3], n23), lane, L, pool(), pool);
     }
 }
 
@@ -1485,14 +1520,13 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     P.flags = flags;
     P.ent = ent;
     P.sseed = seed ? sseed : nullptr;
-    lvk::Images im;
-    for (int k = 0; k < 3; ++k) im.img[k] = c.image[k];
+
     if (seed)
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<true>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0,
-                           s, P, im, ws);
+                           s, P, c.image[2], ws);
     else
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<false>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads),
-                           0, s, P, im, ws);
+                           0, s, P, c.image[2], ws);
     return 0;
 }
 
