@@ -612,11 +612,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     constexpr uint64_t kRow = 16ull * G;       // bytes between rows of a batch
     constexpr uint64_t kBatch = kRow * U;      // bytes per batch
     const uint32_t gl = lane % G;
-    uint64_t blk = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * kGroups + lane / G;
-    const uint64_t gstride = static_cast<uint64_t>(gridDim.x) * kWaves * kGroups;
+#ifndef LVK_BLK_WAVES
+#define LVK_BLK_WAVES 16
+#endif
+    constexpr uint32_t kW = LVK_BLK_WAVES;  // streaming waves per workgroup
+    if (wave >= kW) return;
+    uint64_t blk = (static_cast<uint64_t>(blockIdx.x) * kW + wave) * kGroups + lane / G;
+    const uint64_t gstride = static_cast<uint64_t>(gridDim.x) * kW * kGroups;
     // Rounds of blocks are wave-uniform: the wave runs while its first group
     // has a block; groups past the end are masked.
-    const uint64_t wblk0 = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * kGroups;
+    const uint64_t wblk0 = (static_cast<uint64_t>(blockIdx.x) * kW + wave) * kGroups;
     if (wblk0 >= P.n) return;
     const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
     auto block_ptr = [&](uint64_t k) { return P.base + (k < P.n ? k : 0) * P.stride + 16u * gl; };
@@ -707,15 +712,13 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     return c * kBuckets + (kBuckets - 1 - nb);
 }
 
-// Sort workspace, 16-B aligned.  Header (u32 words): [0, 256) key start
-// (cursor base) per key; [256, 264) class start x4, count x4; [264, 520)
-// per-key totals; [520] scan ticket (zero between calls: the last scan
-// workgroup resets it).  Then the per-workgroup histogram matrix M[wgs][256],
+// Sort workspace, 16-B aligned.  Header (u32 words): [0, 256) unused;
+// [256, 264) class start x4, count x4; [264, 520) per-key totals; [520, 528)
+// unused.  Then the per-workgroup histogram matrix M[wgs][256],
 // then n sorted 16-B entries, then n seeds in entry order.
 constexpr uint32_t kWsCls = kKeys;
 constexpr uint32_t kWsTot = kKeys + 8;
-constexpr uint32_t kWsTicket = kWsTot + kKeys;
-constexpr uint32_t kWsHeader = kWsTicket + 8;  // 528 words, 16-B multiple
+constexpr uint32_t kWsHeader = kWsTot + kKeys + 8;  // 528 words, 16-B multiple
 constexpr uint32_t kSortChunk = kSortThreads * kSortE;  // elements per sorting workgroup (n <= 4M)
 constexpr uint32_t kSortMaxWgs = 1024;
 constexpr uint32_t kScanWgs = kKeys / 16;  // 16 keys per scan workgroup
@@ -791,14 +794,14 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__rest
 
 // Pass 2: column scan of M.  Workgroup b owns keys [16b, 16b+16); thread
 // (sub, kl) sums rows [sub*R, sub*R+R) of key 16b+kl, the 64 partial sums
-// are scanned in LDS, and M[w][k] becomes the offset of workgroup w's first
-// key-k entry within key k.  The last workgroup (ticket; 16 arrivals) scans
-// the key totals into key starts and per-class [start, count).
+// per key are scanned in LDS (Hillis-Steele over sub), and M[w][k] becomes
+// the offset of workgroup w's first key-k entry within key k; the key totals
+// go to the header.  No fence or ticket: the key starts are scanned by each
+// scatter workgroup after the kernel boundary (a device-scope release here
+// writes back the L2 and cost more than this whole pass).
 __global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__ M, uint32_t wgs,
                                                           uint32_t *__restrict__ ws) {
     __shared__ uint32_t part[64][16];
-    __shared__ uint32_t sc[kKeys];
-    __shared__ bool last;
     const uint32_t t = threadIdx.x, kl = t & 15u, sub = t >> 4;
     const uint32_t k = blockIdx.x * 16u + kl;
     const uint32_t R = (wgs + 63u) / 64u;  // <= 16
@@ -812,51 +815,35 @@ __global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__
     }
     part[sub][kl] = sum;
     __syncthreads();
-    if (sub == 0) {
-        uint32_t run = 0;
-        for (uint32_t q = 0; q < 64; ++q) {
-            const uint32_t x = part[q][kl];
-            part[q][kl] = run;
-            run += x;
-        }
-        ws[kWsTot + k] = run;
+    for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive scan over sub
+        const uint32_t x = sub >= d ? part[sub - d][kl] : 0u;
+        __syncthreads();
+        part[sub][kl] += x;
+        __syncthreads();
     }
-    __syncthreads();
-    uint32_t run = part[sub][kl];
+    if (sub == 63) ws[kWsTot + k] = part[63][kl];
+    uint32_t run = part[sub][kl] - sum;  // exclusive
 #pragma unroll
     for (uint32_t r = 0; r < 16; ++r) {
         if (r < R && r0 + r < wgs) M[static_cast<uint64_t>(r0 + r) * kKeys + k] = run;
         run += v[r];
     }
-    __threadfence();
+}
+
+// Exclusive scan of the 256 key totals (one per thread of a 256-thread
+// workgroup) into sc[]; returns this thread's key start.
+__device__ __forceinline__ uint32_t key_starts(const uint32_t *ws, uint32_t *sc) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t mine = ws[kWsTot + t];
+    sc[t] = mine;
     __syncthreads();
-    if (t == 0) last = atomicAdd(&ws[kWsTicket], 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    uint32_t mine = 0;
-    if (t < kKeys) {
-        mine = __hip_atomic_load(&ws[kWsTot + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sc[t] = mine;
-    }
-    __syncthreads();
-    for (uint32_t d = 1; d < kKeys; d <<= 1) {  // Hillis-Steele inclusive scan
-        uint32_t x = 0;
-        if (t < kKeys && t >= d) x = sc[t - d];
+    for (uint32_t d = 1; d < kKeys; d <<= 1) {
+        const uint32_t x = t >= d ? sc[t - d] : 0u;
         __syncthreads();
-        if (t < kKeys) sc[t] += x;
+        sc[t] += x;
         __syncthreads();
     }
-    if (t < kKeys) {
-        const uint32_t excl = sc[t] - mine;
-        ws[t] = excl;
-        if (t % kBuckets == 0) {
-            const uint32_t c = t / kBuckets;
-            ws[kWsCls + c] = excl;                             // start
-            ws[kWsCls + 4 + c] = sc[t + kBuckets - 1] - excl;  // count
-        }
-    }
-    if (t == 0) ws[kWsTicket] = 0;
+    return sc[t] - mine;
 }
 
 // Pass 3: same chunks as pass 1.  Workgroup w's slots for key k start at
@@ -867,14 +854,22 @@ __global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__
 // permuted alongside.
 __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__restrict__ off,
                                                              const uint32_t *__restrict__ len, uint64_t n,
-                                                             uint64_t chunk, const uint32_t *__restrict__ ws,
+                                                             uint64_t chunk, uint32_t *__restrict__ ws,
                                                              const uint32_t *__restrict__ M,
                                                              uint4 *__restrict__ ent,
                                                              const uint32_t *__restrict__ seed,
                                                              uint32_t *__restrict__ sseed) {
     __shared__ uint32_t cur[kKeys];
+    __shared__ uint32_t sc[kKeys];
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    cur[t] = ws[t] + M[static_cast<uint64_t>(blockIdx.x) * kKeys + t];
+    const uint32_t mrow = M[static_cast<uint64_t>(blockIdx.x) * kKeys + t];
+    const uint32_t ks = key_starts(ws, sc);
+    cur[t] = ks + mrow;
+    if (blockIdx.x == 0 && t % kBuckets == 0) {  // per-class [start, count) for the CRC kernel
+        const uint32_t c = t / kBuckets;
+        ws[kWsCls + c] = ks;
+        ws[kWsCls + 4 + c] = sc[t + kBuckets - 1] - ks;
+    }
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortChunk) {
