@@ -725,43 +725,34 @@ constexpr uint32_t kScanWgs = kKeys / 16;  // 16 keys per scan workgroup
 constexpr uint32_t kScanThreads = 1024;    // 16 keys x 64 row ranges
 static_assert(kSortMaxWgs <= 64 * 16, "scan: 64 row ranges of <= 16 rows");
 
-// h[k] += 1 for each valid lane's key k, aggregated per wave: up to four
-// passes over the wave's distinct keys (one LDS atomic per key) -- a uniform
-// batch has one key, and thousands of same-address LDS atomics serialize --
-// then plain per-lane atomics for whatever keys remain.
+// h[k] += 1 for each valid lane's key k.  A wave whose valid lanes share one
+// key (a uniform batch: thousands of same-address LDS atomics would
+// serialize) adds its count with one atomic; otherwise each lane adds its own.
 __device__ __forceinline__ void wave_count(uint32_t *h, uint32_t k, bool valid, uint32_t lane) {
-    uint64_t rem = __ballot(valid);
-#pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {
-        if (!rem) return;  // wave-uniform
-        const int leader = __ffsll(static_cast<long long>(rem)) - 1;
-        const uint32_t kl = __shfl(k, leader);
-        const uint64_t m = __ballot(valid && k == kl);
-        if (static_cast<int>(lane) == leader) atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(m)));
-        rem &= ~m;
+    const uint64_t act = __ballot(valid);
+    if (!act) return;  // wave-uniform
+    const int leader = __ffsll(static_cast<long long>(act)) - 1;
+    const uint32_t kl = __shfl(k, leader);
+    if (__ballot(valid && k != kl) == 0) {
+        if (static_cast<int>(lane) == leader) atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(act)));
+    } else if (valid) {
+        atomicAdd(&h[k], 1u);
     }
-    if ((rem >> lane) & 1ull) atomicAdd(&h[k], 1u);
 }
 
 // Like wave_count, but returns each valid lane's claimed slot h[k]++.
 __device__ __forceinline__ uint32_t wave_claim(uint32_t *h, uint32_t k, bool valid, uint32_t lane) {
-    uint64_t rem = __ballot(valid);
-    uint32_t pos = 0;
-    const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {
-        if (!rem) return pos;  // wave-uniform
-        const int leader = __ffsll(static_cast<long long>(rem)) - 1;
-        const uint32_t kl = __shfl(k, leader);
-        const uint64_t m = __ballot(valid && k == kl);
+    const uint64_t act = __ballot(valid);
+    if (!act) return 0;  // wave-uniform
+    const int leader = __ffsll(static_cast<long long>(act)) - 1;
+    const uint32_t kl = __shfl(k, leader);
+    if (__ballot(valid && k != kl) == 0) {
         uint32_t base = 0;
-        if (static_cast<int>(lane) == leader) base = atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(m)));
+        if (static_cast<int>(lane) == leader) base = atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(act)));
         base = __shfl(base, leader);
-        if (valid && k == kl) pos = base + static_cast<uint32_t>(__popcll(m & below));
-        rem &= ~m;
+        return base + static_cast<uint32_t>(__popcll(act & ((1ull << lane) - 1ull)));
     }
-    if ((rem >> lane) & 1ull) pos = atomicAdd(&h[k], 1u);
-    return pos;
+    return valid ? atomicAdd(&h[k], 1u) : 0u;
 }
 
 // Pass 1: per-workgroup key histogram of a contiguous chunk, in LDS, stored
