@@ -596,7 +596,7 @@ __device__ __forceinline__ uint32_t final_crc(const Params &P, uint32_t X) {
 
 // Every step issues the SAME loads (next batch, and for seeded calls the
 // next block's seed) whether or not a next batch exists -- the last one
-// re-reads the current batch.  The compiler's s_waitcnt counts are static:
+// reads the arena's first row.  The compiler's s_waitcnt counts are static:
 // if one path through a step skips the prefetch, the fold of the current
 // batch waits with the count of that path (vmcnt(2)..(0) after a 4-load
 // prefetch) and so for the prefetch itself, serialising load and compute in
@@ -604,35 +604,33 @@ __device__ __forceinline__ uint32_t final_crc(const Params &P, uint32_t X) {
 template <int G, bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint32_t nb,
                                                                  const uint4 *__restrict__ image) {
-    stage_tables(image);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
-    const Lut L = make_lut(lane);
     constexpr uint32_t kGroups = 64 / G;
     constexpr uint64_t kRow = 16ull * G;       // bytes between rows of a batch
     constexpr uint64_t kBatch = kRow * U;      // bytes per batch
     const uint32_t gl = lane % G;
-#ifndef LVK_BLK_WAVES
-#define LVK_BLK_WAVES 16
-#endif
-    constexpr uint32_t kW = LVK_BLK_WAVES;  // streaming waves per workgroup
-    if (wave >= kW) return;
+    constexpr uint32_t kW = kWaves;  // (8-16 streaming waves per CU measured alike)
     uint64_t blk = (static_cast<uint64_t>(blockIdx.x) * kW + wave) * kGroups + lane / G;
     const uint64_t gstride = static_cast<uint64_t>(gridDim.x) * kW * kGroups;
     // Rounds of blocks are wave-uniform: the wave runs while its first group
     // has a block; groups past the end are masked.
     const uint64_t wblk0 = (static_cast<uint64_t>(blockIdx.x) * kW + wave) * kGroups;
-    if (wblk0 >= P.n) return;
-    const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
     auto block_ptr = [&](uint64_t k) { return P.base + (k < P.n ? k : 0) * P.stride + 16u * gl; };
     auto seed_ld = [&](uint64_t k) { return ~P.seed[k < P.n ? k : 0]; };
 
+    // The first batch (and seed) is requested before the table image is
+    // staged, so its HBM latency overlaps the staging.
     uint64_t ptr = block_ptr(blk);
     uint32_t s0 = SEEDED ? seed_ld(blk) : 0xffffffffu;
     uint32_t s0n = s0;
     uint4 slot0[U], slot1[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) slot0[i] = load16(ptr + kRow * i);
+    stage_tables(image);
+    if (wblk0 >= P.n) return;
+    const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
+    const Lut L = make_lut(lane);
     uint32_t A[U];
     // The flush store's operands live in registers of their own for the whole
     // loop (kept live past it below), so no loop temporary reuses them: a
@@ -646,7 +644,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         const bool lastj = j + 1 == nb;
         const bool more = !lastj || r + 1 < rounds;
         const uint64_t nptr = lastj ? block_ptr(blk + gstride) : ptr + kBatch;
-        const uint64_t lptr = more ? nptr : ptr;  // no next batch: re-read this one
+        // no next batch: a dummy read of the arena's first row, the same lines
+        // for every wave (L2 hits)
+        const uint64_t lptr = more ? nptr : P.base + 16u * gl;
         if constexpr (SEEDED) s0n = seed_ld(blk + gstride);
 #pragma unroll
         for (uint32_t i = 0; i < U; ++i) nxt[i] = load16(lptr + kRow * i);
@@ -1460,8 +1460,8 @@ size_t sort_ws_bytes(uint64_t n) {
            n * (sizeof(uint4) + sizeof(uint32_t));
 }
 
-// The library-owned workspace of (device, stream), grown on demand; its
-// header is zeroed when allocated and every call leaves it zero again.
+// The library-owned workspace of (device, stream), grown on demand (the sort
+// needs no initialised state).
 int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out) {
     std::lock_guard<std::mutex> lk(c.ws_m);
     auto &w = c.ws[s];
@@ -1471,7 +1471,6 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out) {
         w.first = nullptr;
         w.second = 0;
         LV_HIP(hipMalloc(&w.first, need));
-        LV_HIP(hipMemsetAsync(w.first, 0, lvk::kWsHeader * sizeof(uint32_t), s));
         w.second = need;
     }
     *out = w.first;
@@ -1609,7 +1608,7 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
     if (d_ws) {
         if (ws_bytes < sort_ws_bytes(n)) return set_err(LV_ERR_INVALID, "workspace too small");
         if (reinterpret_cast<uintptr_t>(d_ws) % 16) return set_err(LV_ERR_INVALID, "workspace must be 16-byte aligned");
-        LV_HIP(hipMemsetAsync(d_ws, 0, lvk::kWsHeader * sizeof(uint32_t), s));  // caller's header: any state
+        // no initialisation: every workspace word the sort reads, it wrote first
     } else if (int rc = stream_ws(*c, s, n, &d_ws)) {
         return rc;
     }
