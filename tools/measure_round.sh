@@ -14,7 +14,8 @@ export TMPDIR=/tmp
 b() { local name=$1; shift; timeout -k 10 400 python3 bench.py "$@" > "$out/$name.json" 2> "$out/$name.err"; }
 p() { local name=$1; shift
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_$name" -o "$name" -- \
-         python3 "$root/bench.py" --steps 50 --warmup 100 --cpu-seconds 0 --traffic off "$@") > "$out/prof_$name.log" 2>&1; }
+         python3 "$root/bench.py" --steps 50 --warmup 100 --cpu-seconds 0 --traffic off "$@") > "$out/prof_$name.log" 2>&1 &&
+      python3 tools/kstats_steady.py "$(ls "$out/prof_$name"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_${name}_steady.json" > /dev/null; }
 b default &&
 b c3_offsets --workload c3 --api offsets --cpu-seconds 5 &&
 b c2 --workload c2 --api offsets --cpu-seconds 5 &&
