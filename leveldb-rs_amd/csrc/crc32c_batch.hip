@@ -1314,6 +1314,9 @@ struct DevCtx {
     size_t h_stage_cap[2] = {0, 0};
     hipEvent_t ev[2] = {nullptr, nullptr};
     hipStream_t stream = nullptr;
+    uint8_t *d_scr[2] = {nullptr, nullptr};  // scratch for other host paths (WAL scan)
+    size_t d_scr_cap[2] = {0, 0};
+    int dev = 0;
 };
 
 constexpr size_t kStageBytes = 64ull << 20;  // pinned staging slot for pageable input
@@ -1652,6 +1655,64 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
     return check_launch();
 }
 
+}  // extern "C"
+
+// Caller holds c.host_m.  Copies h[0, bytes) to c.d_arena and zeroes `pad`
+// bytes after it, on c.stream.
+static int upload_locked(DevCtx &c, const uint8_t *h, size_t bytes, size_t pad) {
+    if (!c.stream) LV_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    for (auto &ev : c.ev)
+        if (!ev) LV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipStream_t s = c.stream;
+    if (int rc = grow_dev(&c.d_arena, &c.d_arena_cap, bytes + (pad > 16 ? pad : 16))) return rc;
+    if (pad) LV_HIP(hipMemsetAsync(c.d_arena + bytes, 0, pad, s));
+    if (bytes == 0) return LV_OK;
+    // DMA straight from pinned/registered memory; otherwise a two-slot
+    // pipeline (parallel memcpy into one pinned slot while the other slot's
+    // H2D runs)
+    if (is_pinned(h)) {
+        LV_HIP(hipMemcpyAsync(c.d_arena, h, bytes, hipMemcpyHostToDevice, s));
+        return LV_OK;
+    }
+    for (int k = 0; k < 2; ++k)
+        if (int rc = grow_pinned(&c.h_stage[k], &c.h_stage_cap[k], kStageBytes)) return rc;
+    size_t k = 0;
+    for (size_t pos = 0; pos < bytes; pos += kStageBytes, ++k) {
+        const size_t len = bytes - pos < kStageBytes ? bytes - pos : kStageBytes;
+        const int slot = static_cast<int>(k & 1);
+        if (k >= 2) LV_HIP(hipEventSynchronize(c.ev[slot]));
+        par_memcpy(c.h_stage[slot], h + pos, len);
+        LV_HIP(hipMemcpyAsync(c.d_arena + pos, c.h_stage[slot], len, hipMemcpyHostToDevice, s));
+        LV_HIP(hipEventRecord(c.ev[slot], s));
+    }
+    return LV_OK;
+}
+
+namespace lvgpu_internal {
+int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath *hp) {
+    LV_HIP(hipSetDevice(device));
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    hp->lk = std::unique_lock<std::mutex>(c->host_m);
+    if (int rc = upload_locked(*c, h, bytes, pad)) return rc;
+    hp->stream = c->stream;
+    hp->d_arena = c->d_arena;
+    return LV_OK;
+}
+
+int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d) {
+    (void)hp;  // the lock it holds is the device's host_m
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    if (slot < 0 || slot > 1) return set_err(LV_ERR_INVALID, "scratch slot");
+    if (int rc = grow_dev(&c->d_scr[slot], &c->d_scr_cap[slot], bytes ? bytes : 16)) return rc;
+    *d = c->d_scr[slot];
+    return LV_OK;
+}
+}  // namespace lvgpu_internal
+
+extern "C" {
+
 int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off,
                          const uint32_t *h_len, const uint32_t *h_seed, uint32_t *h_out, size_t n,
                          uint32_t flags, int device) {
@@ -1666,12 +1727,9 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     std::lock_guard<std::mutex> lk(c->host_m);
-    if (!c->stream) LV_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (auto &ev : c->ev)
-        if (!ev) LV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (int rc = upload_locked(*c, h_arena, arena_bytes, 0)) return rc;
     hipStream_t s = c->stream;
     const size_t meta = n * (8 + 4 + 4 + 4);
-    if (int rc = grow_dev(&c->d_arena, &c->d_arena_cap, arena_bytes + 16)) return rc;
     if (int rc = grow_dev(&c->d_meta, &c->d_meta_cap, meta)) return rc;
     if (int rc = grow_pinned(&c->h_meta, &c->h_meta_cap, meta)) return rc;
     uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_meta);
@@ -1684,25 +1742,6 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     std::memcpy(c->h_meta + n * 8, h_len, n * 4);
     if (h_seed) std::memcpy(c->h_meta + n * 12, h_seed, n * 4);
     LV_HIP(hipMemcpyAsync(d_off, c->h_meta, n * (h_seed ? 16 : 12), hipMemcpyHostToDevice, s));
-
-    // payload: DMA straight from pinned/registered memory; otherwise a
-    // two-slot pipeline (parallel memcpy into one pinned slot while the other
-    // slot's H2D runs)
-    if (is_pinned(h_arena)) {
-        LV_HIP(hipMemcpyAsync(c->d_arena, h_arena, arena_bytes, hipMemcpyHostToDevice, s));
-    } else {
-        for (auto &st : c->h_stage)
-            if (int rc = grow_pinned(&st, &c->h_stage_cap[&st - c->h_stage], kStageBytes)) return rc;
-        size_t k = 0;
-        for (size_t pos = 0; pos < arena_bytes; pos += kStageBytes, ++k) {
-            const size_t len = arena_bytes - pos < kStageBytes ? arena_bytes - pos : kStageBytes;
-            const int slot = static_cast<int>(k & 1);
-            if (k >= 2) LV_HIP(hipEventSynchronize(c->ev[slot]));
-            par_memcpy(c->h_stage[slot], h_arena + pos, len);
-            LV_HIP(hipMemcpyAsync(c->d_arena + pos, c->h_stage[slot], len, hipMemcpyHostToDevice, s));
-            LV_HIP(hipEventRecord(c->ev[slot], s));
-        }
-    }
     uint8_t *ws = nullptr;
     if (int rc = stream_ws(*c, s, n, &ws)) return rc;
     if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s))

@@ -10,8 +10,23 @@ struct lv_wal_scan {
     std::vector<uint32_t> info;  // type | status << 8 | payload_length << 16
 };
 
+#include <mutex>
+
 namespace lvgpu_internal {
 int set_error(int code, const char *msg);  // lv_last_error plumbing (crc32c_batch.hip)
 void clear_error();
 int launch_status();                       // hipGetLastError -> LV status + message
+
+// Host-memory path of one device (crc32c_batch.hip): holds the device's
+// host-path lock while alive.  host_upload copies `bytes` of host memory into
+// the device's cached arena (pinned input: one DMA; pageable: a pipelined
+// pinned staging copy) followed by `pad` zero bytes, on the device's stream.
+struct HostPath {
+    std::unique_lock<std::mutex> lk;
+    void *stream = nullptr;     // hipStream_t
+    uint8_t *d_arena = nullptr;
+};
+int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath *hp);
+// Cached device scratch buffer `slot` (0..1) of the HostPath's device, >= bytes.
+int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d);
 }

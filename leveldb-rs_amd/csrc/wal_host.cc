@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lvgpu/crc32c.h"
@@ -339,12 +340,34 @@ int lv_wal_encode_host(const uint8_t *payload, const uint64_t *rec_off, const ui
     std::vector<uint32_t> len(frags.size()), seed(frags.size()), crc(frags.size());
     uint32_t type_crc[5];
     for (uint8_t t = 0; t < 5; ++t) type_crc[t] = lv_crc32c_value(&t, 1);  // log_writer.rs:136-142
-    for (size_t i = 0; i < frags.size(); ++i) {
-        const Frag &f = frags[i];
-        if (f.len) std::memcpy(out + f.out_pos + kHeader, payload + f.src, f.len);
-        off[i] = f.out_pos + kHeader;
-        len[i] = f.len;
-        seed[i] = type_crc[f.type];
+    // The payload copy is the host's share of the work (the whole log's
+    // bytes): split it over up to 8 threads by fragment ranges of equal bytes.
+    auto copy_range = [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            const Frag &f = frags[i];
+            if (f.len) std::memcpy(out + f.out_pos + kHeader, payload + f.src, f.len);
+            off[i] = f.out_pos + kHeader;
+            len[i] = f.len;
+            seed[i] = type_crc[f.type];
+        }
+    };
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt == 0 ? 1 : (nt > 8 ? 8 : nt);
+    if (pos < (8u << 20) || nt == 1 || frags.size() < 2 * nt) {
+        copy_range(0, frags.size());
+    } else {
+        std::vector<std::thread> th;
+        size_t lo = 0;
+        for (unsigned t = 1; t <= nt && lo < frags.size(); ++t) {
+            size_t hi = lo;
+            const uint64_t until = pos * t / nt;  // fragment i ends near out byte until
+            while (hi < frags.size() && (t == nt || frags[hi].out_pos < until)) ++hi;
+            if (hi == lo) continue;
+            th.emplace_back(copy_range, lo, hi);
+            lo = hi;
+        }
+        if (lo < frags.size()) copy_range(lo, frags.size());
+        for (auto &x : th) x.join();
     }
     if (!frags.empty()) {
         if (int rc = lv_crc32c_batch_host(out, pos, off.data(), len.data(), seed.data(), crc.data(), frags.size(),

@@ -83,22 +83,21 @@ namespace {
         }                                                                                  \
     } while (0)
 
-// Free scan buffers after the stream drains (errors here are not actionable).
-void release(hipStream_t s, std::initializer_list<void *> ptrs) {
-    if (s) (void)hipStreamSynchronize(s);
-    for (void *p : ptrs)
-        if (p) (void)hipFree(p);
-    if (s) (void)hipStreamDestroy(s);
-}
+constexpr size_t align16(size_t x) { return (x + 15) & ~static_cast<size_t>(15); }
 
 }  // namespace
 
+// The log goes to the device through the device's host path (cached arena;
+// pinned input: one DMA, pageable: pipelined pinned staging) and every device
+// array comes from its cached scratch buffers, so a scan allocates nothing on
+// the device after the first call.
 extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int device) {
     lv_wal_scan *scan = new lv_wal_scan();
-    uint8_t *d_log = nullptr, *d_tmp = nullptr;
+    lvgpu_internal::HostPath hp;
+    hipStream_t s = nullptr;
+    uint8_t *d_log = nullptr, *scr0 = nullptr, *scr1 = nullptr, *d_tmp = nullptr;
     uint32_t *d_counts = nullptr, *d_first = nullptr, *d_len = nullptr, *d_info = nullptr, *d_crc = nullptr;
     uint64_t *d_hdr = nullptr, *d_unit = nullptr;
-    hipStream_t s = nullptr;
     size_t tmp_bytes = 0;
     uint32_t last_first = 0, last_count = 0, total = 0;
     const uint64_t nblocks = (bytes + lvw::kBlock - 1) / lvw::kBlock;
@@ -113,31 +112,32 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
         delete scan;
         return nullptr;
     }
-    WAL_HIP(hipSetDevice(device));
-    WAL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    WAL_HIP(hipMalloc(&d_log, bytes + 16));
-    WAL_HIP(hipMemsetAsync(d_log + bytes, 0, 16, s));
-    WAL_HIP(hipMemcpyAsync(d_log, log, bytes, hipMemcpyHostToDevice, s));
-    WAL_HIP(hipMalloc(&d_counts, nblocks * 4));
-    WAL_HIP(hipMalloc(&d_first, nblocks * 4));
+    if (lvgpu_internal::host_upload(device, log, bytes, 16, &hp)) goto fail;  // 16 zero bytes: load8's 2nd word
+    s = static_cast<hipStream_t>(hp.stream);
+    d_log = hp.d_arena;
+    WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_counts, d_first, nblocks, s));
+    if (lvgpu_internal::host_scratch(&hp, 0, align16(nblocks * 4) * 2 + tmp_bytes, &scr0)) goto fail;
+    d_counts = reinterpret_cast<uint32_t *>(scr0);
+    d_first = reinterpret_cast<uint32_t *>(scr0 + align16(nblocks * 4));
+    d_tmp = scr0 + 2 * align16(nblocks * 4);
     {
         const uint32_t grid = static_cast<uint32_t>((nblocks + 255) / 256);
         hipLaunchKernelGGL(lvw::frame_blocks<false>, dim3(grid), dim3(256), 0, s, d_log, bytes, nblocks, d_counts,
                            nullptr, nullptr, nullptr, nullptr, nullptr);
         WAL_HIP(hipGetLastError());
-        WAL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_counts, d_first, nblocks, s));
-        WAL_HIP(hipMalloc(&d_tmp, tmp_bytes));
         WAL_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_counts, d_first, nblocks, s));
         WAL_HIP(hipMemcpyAsync(&last_first, d_first + nblocks - 1, 4, hipMemcpyDeviceToHost, s));
         WAL_HIP(hipMemcpyAsync(&last_count, d_counts + nblocks - 1, 4, hipMemcpyDeviceToHost, s));
         WAL_HIP(hipStreamSynchronize(s));
         total = last_first + last_count;
         if (total) {
-            WAL_HIP(hipMalloc(&d_hdr, total * 8ull));
-            WAL_HIP(hipMalloc(&d_unit, total * 8ull));
-            WAL_HIP(hipMalloc(&d_len, total * 4ull));
-            WAL_HIP(hipMalloc(&d_info, total * 4ull));
-            WAL_HIP(hipMalloc(&d_crc, total * 4ull));
+            const size_t t8 = align16(total * 8ull), t4 = align16(total * 4ull);
+            if (lvgpu_internal::host_scratch(&hp, 1, 2 * t8 + 3 * t4, &scr1)) goto fail;
+            d_hdr = reinterpret_cast<uint64_t *>(scr1);
+            d_unit = reinterpret_cast<uint64_t *>(scr1 + t8);
+            d_len = reinterpret_cast<uint32_t *>(scr1 + 2 * t8);
+            d_info = reinterpret_cast<uint32_t *>(scr1 + 2 * t8 + t4);
+            d_crc = reinterpret_cast<uint32_t *>(scr1 + 2 * t8 + 2 * t4);
             hipLaunchKernelGGL(lvw::frame_blocks<true>, dim3(grid), dim3(256), 0, s, d_log, bytes, nblocks, nullptr,
                                d_first, d_hdr, d_unit, d_len, d_info);
             WAL_HIP(hipGetLastError());
@@ -154,10 +154,9 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
             WAL_HIP(hipStreamSynchronize(s));
         }
     }
-    release(s, {d_log, d_tmp, d_counts, d_first, d_hdr, d_unit, d_len, d_info, d_crc});
     return scan;
 fail:
-    release(s, {d_log, d_tmp, d_counts, d_first, d_hdr, d_unit, d_len, d_info, d_crc});
+    if (s) (void)hipStreamSynchronize(s);
     delete scan;
     return nullptr;
 }
