@@ -40,7 +40,9 @@ def parse():
     # warmup covers that transient so the timed steps are steady state.
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=100)
-    p.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"])
+    p.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "kib", "tiny"],
+                   help="c2-c5: SURVEY 8d configs; kib (1 M x 1 KiB) and tiny (1 M x 1-64 B): "
+                        "offsets-API diagnostics for the small length classes")
     p.add_argument("--api", default="strided", choices=["offsets", "strided"],
                    help="strided = lv_crc32c_batch_strided (fixed-size table blocks); "
                         "offsets = lv_crc32c_batch_device (arbitrary buffers)")
@@ -86,6 +88,9 @@ def build_workload(torch, lvgpu, name, dev, rank, blocks=None):
         k = np.minimum(k, 2048)
         lens = (32 * k).astype(np.uint32)
         desc = "c4: 1,048,576 buffers, L = 32*k, k ~ Zipf(1.1) on 1..2048, byte-packed"
+    elif name in ("kib", "tiny"):
+        lens = (np.full(1048576, 1024) if name == "kib" else rng.integers(1, 65, 1048576)).astype(np.uint32)
+        desc = f"{name}: 1,048,576 buffers of " + ("1 KiB" if name == "kib" else "1-64 B") + ", byte-packed"
     else:  # c2: WAL physical records from Random(301).skewed(17) record sizes
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         lens = wal_unit_lengths(1048576)

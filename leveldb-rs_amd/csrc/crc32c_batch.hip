@@ -1193,8 +1193,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     const Lut L = make_lut(lane);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t grid = gridDim.x;
-    if (wave < kSmallWaves) {
-        const uint64_t sw = blockIdx.x * kSmallWaves + wave, nsw = grid * kSmallWaves;
+    const uint32_t n23 = cls[6] + cls[7];
+    // With no large buffers at all, every wave walks the small classes.
+    const uint32_t nsmall = n23 ? kSmallWaves : kWaves;
+    if (wave < nsmall) {
+        const uint64_t sw = blockIdx.x * nsmall + wave, nsw = grid * nsmall;
         uint64_t k = 0;
         auto stride = [&]() { return sw + (++k) * nsw; };
         if (cls[4]) {
@@ -1203,7 +1206,6 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         }
         if (cls[5]) sorted_stream<4, SEEDED>(sub_list(P, cls[1], cls[5]), lane, L, sw, stride);
     }
-    const uint32_t n23 = cls[6] + cls[7];
     if (n23) {
         auto pool = [&]() -> uint64_t {
             uint32_t k = 0;
