@@ -454,10 +454,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # LVGPU_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs
+    # than ranks (ranks share devices round-robin; RCCL refuses two ranks on
+    # one device).  The data path has no collective either way.
+    backend = os.environ.get("LVGPU_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     lvgpu.device_init()
@@ -494,7 +500,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

@@ -170,8 +170,26 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 // W4K < 0: W4 = the Latin half of region A (Shift_{64G} for the image's G);
 // W4K = k >= 0: W4 = plain combine table k (Shift_{16*2^k}) -- how groups of
 // G = 1 and 4 run on a G = 16 image (Shift_64 = k 2, Shift_256 = k 4).
+// Experiment switches (wrong CRCs; timing studies only, never built into
+// the product library, tools/build_variant.sh): LVK_EXP_NOSHIFT drops the
+// row-shift lookups, LVK_EXP_NOFOLD all lookups (the load structure alone),
+// LVK_EXP_NOSTAGE the blocks kernel's table staging.
+#ifndef LVK_EXP_NOSHIFT
+#define LVK_EXP_NOSHIFT 0
+#endif
+#ifndef LVK_EXP_NOFOLD
+#define LVK_EXP_NOFOLD 0
+#endif
+#ifndef LVK_EXP_NOSTAGE
+#define LVK_EXP_NOSTAGE 0
+#endif
 template <bool FIRST, int W4K = -1>
 __device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U], const Lut &L) {
+#if LVK_EXP_NOFOLD  // experiment only: no lookups at all (load-structure bound)
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) A[i] = (FIRST ? 0u : A[i]) ^ xor3(v[i].x, v[i].y, v[i].z) ^ v[i].w;
+    return;
+#endif
     uint32_t s[U], w[U], w3[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) s[i] = v[i].x;
@@ -179,6 +197,12 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U]
 #pragma unroll
         for (uint32_t i = 0; i < U; ++i) {
             w[i] = comb_shift(A[i], W4K);
+            w3[i] = 0u;
+        }
+    } else if constexpr (!FIRST && LVK_EXP_NOSHIFT) {  // experiment only: wrong CRCs
+#pragma unroll
+        for (uint32_t i = 0; i < U; ++i) {
+            w[i] = A[i];
             w3[i] = 0u;
         }
     } else if constexpr (!FIRST) {
@@ -567,6 +591,27 @@ __global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(Params P, const 
 // group returns the (optionally masked) CRC.
 // W1K/W2K < 0: the image's Latin W1/W2 (region B); k >= 0: plain combine
 // table k (for G = 1, 4 on a G = 16 image: Shift_16G, Shift_32G).
+// x of lane l + 2^k.  Within 16-lane rows (k < 4) one DPP row_shl move
+// (VALU, no LDS round trip); lanes past the row end read 0, and only lanes
+// whose tree stays inside their group use the value, so G <= 16 groups never
+// see it.  Wider steps go through ds_bpermute.
+#ifndef LVK_DPP_TREE
+#define LVK_DPP_TREE 1
+#endif
+template <int G>
+__device__ __forceinline__ uint32_t lanes_down(uint32_t x, int k) {
+#if LVK_DPP_TREE
+    switch (k) {
+    case 0: return __builtin_amdgcn_mov_dpp(x, 0x101, 0xf, 0xf, true);
+    case 1: return __builtin_amdgcn_mov_dpp(x, 0x102, 0xf, 0xf, true);
+    case 2: return __builtin_amdgcn_mov_dpp(x, 0x104, 0xf, 0xf, true);
+    case 3: return __builtin_amdgcn_mov_dpp(x, 0x108, 0xf, 0xf, true);
+    default: break;
+    }
+#endif
+    return __shfl_down(x, 1u << k, G);
+}
+
 template <int G, int W1K = -1, int W2K = -1>
 __device__ __forceinline__ uint32_t merge_group(const uint32_t (&A)[U], const Lut &L) {
     uint32_t x01, x23, X;
@@ -583,7 +628,7 @@ __device__ __forceinline__ uint32_t merge_group(const uint32_t (&A)[U], const Lu
         X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
 #pragma unroll
     for (int k = 0; (1 << k) < G; ++k) {
-        const uint32_t other = __shfl_down(X, 1u << k, G);
+        const uint32_t other = lanes_down<G>(X, k);
         X = comb_shift(X, k) ^ other;
     }
     return X;
@@ -627,7 +672,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     uint4 slot0[U], slot1[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) slot0[i] = load16(ptr + kRow * i);
+#if !LVK_EXP_NOSTAGE
     stage_tables(image);
+#endif
     if (wblk0 >= P.n) return;
     const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
     const Lut L = make_lut(lane);

@@ -20,7 +20,25 @@ __global__ __launch_bounds__(1024) void probe_stream(const u32x4* __restrict__ p
   if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <int G, int U>
+template <bool NT>
+__global__ __launch_bounds__(1024) void probe_stream_u(const u32x4* __restrict__ p, uint64_t n16, uint32_t* out) {
+  // 4 independent 16-B loads per lane per iteration, 64 KiB per workgroup-iteration
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x * 4 + threadIdx.x; i < n16; i += stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      g_u32x4* q = (g_u32x4*)p + i + j * blockDim.x;
+      v[j] = NT ? __builtin_nontemporal_load(q) : *q;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int G, int U, bool NT = false>
 __global__ __launch_bounds__(1024) void probe_groups(const u32x4* __restrict__ p, uint64_t nblocks, uint32_t blk16, uint32_t* out) {
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t gid = ((uint64_t)blockIdx.x * 16 + wave) * (64 / G) + lane / G;
@@ -31,9 +49,33 @@ __global__ __launch_bounds__(1024) void probe_groups(const u32x4* __restrict__ p
     for (uint32_t r = 0; r < blk16 / G; r += U) {
       u32x4 v[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) v[j] = q[(r + j) * G];
+      for (int j = 0; j < U; ++j) v[j] = NT ? __builtin_nontemporal_load(q + (r + j) * G) : q[(r + j) * G];
 #pragma unroll
       for (int j = 0; j < U; ++j) acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// G lanes per 4 KiB block, each lane owning 32 contiguous bytes of a 32*G-byte
+// row (two 16-B loads at +0 and +16), U rows per batch, nt
+template <int G, int U>
+__global__ __launch_bounds__(1024) void probe_pairs(const u32x4* __restrict__ p, uint64_t nblocks, uint32_t blk16, uint32_t* out) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t gid = ((uint64_t)blockIdx.x * 16 + wave) * (64 / G) + lane / G;
+  const uint64_t gstride = (uint64_t)gridDim.x * 16 * (64 / G);
+  uint32_t acc = 0;
+  for (uint64_t b = gid; b < nblocks; b += gstride) {
+    const g_u32x4* q = (g_u32x4*)p + b * blk16 + 2 * (lane % G);
+    for (uint32_t r = 0; r < blk16 / (2 * G); r += U) {
+      u32x4 v[U][2];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        v[j][0] = __builtin_nontemporal_load(q + (r + j) * 2 * G);
+        v[j][1] = __builtin_nontemporal_load(q + (r + j) * 2 * G + 1);
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) acc ^= v[j][0].x ^ v[j][0].y ^ v[j][0].z ^ v[j][0].w ^ v[j][1].x ^ v[j][1].w;
     }
   }
   if (acc == 0x12345678u) out[0] = acc;
@@ -48,9 +90,9 @@ int main() {
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
   auto run = [&](const char* name, auto launch) {
     std::vector<float> ts;
-    for (int it = 0; it < 23; ++it) {
+    for (int it = 0; it < 100; ++it) {
       hipEventRecord(a); launch(); hipEventRecord(b); hipEventSynchronize(b);
-      float ms; hipEventElapsedTime(&ms, a, b); if (it >= 3) ts.push_back(ms);
+      float ms; hipEventElapsedTime(&ms, a, b); if (it >= 60) ts.push_back(ms);
     }
     std::sort(ts.begin(), ts.end());
     printf("%-40s median %.4f ms  %.0f GB/s  (min %.4f ms %.0f GB/s)\n", name, ts[ts.size()/2], bytes / (ts[ts.size()/2] * 1e-3) / 1e9, ts[0], bytes / (ts[0]*1e-3)/1e9);
@@ -66,5 +108,19 @@ int main() {
   run("groups G=4 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<4,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("groups G=1 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<1,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("groups G=16 U=4 4KiB wg=2cus", [&] { hipLaunchKernelGGL((probe_groups<16,4>), dim3(2*cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  for (int wgs : {cus, 2 * cus, 4 * cus}) {
+    char nm[64]; snprintf(nm, 64, "stream4 nt wg=%d x1024", wgs);
+    run(nm, [&] { hipLaunchKernelGGL(probe_stream_u<true>, dim3(wgs), dim3(1024), 0, 0, d, bytes / 16, o); });
+    snprintf(nm, 64, "stream4 rt wg=%d x1024", wgs);
+    run(nm, [&] { hipLaunchKernelGGL(probe_stream_u<false>, dim3(wgs), dim3(1024), 0, 0, d, bytes / 16, o); });
+  }
+  run("groups nt G=16 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<16,4,true>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("groups nt G=16 U=8 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<16,8,true>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("groups nt G=64 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<64,4,true>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("groups nt G=16 U=4 4KiB wg=2cus", [&] { hipLaunchKernelGGL((probe_groups<16,4,true>), dim3(2*cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("pairs nt G=16 U=2 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<16,2>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("pairs nt G=16 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<16,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("pairs nt G=8 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<8,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("pairs nt G=32 U=2 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<32,2>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   return 0;
 }
