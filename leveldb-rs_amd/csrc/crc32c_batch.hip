@@ -591,28 +591,26 @@ __global__ __launch_bounds__(kThreads) void crc32c_batch_kernel(Params P, const 
 // group returns the (optionally masked) CRC.
 // W1K/W2K < 0: the image's Latin W1/W2 (region B); k >= 0: plain combine
 // table k (for G = 1, 4 on a G = 16 image: Shift_16G, Shift_32G).
-// x of lane l + 2^k.  Within 16-lane rows (k < 4) one DPP row_shl move
+// x of lane l + 2^k.  DPP: within 16-lane rows (k < 4) one row_shl move
 // (VALU, no LDS round trip); lanes past the row end read 0, and only lanes
 // whose tree stays inside their group use the value, so G <= 16 groups never
-// see it.  Wider steps go through ds_bpermute.
-#ifndef LVK_DPP_TREE
-#define LVK_DPP_TREE 1
-#endif
-template <int G>
+// see it.  Wider steps go through ds_bpermute.  Measured: blocks kernel
+// +0.4 % with DPP; class kernel -1 % (C2) / -2 % (C4), so it keeps bpermute.
+template <int G, bool DPP>
 __device__ __forceinline__ uint32_t lanes_down(uint32_t x, int k) {
-#if LVK_DPP_TREE
-    switch (k) {
-    case 0: return __builtin_amdgcn_mov_dpp(x, 0x101, 0xf, 0xf, true);
-    case 1: return __builtin_amdgcn_mov_dpp(x, 0x102, 0xf, 0xf, true);
-    case 2: return __builtin_amdgcn_mov_dpp(x, 0x104, 0xf, 0xf, true);
-    case 3: return __builtin_amdgcn_mov_dpp(x, 0x108, 0xf, 0xf, true);
-    default: break;
+    if constexpr (DPP) {
+        switch (k) {
+        case 0: return __builtin_amdgcn_mov_dpp(x, 0x101, 0xf, 0xf, true);
+        case 1: return __builtin_amdgcn_mov_dpp(x, 0x102, 0xf, 0xf, true);
+        case 2: return __builtin_amdgcn_mov_dpp(x, 0x104, 0xf, 0xf, true);
+        case 3: return __builtin_amdgcn_mov_dpp(x, 0x108, 0xf, 0xf, true);
+        default: break;
+        }
     }
-#endif
     return __shfl_down(x, 1u << k, G);
 }
 
-template <int G, int W1K = -1, int W2K = -1>
+template <int G, int W1K = -1, int W2K = -1, bool DPP = false>
 __device__ __forceinline__ uint32_t merge_group(const uint32_t (&A)[U], const Lut &L) {
     uint32_t x01, x23, X;
     if constexpr (W1K >= 0) {
@@ -628,7 +626,7 @@ __device__ __forceinline__ uint32_t merge_group(const uint32_t (&A)[U], const Lu
         X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
 #pragma unroll
     for (int k = 0; (1 << k) < G; ++k) {
-        const uint32_t other = lanes_down<G>(X, k);
+        const uint32_t other = lanes_down<G, DPP>(X, k);
         X = comb_shift(X, k) ^ other;
     }
     return X;
@@ -706,7 +704,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         if (lastj) {
             // round r's K results -> LDS slot (r % G)*K + group; one store of
             // the wave's 64 slots every G rounds (and after the last round)
-            const uint32_t X = merge_group<G>(A, L);
+            const uint32_t X = merge_group<G, -1, -1, true>(A, L);
             if (gl == 0) g_ocrc[wave][(r % G) * kGroups + lane / G] = final_crc(P, X);
             if ((r + 1) % G == 0 || r + 1 == rounds) {
                 __builtin_amdgcn_wave_barrier();
@@ -1211,6 +1209,9 @@ __device__ __forceinline__ Params sub_list(const Params &P0, uint32_t start, uin
 #define LVK_SMALL_WAVES 4
 #endif
 constexpr uint32_t kSmallWaves = LVK_SMALL_WAVES;
+#ifndef LVK_SMALL_ALL
+#define LVK_SMALL_ALL 1
+#endif
 
 // Next round of the workgroup's large-buffer share: a word of combine table
 // k = 5 (Shift_512), which no group of the class kernel uses, since the LDS
@@ -1242,7 +1243,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     const uint64_t grid = gridDim.x;
     const uint32_t n23 = cls[6] + cls[7];
     // With no large buffers at all, every wave walks the small classes.
+#if LVK_SMALL_ALL
     const uint32_t nsmall = n23 ? kSmallWaves : kWaves;
+#else
+    constexpr uint32_t nsmall = kSmallWaves;
+#endif
     if (wave < nsmall) {
         const uint64_t sw = blockIdx.x * nsmall + wave, nsw = grid * nsmall;
         uint64_t k = 0;

@@ -333,3 +333,40 @@ def test_sorted_walk_edges(torch_dev, arena):
     got = gpu_batch(torch, dev, arena, offs, lens, seeds, True)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(offs[i], lens[i]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("workload", ["c2", "c4"])
+def test_full_size_offsets_api(torch_dev, workload):
+    """Configs 2 and 4 at full size (1,048,576 byte-packed buffers, 5.6-5.8 GiB,
+    exactly bench.py's workloads): every CRC of lv_crc32c_batch_device
+    bit-exact vs the oracle, unseeded, and seeded + masked with random seeds."""
+    torch, dev = torch_dev
+    import bench
+    arena, off, ln, nbytes, _ = bench.build_workload(torch, lvgpu, workload, dev, 0)
+    out = lvgpu.batch(arena, off, ln)
+    rng = np.random.default_rng(11)
+    seeds = rng.integers(0, 2**32, size=off.numel(), dtype=np.uint64).astype(np.uint32)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out_s = lvgpu.batch(arena, off, ln, sd, masked=True)
+    torch.cuda.synchronize()
+    host = arena.cpu().numpy()
+    o = off.cpu().numpy().astype(np.uint64)
+    n = ln.cpu().numpy().view(np.uint32)
+    assert int(n.astype(np.uint64).sum()) == nbytes
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle_batch(host, o, n, None, False))
+    assert np.array_equal(out_s.cpu().numpy().view(np.uint32), oracle_batch(host, o, n, seeds, True))
+
+
+def test_full_size_c5_shard(torch_dev):
+    """Config 5's per-GPU shard at full size: 2,097,152 x 4 KiB = 8 GiB through
+    the uniform-block kernel, every CRC bit-exact vs the oracle."""
+    torch, dev = torch_dev
+    import bench
+    arena, off, ln, nbytes, _ = bench.build_workload(torch, lvgpu, "c5", dev, 0)
+    n = off.numel()
+    out = lvgpu.batch_strided(arena, 4096, 4096, n)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    host = arena.cpu().numpy()
+    want = oracle_batch(host, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096, np.uint32), None, False)
+    assert np.array_equal(got, want)

@@ -118,6 +118,11 @@ int main() {
   run("groups nt G=16 U=8 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<16,8,true>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("groups nt G=64 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<64,4,true>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("groups nt G=16 U=4 4KiB wg=2cus", [&] { hipLaunchKernelGGL((probe_groups<16,4,true>), dim3(2*cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  // rows not 128-B aligned (the offsets API's end-aligned rows of byte-packed buffers)
+  for (int sh : {16, 48, 64, 112}) {
+    char nm[64]; snprintf(nm, 64, "groups nt G=16 U=4 4KiB +%dB", sh);
+    run(nm, [&] { hipLaunchKernelGGL((probe_groups<16,4,true>), dim3(cus), dim3(1024), 0, 0, d + sh / 16, nb - 1, 256u, o); });
+  }
   run("pairs nt G=16 U=2 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<16,2>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("pairs nt G=16 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<16,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("pairs nt G=8 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<8,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
