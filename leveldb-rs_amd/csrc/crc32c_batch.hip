@@ -1095,6 +1095,116 @@ __device__ __forceinline__ uint32_t fold_tail(uint32_t X, uint4 V, const RGeo &q
     return X;
 }
 
+// ---- 256-B-aligned rows (the G = 16 classes) ----
+// End-aligned rows of byte-packed buffers sit off the 128-B line grid: a
+// 256-B group row then touches 3 lines instead of 2, and such rows read 11 %
+// slower (6.12 vs 6.86 TB/s, tools/hbm_read_probe).  The G = 16 walk
+// therefore puts rows on the absolute 256-B grid.  u = granule index from the
+// 256-B boundary at or below the buffer start (g0 = u ph); the last whole
+// granule u_e = ph + ng - 1 sits in row R_e, lane e, and R_e is row 3 of the
+// last batch.  Granules before g0 and after u_e are zero in registers.  With
+// lanes l > e read as belonging to the row BEFORE (their last data row is
+// R_e - 1), every lane's distance to the end is 16 * (15 - l') for the
+// rotated lane index l' = (l - e - 1) mod 16, so one lane rotation per buffer
+// turns the ordinary merge tree into the exact CRC (merge_al).
+#ifndef LVK_AL_RT_LAST
+#define LVK_AL_RT_LAST 0
+#endif
+struct AGeo {
+    int32_t ph;  // granule phase of g0 in its 256-B row
+    int32_t re;  // row of the last whole granule (from ph's row)
+    int32_t e;   // its lane
+};
+
+__device__ __forceinline__ AGeo al_geo(const RGeo &q) {
+    AGeo g;
+    g.ph = static_cast<int32_t>((q.abase() >> 4) & 15u);
+    const int32_t ue = g.ph + static_cast<int32_t>(q.ng()) - 1;
+    g.re = ue >> 4;
+    g.e = ue & 15;
+    return g;
+}
+
+// Wave max of the groups' batch counts (>= 1).
+__device__ __forceinline__ uint32_t round_nbw_al(const AGeo &g) {
+    const int32_t nb = (g.re + 4) >> 2;
+    return wave_max_u32(nb < 1 ? 1u : static_cast<uint32_t>(nb), 16);
+}
+
+// Abs row rho of batch j, row i, in a round of nbw batches.
+__device__ __forceinline__ int32_t al_row(const AGeo &g, uint32_t nbw, uint32_t j, uint32_t i) {
+    return g.re + static_cast<int32_t>(4u * j + i + 1u) - static_cast<int32_t>(4u * nbw);
+}
+
+// Last batch that holds head granules (d <= 1) for any group.
+__device__ __forceinline__ uint32_t round_jfix_al(const RGeo &q, uint32_t nbw) {
+    const AGeo g = al_geo(q);
+    const int32_t uh = g.ph + ((q.alow() > 12u && q.ng() >= 2u) ? 1 : 0);
+    const int32_t jh = ((uh >> 4) - g.re - 1 + static_cast<int32_t>(4u * nbw)) >> 2;
+    return wave_max_u32(static_cast<uint32_t>(jh), 16);
+}
+
+__device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
+                                               uint4 (&v)[U]) {
+    const AGeo g = al_geo(q);
+    const uint64_t ab = q.abase();
+    const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+        int32_t d = 16 * al_row(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
+        d = d < 0 ? 0 : (d > dmax ? dmax : d);
+        const uint64_t ad = ab + (static_cast<uint32_t>(d) << 4);
+        v[i] = (LVK_AL_RT_LAST && i == U - 1) ? load16_rt(ad) : load16(ad);
+    }
+}
+
+// Head fix-up (as fix_rbatch) plus the zero granules past u_e.
+__device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
+                                              uint4 (&v)[U]) {
+    const AGeo g = al_geo(q);
+    const uint32_t s0 = q.len >= 4 ? ~q.seed : 0u;
+    const int32_t alow = static_cast<int32_t>(q.alow());
+    const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+        const int32_t d = 16 * al_row(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
+        if (d < 0 || d > dmax) {
+            v[i] = make_uint4(0, 0, 0, 0);
+        } else if (d == 0 || (d == 1 && alow > 12)) {
+            const int32_t rel = d * 16 - alow;
+            v[i].x = fix_word(v[i].x, rel, s0);
+            v[i].y = fix_word(v[i].y, rel + 4, s0);
+            v[i].z = fix_word(v[i].z, rel + 8, s0);
+            v[i].w = fix_word(v[i].w, rel + 12, s0);
+        }
+    }
+}
+
+// Row merge by Horner with W1 = Shift_256: X = W1(W1(W1(A0)^A1)^A2)^A3.
+// Lanes past e end one row earlier: their last row is row 2 of the last
+// batch, and their row-3 accumulator must be taken BEFORE the last batch's
+// W4 step (a3p), so their Horner runs (a3p, A0, A1, A2).  Then the lane
+// rotation by e + 1 (one ds_bpermute) and the ordinary tree: lane 0 of the
+// group holds R over the buffer's whole granules.
+// (In the depth-2 form W2(W1(h0)^h1) ^ (W1(h2)^h3).)  `rot` (wave-uniform)
+// is false when every group of the wave ends at lane 15 (e.g. aligned table
+// blocks): no early lanes, no rotation.
+__device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[U], uint32_t a3p, const Lut &L, const RGeo &q,
+                                             uint32_t gl, uint32_t lane, bool rot) {
+    const AGeo g = al_geo(q);
+    const bool early = static_cast<int32_t>(gl) > g.e;
+    const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
+    const uint32_t x23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
+    uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+    if (rot) X = __shfl(X, static_cast<int32_t>((lane & ~15u) | ((gl + static_cast<uint32_t>(g.e) + 1u) & 15u)));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t other = lanes_down<16, false>(X, k);
+        X = comb_shift(X, k) ^ other;
+    }
+    return X;
+}
+
 __device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q, uint32_t X, const uint4 &tail,
                                                  uint32_t gl, const Lut &L) {
     X = fold_tail(X, tail, q, L);
@@ -1116,9 +1226,13 @@ __device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q,
 // loads and spills cost more than the conservative wait counts they remove.)
 // The image is always the G = 16 one: groups of G = 1 and 4 take their
 // row-shift and merge tables from the plain combine tables.
+#ifndef LVK_ALIGNED_ROWS
+#define LVK_ALIGNED_ROWS 1
+#endif
 template <int G, bool SEEDED, class Next>
 __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, const Lut &L, uint64_t rho,
                                               Next next) {
+    constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
     constexpr uint32_t K = 64 / G;
     constexpr int W4K = G == 16 ? -1 : (G == 4 ? 4 : 2);  // Shift_{64G}
     constexpr int W1K = G == 16 ? -1 : (G == 4 ? 2 : 0);  // Shift_{16G}
@@ -1130,15 +1244,22 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
     uint64_t rhon = next();
 
     RGeo q = load_rgeo<SEEDED>(P, rho * K + grp);
-    uint32_t nbw = round_nbw<G>(q);
-    uint32_t jfix = round_jfix<G>(q, nbw);
+    // (AL) some group of the round ends before lane 15.  The row geometry
+    // (al_geo) is recomputed from q where it is used: fewer live registers.
+    bool rot = AL && __any(al_geo(q).e != 15);
+    uint32_t nbw = AL ? round_nbw_al(al_geo(q)) : round_nbw<G>(q);
+    uint32_t jfix = AL ? round_jfix_al(q, nbw) : round_jfix<G>(q, nbw);
     RGeo qn = q;
     if (rhon < nr) qn = load_rgeo<SEEDED>(P, rhon * K + grp);
     uint32_t nbwn = 0;
     uint4 tail;
     uint4 slot0[U], slot1[U];
-    load_rbatch<G>(q, nbw, 0, gl, slot0);
+    if constexpr (AL)
+        load_rbatch_al(q, nbw, 0, gl, slot0);
+    else
+        load_rbatch<G>(q, nbw, 0, gl, slot0);
     uint32_t A[U];
+    uint32_t a3p = 0;  // (AL) the row-3 accumulator before the last batch
     uint32_t c = 0;  // rounds finished (output staging slot)
     uint32_t j = 0;
 
@@ -1146,15 +1267,30 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
         const bool lastj = j + 1 == nbw;
         const bool more = rhon < nr;
         if (!lastj) {
-            load_rbatch<G>(q, nbw, j + 1, gl, nxt);
+            if constexpr (AL)
+                load_rbatch_al(q, nbw, j + 1, gl, nxt);
+            else
+                load_rbatch<G>(q, nbw, j + 1, gl, nxt);
         } else {
             tail = load_rtail(q, gl);  // consumed after this batch's fold
             if (more) {
-                nbwn = round_nbw<G>(qn);
-                load_rbatch<G>(qn, nbwn, 0, gl, nxt);
+                if constexpr (AL) {
+                    nbwn = round_nbw_al(al_geo(qn));
+                    load_rbatch_al(qn, nbwn, 0, gl, nxt);
+                } else {
+                    nbwn = round_nbw<G>(qn);
+                    load_rbatch<G>(qn, nbwn, 0, gl, nxt);
+                }
             }
         }
-        if (j <= jfix) fix_rbatch<G>(q, nbw, j, gl, cur);
+        if constexpr (AL) {
+            if (j <= jfix || (lastj && rot)) fix_rbatch_al(q, nbw, j, gl, cur);
+        } else if (j <= jfix) {
+            fix_rbatch<G>(q, nbw, j, gl, cur);
+        }
+        if constexpr (AL) {
+            if (lastj) a3p = j == 0 ? 0u : A[U - 1];
+        }
         if (j == 0)
             fold_batch<true, W4K>(cur, A, L);
         else
@@ -1163,7 +1299,11 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
             ++j;
             return false;
         }
-        uint32_t X = merge_group<G, W1K, W2K>(A, L);
+        uint32_t X;
+        if constexpr (AL)
+            X = merge_al(A, a3p, L, q, gl, lane, rot);
+        else
+            X = merge_group<G, W1K, W2K>(A, L);
         const uint32_t crc = finish_round(P, q, X, tail, gl, L);
         const uint32_t slot = (c % G) * K + grp;
         if (gl == 0) {
@@ -1180,7 +1320,12 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
         ++c;
         q = qn;
         nbw = nbwn;
-        jfix = round_jfix<G>(q, nbw);
+        if constexpr (AL) {
+            rot = __any(al_geo(q).e != 15);
+            jfix = round_jfix_al(q, nbw);
+        } else {
+            jfix = round_jfix<G>(q, nbw);
+        }
         rhon = next();
         if (rhon < nr) qn = load_rgeo<SEEDED>(P, rhon * K + grp);
         j = 0;

@@ -335,6 +335,28 @@ def test_sorted_walk_edges(torch_dev, arena):
     assert bad.size == 0, [(offs[i], lens[i]) for i in bad[:10]]
 
 
+def test_aligned_row_geometry(torch_dev, arena):
+    """The G = 16 classes walk rows on the absolute 256-B grid (merge_al):
+    every start phase in the 256-B row (granule 0..15) x byte alignments, with
+    lengths that put the last whole granule on every lane e = 0..15, plus
+    single-batch, 32 KiB-edge and > 32 KiB buffers; seeded and masked."""
+    torch, dev = torch_dev
+    rng = random.Random(77)
+    lengths = [2049 + 16 * t + rng.randrange(16) for t in range(16)] + [4096, 4097, 32768, 32769,
+                                                                          40000 + rng.randrange(256)]
+    offs, lens = [], []
+    for ln in lengths:
+        for ph in range(16):
+            for mis in range(0, 16, 3):
+                offs.append(256 * rng.randrange(1, 800) + 16 * ph + mis)
+                lens.append(ln)
+    seeds = [rng.getrandbits(32) for _ in offs]
+    want = oracle_batch(arena, offs, lens, seeds, True)
+    got = gpu_batch(torch, dev, arena, offs, lens, seeds, True)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(offs[i], lens[i]) for i in bad[:10]]
+
+
 @pytest.mark.parametrize("workload", ["c2", "c4"])
 def test_full_size_offsets_api(torch_dev, workload):
     """Configs 2 and 4 at full size (1,048,576 byte-packed buffers, 5.6-5.8 GiB,
