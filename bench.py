@@ -496,6 +496,7 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    el_own = time.perf_counter() - t0  # this rank alone (per_gpu)
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -515,6 +516,13 @@ def main():
     if os.environ.get("LVGPU_BENCH_TRACE"):
         print("per-launch ms:", " ".join(f"{x:.4f}" for x in kern_seq), file=sys.stderr)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    # per-GPU figures: each rank's own timed-pass rate and kernel rate
+    own = {"rank": rank, "device": local, "GiB_per_s": round(nbytes * args.steps / 2**30 / el_own, 2),
+           "kernel_GB_per_s": round(nbytes / (kern_avg_ms * 1e-3) / 1e9, 1)}
+    per_rank = [own]
+    if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, own)
 
     total_bytes = nbytes * world
     value = total_bytes * args.steps / 2**30 / el
@@ -554,6 +562,7 @@ def main():
                          "timing": "HIP events around each of K launches on the launch stream, in a second "
                                    "pass of the K timed steps"},
             "cpu_baseline": cpu,
+            "per_gpu": per_rank,
         }
         print(json.dumps(result), flush=True)
     if dist:
