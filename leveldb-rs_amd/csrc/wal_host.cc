@@ -334,21 +334,38 @@ int lv_wal_encode_host(const uint8_t *payload, const uint64_t *rec_off, const ui
     }
     *out_len = pos;
     if (!out || out_cap < pos) return lvgpu_internal::set_error(LV_ERR_INVALID, "output buffer too small");
-    // Pass 2: bytes, then one GPU batch: crc = mask(extend(type_crc[t], frag)).
+    // Pass 2: the fragment CRCs and the bytes, concurrently.  A fragment's CRC
+    // covers payload bytes only (crc = mask(extend(type_crc[t], frag)),
+    // log_writer.rs:123-125), so the GPU batch runs over the caller's payload
+    // buffer -- its upload overlaps the host's layout copy instead of
+    // following it.
     for (const auto &p : pads) std::memset(out + p.first, 0, p.second);
     std::vector<uint64_t> off(frags.size());
     std::vector<uint32_t> len(frags.size()), seed(frags.size()), crc(frags.size());
     uint32_t type_crc[5];
     for (uint8_t t = 0; t < 5; ++t) type_crc[t] = lv_crc32c_value(&t, 1);  // log_writer.rs:136-142
+    uint64_t pay_end = 0;
+    for (size_t i = 0; i < frags.size(); ++i) {
+        const Frag &f = frags[i];
+        off[i] = f.src;
+        len[i] = f.len;
+        seed[i] = type_crc[f.type];
+        if (f.src + f.len > pay_end) pay_end = f.src + f.len;
+    }
+    int crc_rc = LV_OK;
+    std::thread gpu;
+    if (!frags.empty())
+        gpu = std::thread([&] {
+            static const uint8_t empty = 0;  // all records empty: nothing to read, a valid arena
+            crc_rc = lv_crc32c_batch_host(pay_end ? payload : &empty, pay_end, off.data(), len.data(), seed.data(),
+                                          crc.data(), frags.size(), LV_CRC_MASK, device);
+        });
     // The payload copy is the host's share of the work (the whole log's
     // bytes): split it over up to 8 threads by fragment ranges of equal bytes.
     auto copy_range = [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
             const Frag &f = frags[i];
             if (f.len) std::memcpy(out + f.out_pos + kHeader, payload + f.src, f.len);
-            off[i] = f.out_pos + kHeader;
-            len[i] = f.len;
-            seed[i] = type_crc[f.type];
         }
     };
     unsigned nt = std::thread::hardware_concurrency();
@@ -369,11 +386,8 @@ int lv_wal_encode_host(const uint8_t *payload, const uint64_t *rec_off, const ui
         if (lo < frags.size()) copy_range(lo, frags.size());
         for (auto &x : th) x.join();
     }
-    if (!frags.empty()) {
-        if (int rc = lv_crc32c_batch_host(out, pos, off.data(), len.data(), seed.data(), crc.data(), frags.size(),
-                                          LV_CRC_MASK, device))
-            return rc;
-    }
+    if (gpu.joinable()) gpu.join();
+    if (crc_rc) return crc_rc;
     for (size_t i = 0; i < frags.size(); ++i) {  // log_writer.rs:117-125
         uint8_t *h = out + frags[i].out_pos;
         h[0] = static_cast<uint8_t>(crc[i]);

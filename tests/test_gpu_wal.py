@@ -88,6 +88,10 @@ def test_encode_matches_writer(gpu, dest_length):
 def test_encode_empty_batch(gpu):
     import lvgpu.wal as LW
     assert LW.encode([]) == b""
+    # records with no payload bytes at all: every fragment CRC covers zero bytes
+    empties = [b""] * 5
+    for dest_length in (0, B - H - 2):
+        assert LW.encode(empties, dest_length=dest_length) == _oracle_encode(empties, dest_length)
 
 
 def test_encode_then_scan_then_read(gpu):
