@@ -55,6 +55,12 @@ def parse():
     p.add_argument("--wal", action="store_true",
                    help="WAL rows of SURVEY 8f: time lv_wal_encode_host and lv_wal_scan_host (+ reader) on a "
                         "~1 GiB log of Random(301).skewed(17) records; one JSON line")
+    p.add_argument("--table", action="store_true",
+                   help="SURVEY 8f row 3: seal + verify SSTable block trailers of a 1 GiB table in HBM "
+                        "(262,144 blocks of 4096-4351 B); one JSON line")
+    p.add_argument("--hash", action="store_true",
+                   help="SURVEY 8f row 4: batched hash() + cache shard of 16 M byte-packed keys (8-64 B) in HBM; "
+                        "one JSON line")
     p.add_argument("--c1", action="store_true",
                    help="CPU-only config 1: the benches/crc32c.rs sweep (oracle extend_sw/extend_hw and the "
                         "product's scalar drop-ins), one JSON line; no GPU")
@@ -359,6 +365,120 @@ def c1_sweep(args):
                       "results": rows}), flush=True)
 
 
+def _event_times(torch, fn, steps, warmup):
+    """Median and mean ms of `fn` by HIP events on the current stream."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in evs:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in evs)
+    return ts[len(ts) // 2], sum(ts) / len(ts)
+
+
+def table_bench(args):
+    """SURVEY 8f row 3 in HBM: lv_sst_seal_blocks_device writes the
+    type(1) || mask(crc32c(contents || type)) trailer of every block of a table
+    being built; lv_sst_verify_blocks_device checks them (table/format.rs
+    BlockHandle extents; trailer layout parity unpinned).  Blocks of
+    4096 + U[0, 256) bytes (a 4 KiB block_size threshold overshoots by up to
+    one entry), each followed by its 5-byte trailer; ~1 GiB.  Algorithmic
+    bytes: contents + type (seal also writes 4 B, verify reads 4 B)."""
+    import numpy as np
+    import torch
+    import lvgpu
+    import lvgpu.table as T
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    lvgpu.device_init()
+    n = args.blocks or 262144
+    rng = np.random.default_rng(0x55AB1E)
+    sizes = (4096 + rng.integers(0, 256, n)).astype(np.int64)
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(sizes[:-1] + 5)
+    total = int(offs[-1] + sizes[-1] + 5)
+    f = torch.empty(total, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(f, 0, PAYLOAD_SEED)
+    h = torch.from_numpy(np.stack([offs, sizes], axis=1).copy()).to(dev)
+    seal_p50, seal_avg = _event_times(torch, lambda: T.seal_blocks(f, h), args.steps, args.warmup)
+    ver_p50, ver_avg = _event_times(torch, lambda: T.verify_blocks(f, h), args.steps, args.warmup)
+    st, crc = T.verify_blocks(f, h, out_crc=True)
+    torch.cuda.synchronize()
+    if not bool((st == T.BLOCK_OK).all()):
+        raise SystemExit("table bench: a sealed block failed verification")
+    host = f[:int(offs[min(n, 2000) - 1] + sizes[min(n, 2000) - 1] + 1)].cpu().numpy().tobytes()
+    got = crc[:2000].cpu().numpy().view(np.uint32)
+    for k in range(min(n, 2000)):
+        o, sz = int(offs[k]), int(sizes[k])
+        if W.value(host[o:o + sz + 1]) != int(got[k]):
+            raise SystemExit("table bench parity check failed")
+    unit = int(sizes.sum()) + n  # contents + type byte per block
+    res = {"metric": "SSTable block trailer seal / verify, device-resident", "unit": "GiB/s",
+           "blocks": n, "bytes_per_call": unit, "table_bytes": total,
+           "seal": {"GiB_per_s": round(unit / 2**30 / (seal_avg * 1e-3), 1), "ms_avg": round(seal_avg, 4),
+                    "ms_p50": round(seal_p50, 4), "frac_of_8TBps": round(unit / (seal_avg * 1e-3) / 8e12, 4)},
+           "verify": {"GiB_per_s": round(unit / 2**30 / (ver_avg * 1e-3), 1), "ms_avg": round(ver_avg, 4),
+                      "ms_p50": round(ver_p50, 4), "frac_of_8TBps": round(unit / (ver_avg * 1e-3) / 8e12, 4)},
+           "timing": "HIP events around each call (CRC batch + trailer kernels)", "parity": "first 2000 blocks vs oracle",
+           "data": "synthetic splitmix64 contents in HBM"}
+    print(json.dumps(res), flush=True)
+    return res
+
+
+def hash_bench(args):
+    """SURVEY 8f row 4 in HBM: lv_hash_batch_device over 16,777,216 byte-packed
+    keys of 8-64 bytes (cache-key sized; util/hash.rs:20-51, cache shard
+    cache.rs:394-399).  One lane per key (the hash is a serial chain), so the
+    bound is HBM: key bytes + 12 B metadata + 4 B output per key."""
+    import numpy as np
+    import torch
+    import lvgpu
+    from lvgpu import hash as H
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    lvgpu.device_init()
+    n = args.blocks or 16777216
+    rng = np.random.default_rng(0x4A54)
+    lens = rng.integers(8, 65, n).astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(offs[-1] + lens[-1])
+    arena = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, PAYLOAD_SEED)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    p50, avg = _event_times(torch, lambda: H.hash_batch(arena, o, ln, out=out, shard=True), args.steps, args.warmup)
+    H.hash_batch(arena, o, ln, out=out)
+    torch.cuda.synchronize()
+    L = W.lib()
+    L.oracle_hash_batch.restype = None
+    L.oracle_hash_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t]
+    k = min(n, 100000)
+    host = arena[:int(offs[k - 1] + lens[k - 1])].cpu().numpy()
+    want = np.zeros(k, dtype=np.uint32)
+    L.oracle_hash_batch(host.ctypes.data, offs[:k].ctypes.data, lens[:k].ctypes.data, None, want.ctypes.data, k)
+    if not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
+        raise SystemExit("hash bench parity check failed")
+    moved = total + 16 * n  # key bytes + off/len + out
+    res = {"metric": "batched leveldb hash() + cache shard, device-resident", "unit": "Gkeys/s",
+           "keys": n, "key_bytes": total, "value": round(n / (avg * 1e-3) / 1e9, 3), "ms_avg": round(avg, 4),
+           "ms_p50": round(p50, 4), "hbm_GB_per_s": round(moved / (avg * 1e-3) / 1e9, 1),
+           "frac_of_8TBps": round(moved / (avg * 1e-3) / 8e12, 4),
+           "note": "hbm bytes = key bytes + 8 B offset + 4 B length + 4 B output per key",
+           "parity": "first 100000 keys vs oracle", "data": "synthetic splitmix64 keys in HBM"}
+    print(json.dumps(res), flush=True)
+    return res
+
+
 def wal_bench(args):
     """SURVEY 8f rows 1-2 end to end from host memory: group-commit encode
     (lv_wal_encode_host: layout + one GPU CRC batch) and whole-log verify
@@ -447,6 +567,10 @@ def main():
         return c1_sweep(args)
     if args.e2e:
         return e2e(args)
+    if args.table:
+        return table_bench(args)
+    if args.hash:
+        return hash_bench(args)
     import torch
     import lvgpu
 

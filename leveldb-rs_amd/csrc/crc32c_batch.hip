@@ -183,61 +183,63 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 #ifndef LVK_EXP_NOSTAGE
 #define LVK_EXP_NOSTAGE 0
 #endif
-template <bool FIRST, int W4K = -1>
-__device__ __forceinline__ void fold_batch(const uint4 (&v)[U], uint32_t (&A)[U], const Lut &L) {
+// NU rows per batch; W4OFF = LDS offset of the Latin row-shift table (the
+// image's W4 = Shift_{64G}, or region B's W2 = Shift_{32G} for NU = 2).
+template <bool FIRST, int W4K = -1, uint32_t NU = U, uint32_t W4OFF = kRegionA + kHalf>
+__device__ __forceinline__ void fold_batch(const uint4 (&v)[NU], uint32_t (&A)[NU], const Lut &L) {
 #if LVK_EXP_NOFOLD  // experiment only: no lookups at all (load-structure bound)
 #pragma unroll
-    for (uint32_t i = 0; i < U; ++i) A[i] = (FIRST ? 0u : A[i]) ^ xor3(v[i].x, v[i].y, v[i].z) ^ v[i].w;
+    for (uint32_t i = 0; i < NU; ++i) A[i] = (FIRST ? 0u : A[i]) ^ xor3(v[i].x, v[i].y, v[i].z) ^ v[i].w;
     return;
 #endif
-    uint32_t s[U], w[U], w3[U];
+    uint32_t s[NU], w[NU], w3[NU];
 #pragma unroll
-    for (uint32_t i = 0; i < U; ++i) s[i] = v[i].x;
+    for (uint32_t i = 0; i < NU; ++i) s[i] = v[i].x;
     if constexpr (!FIRST && W4K >= 0) {
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
+        for (uint32_t i = 0; i < NU; ++i) {
             w[i] = comb_shift(A[i], W4K);
             w3[i] = 0u;
         }
     } else if constexpr (!FIRST && LVK_EXP_NOSHIFT) {  // experiment only: wrong CRCs
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
+        for (uint32_t i = 0; i < NU; ++i) {
             w[i] = A[i];
             w3[i] = 0u;
         }
     } else if constexpr (!FIRST) {
-        uint32_t aa[U][4];
+        uint32_t aa[NU][4];
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
+        for (uint32_t i = 0; i < NU; ++i) {
             aa[i][0] = lut_addr<0>(A[i], L);
             aa[i][1] = lut_addr<1>(A[i], L);
             aa[i][2] = lut_addr<2>(A[i], L);
             aa[i][3] = lut_addr<3>(A[i], L);
         }
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
-            w[i] = xor3(lds_word(aa[i][0] + kRegionA + kHalf), lds_word(aa[i][1] + kRegionA + kHalf),
-                        lds_word(aa[i][2] + kRegionA + kHalf));
-            w3[i] = lds_word(aa[i][3] + kRegionA + kHalf);
+        for (uint32_t i = 0; i < NU; ++i) {
+            w[i] = xor3(lds_word(aa[i][0] + W4OFF), lds_word(aa[i][1] + W4OFF),
+                        lds_word(aa[i][2] + W4OFF));
+            w3[i] = lds_word(aa[i][3] + W4OFF);
         }
     }
 #pragma unroll
     for (uint32_t step = 0; step < 4; ++step) {
-        uint32_t ad[U][4];
+        uint32_t ad[NU][4];
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
+        for (uint32_t i = 0; i < NU; ++i) {
             ad[i][0] = lut_addr<0>(s[i], L);
             ad[i][1] = lut_addr<1>(s[i], L);
             ad[i][2] = lut_addr<2>(s[i], L);
             ad[i][3] = lut_addr<3>(s[i], L);
         }
-        uint32_t t[U][4];
+        uint32_t t[NU][4];
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i)
+        for (uint32_t i = 0; i < NU; ++i)
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) t[i][k] = lds_word(ad[i][k] + kRegionA);
 #pragma unroll
-        for (uint32_t i = 0; i < U; ++i) {
+        for (uint32_t i = 0; i < NU; ++i) {
             const uint32_t x = xor3(t[i][0], t[i][1], t[i][2]);
             if (step < 3) {
                 const uint32_t nw = step == 0 ? v[i].y : step == 1 ? v[i].z : v[i].w;
@@ -749,9 +751,18 @@ __device__ __forceinline__ uint32_t len_class(uint32_t len) {
     return len <= 256u ? 0u : len <= 2048u ? 1u : len <= 32768u ? 2u : 3u;
 }
 
+// Rows per batch of the G = 16 classes' aligned-row walk (sorted_stream).
+#ifndef LVK_AL_ROWS
+#define LVK_AL_ROWS 4
+#endif
+#ifndef LVK_ALIGNED_ROWS
+#define LVK_ALIGNED_ROWS 1
+#endif
+constexpr uint32_t kAlRows = LVK_ALIGNED_ROWS ? LVK_AL_ROWS : U;
+
 __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     const uint32_t c = len_class(len);
-    const uint32_t gu16 = 16u * U * (c == 0 ? 1u : c == 1 ? 4u : 16u);
+    const uint32_t gu16 = 16u * (c >= 2 ? kAlRows : U) * (c == 0 ? 1u : c == 1 ? 4u : 16u);
     uint32_t nb = (len + gu16 - 1) / gu16;  // batches, ignoring start alignment
     nb = nb < kBuckets - 1 ? nb : kBuckets - 1;
     return c * kBuckets + (kBuckets - 1 - nb);
@@ -1125,49 +1136,54 @@ __device__ __forceinline__ AGeo al_geo(const RGeo &q) {
     return g;
 }
 
-// Wave max of the groups' batch counts (>= 1).
+// Wave max of the groups' batch counts (>= 1) at NU rows per batch.
+template <uint32_t NU>
 __device__ __forceinline__ uint32_t round_nbw_al(const AGeo &g) {
-    const int32_t nb = (g.re + 4) >> 2;
+    const int32_t nb = (g.re + static_cast<int32_t>(NU)) / static_cast<int32_t>(NU);
     return wave_max_u32(nb < 1 ? 1u : static_cast<uint32_t>(nb), 16);
 }
 
-// Abs row rho of batch j, row i, in a round of nbw batches.
+// Abs row rho of batch j, row i, in a round of nbw batches of NU rows.
+template <uint32_t NU>
 __device__ __forceinline__ int32_t al_row(const AGeo &g, uint32_t nbw, uint32_t j, uint32_t i) {
-    return g.re + static_cast<int32_t>(4u * j + i + 1u) - static_cast<int32_t>(4u * nbw);
+    return g.re + static_cast<int32_t>(NU * j + i + 1u) - static_cast<int32_t>(NU * nbw);
 }
 
 // Last batch that holds head granules (d <= 1) for any group.
+template <uint32_t NU>
 __device__ __forceinline__ uint32_t round_jfix_al(const RGeo &q, uint32_t nbw) {
     const AGeo g = al_geo(q);
     const int32_t uh = g.ph + ((q.alow() > 12u && q.ng() >= 2u) ? 1 : 0);
-    const int32_t jh = ((uh >> 4) - g.re - 1 + static_cast<int32_t>(4u * nbw)) >> 2;
+    const int32_t jh = ((uh >> 4) - g.re - 1 + static_cast<int32_t>(NU * nbw)) / static_cast<int32_t>(NU);
     return wave_max_u32(static_cast<uint32_t>(jh), 16);
 }
 
+template <uint32_t NU>
 __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
-                                               uint4 (&v)[U]) {
+                                               uint4 (&v)[NU]) {
     const AGeo g = al_geo(q);
     const uint64_t ab = q.abase();
     const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
 #pragma unroll
-    for (uint32_t i = 0; i < U; ++i) {
-        int32_t d = 16 * al_row(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
+    for (uint32_t i = 0; i < NU; ++i) {
+        int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
         d = d < 0 ? 0 : (d > dmax ? dmax : d);
         const uint64_t ad = ab + (static_cast<uint32_t>(d) << 4);
-        v[i] = (LVK_AL_RT_LAST && i == U - 1) ? load16_rt(ad) : load16(ad);
+        v[i] = (LVK_AL_RT_LAST && i == NU - 1) ? load16_rt(ad) : load16(ad);
     }
 }
 
 // Head fix-up (as fix_rbatch) plus the zero granules past u_e.
+template <uint32_t NU>
 __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
-                                              uint4 (&v)[U]) {
+                                              uint4 (&v)[NU]) {
     const AGeo g = al_geo(q);
     const uint32_t s0 = q.len >= 4 ? ~q.seed : 0u;
     const int32_t alow = static_cast<int32_t>(q.alow());
     const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
 #pragma unroll
-    for (uint32_t i = 0; i < U; ++i) {
-        const int32_t d = 16 * al_row(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
+    for (uint32_t i = 0; i < NU; ++i) {
+        const int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
         if (d < 0 || d > dmax) {
             v[i] = make_uint4(0, 0, 0, 0);
         } else if (d == 0 || (d == 1 && alow > 12)) {
@@ -1189,13 +1205,20 @@ __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint3
 // (In the depth-2 form W2(W1(h0)^h1) ^ (W1(h2)^h3).)  `rot` (wave-uniform)
 // is false when every group of the wave ends at lane 15 (e.g. aligned table
 // blocks): no early lanes, no rotation.
-__device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[U], uint32_t a3p, const Lut &L, const RGeo &q,
+template <uint32_t NU>
+__device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a3p, const Lut &L, const RGeo &q,
                                              uint32_t gl, uint32_t lane, bool rot) {
     const AGeo g = al_geo(q);
     const bool early = static_cast<int32_t>(gl) > g.e;
-    const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
-    const uint32_t x23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
-    uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+    uint32_t X;
+    if constexpr (NU == 4) {
+        const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
+        const uint32_t x23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
+        X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+    } else {  // NU = 2: W1(h0) ^ h1
+        static_assert(NU == 2, "aligned rows: 2 or 4 rows per batch");
+        X = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
+    }
     if (rot) X = __shfl(X, static_cast<int32_t>((lane & ~15u) | ((gl + static_cast<uint32_t>(g.e) + 1u) & 15u)));
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1226,13 +1249,13 @@ __device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q,
 // loads and spills cost more than the conservative wait counts they remove.)
 // The image is always the G = 16 one: groups of G = 1 and 4 take their
 // row-shift and merge tables from the plain combine tables.
-#ifndef LVK_ALIGNED_ROWS
-#define LVK_ALIGNED_ROWS 1
-#endif
 template <int G, bool SEEDED, class Next>
 __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, const Lut &L, uint64_t rho,
                                               Next next) {
     constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
+    constexpr uint32_t NU = AL ? kAlRows : U;          // rows per batch
+    // Latin row shift Shift_{16 G NU}: the image's W4 (NU = 4) or W2 (NU = 2)
+    constexpr uint32_t W4OFF = NU == 4 ? kRegionA + kHalf : kRegionB + kHalf;
     constexpr uint32_t K = 64 / G;
     constexpr int W4K = G == 16 ? -1 : (G == 4 ? 4 : 2);  // Shift_{64G}
     constexpr int W1K = G == 16 ? -1 : (G == 4 ? 2 : 0);  // Shift_{16G}
@@ -1247,36 +1270,36 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
     // (AL) some group of the round ends before lane 15.  The row geometry
     // (al_geo) is recomputed from q where it is used: fewer live registers.
     bool rot = AL && __any(al_geo(q).e != 15);
-    uint32_t nbw = AL ? round_nbw_al(al_geo(q)) : round_nbw<G>(q);
-    uint32_t jfix = AL ? round_jfix_al(q, nbw) : round_jfix<G>(q, nbw);
+    uint32_t nbw = AL ? round_nbw_al<NU>(al_geo(q)) : round_nbw<G>(q);
+    uint32_t jfix = AL ? round_jfix_al<NU>(q, nbw) : round_jfix<G>(q, nbw);
     RGeo qn = q;
     if (rhon < nr) qn = load_rgeo<SEEDED>(P, rhon * K + grp);
     uint32_t nbwn = 0;
     uint4 tail;
-    uint4 slot0[U], slot1[U];
+    uint4 slot0[NU], slot1[NU];
     if constexpr (AL)
-        load_rbatch_al(q, nbw, 0, gl, slot0);
+        load_rbatch_al<NU>(q, nbw, 0, gl, slot0);
     else
         load_rbatch<G>(q, nbw, 0, gl, slot0);
-    uint32_t A[U];
-    uint32_t a3p = 0;  // (AL) the row-3 accumulator before the last batch
+    uint32_t A[NU];
+    uint32_t a3p = 0;  // (AL) the last row's accumulator before the last batch
     uint32_t c = 0;  // rounds finished (output staging slot)
     uint32_t j = 0;
 
-    auto step = [&](uint4(&cur)[U], uint4(&nxt)[U]) -> bool {
+    auto step = [&](uint4(&cur)[NU], uint4(&nxt)[NU]) -> bool {
         const bool lastj = j + 1 == nbw;
         const bool more = rhon < nr;
         if (!lastj) {
             if constexpr (AL)
-                load_rbatch_al(q, nbw, j + 1, gl, nxt);
+                load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt);
             else
                 load_rbatch<G>(q, nbw, j + 1, gl, nxt);
         } else {
             tail = load_rtail(q, gl);  // consumed after this batch's fold
             if (more) {
                 if constexpr (AL) {
-                    nbwn = round_nbw_al(al_geo(qn));
-                    load_rbatch_al(qn, nbwn, 0, gl, nxt);
+                    nbwn = round_nbw_al<NU>(al_geo(qn));
+                    load_rbatch_al<NU>(qn, nbwn, 0, gl, nxt);
                 } else {
                     nbwn = round_nbw<G>(qn);
                     load_rbatch<G>(qn, nbwn, 0, gl, nxt);
@@ -1284,24 +1307,24 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
             }
         }
         if constexpr (AL) {
-            if (j <= jfix || (lastj && rot)) fix_rbatch_al(q, nbw, j, gl, cur);
+            if (j <= jfix || (lastj && rot)) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
         } else if (j <= jfix) {
             fix_rbatch<G>(q, nbw, j, gl, cur);
         }
         if constexpr (AL) {
-            if (lastj) a3p = j == 0 ? 0u : A[U - 1];
+            if (lastj) a3p = j == 0 ? 0u : A[NU - 1];
         }
         if (j == 0)
-            fold_batch<true, W4K>(cur, A, L);
+            fold_batch<true, W4K, NU, W4OFF>(cur, A, L);
         else
-            fold_batch<false, W4K>(cur, A, L);
+            fold_batch<false, W4K, NU, W4OFF>(cur, A, L);
         if (!lastj) {
             ++j;
             return false;
         }
         uint32_t X;
         if constexpr (AL)
-            X = merge_al(A, a3p, L, q, gl, lane, rot);
+            X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
         else
             X = merge_group<G, W1K, W2K>(A, L);
         const uint32_t crc = finish_round(P, q, X, tail, gl, L);
@@ -1322,7 +1345,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
         nbw = nbwn;
         if constexpr (AL) {
             rot = __any(al_geo(q).e != 15);
-            jfix = round_jfix_al(q, nbw);
+            jfix = round_jfix_al<NU>(q, nbw);
         } else {
             jfix = round_jfix<G>(q, nbw);
         }
