@@ -18,6 +18,7 @@
 namespace lvh {
 
 constexpr uint32_t kM = 0xc6a4a793u;  // hash.rs:23
+constexpr uint32_t kFastDw = 17;      // dwords of the register fast path (keys <= 64 B + misalignment)
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
@@ -42,13 +43,72 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     const uint64_t o = off[i];
     const uint32_t L = len[i];
     uint32_t h = (seed ? seed[i] : 0u) ^ (kM * L);  // hash.rs:25
-    if (L) {
-        const uint32_t bs = static_cast<uint32_t>(o & 3u);
+    const uint32_t bs = static_cast<uint32_t>(o & 3u);
+    const uint32_t nw = L >> 2;               // whole words, hash.rs:29
+    const uint32_t ndw = (bs + L + 3) >> 2;   // dwords covering the buffer
+    if (L && ndw <= kFastDw) {
+        // Keys of up to ~64 B (cache keys): every dword of the key is
+        // requested at once (whole quads where they fit, single dwords at the
+        // end, zeros past the key), so a key costs one memory latency; the
+        // chain then runs from registers, predicated per lane.
         const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
-        const uint32_t nw = L >> 2;               // whole words, hash.rs:29
-        const uint32_t ndw = (bs + L + 3) >> 2;   // dwords covering the buffer
+        uint32_t w[kFastDw + 1];
+        w[0] = d[0];
+#pragma unroll
+        for (uint32_t m = 0; m < 4; ++m) {
+            const uint32_t b = 4 * m + 1;
+            if (b + 3 < ndw) {
+                const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + b);
+                w[b] = v.x;
+                w[b + 1] = v.y;
+                w[b + 2] = v.z;
+                w[b + 3] = v.w;
+            } else {
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) w[b + t] = b + t < ndw ? d[b + t] : 0u;
+            }
+        }
+        w[kFastDw] = 0u;
+        uint32_t tw = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kFastDw; ++j) {
+            const uint32_t wj = funnel(w[j + 1], w[j], bs);
+            if (j < nw)
+                h = mix(h, wj);
+            else if (j == nw)
+                tw = wj;
+        }
+        const uint32_t diff = L - 4 * nw;          // hash.rs:38-48
+        if (diff) {
+            if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
+            if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;
+            h += tw & 0xffu;
+            h *= kM;
+            h ^= h >> 24;
+        }
+    } else if (L) {
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
         uint32_t cur = d[0];
         uint32_t k = 0;
+        // The first 4 quads (keys up to ~64 B: cache keys) are requested
+        // together, so a key costs one memory latency rather than one per
+        // quad; the loop below continues for longer keys.
+        constexpr uint32_t kPre = 4;
+        u32x4a4 pre[kPre];
+#pragma unroll
+        for (uint32_t m = 0; m < kPre; ++m)
+            if (4 * m + 4 <= nw && 4 * m + 4 < ndw) pre[m] = *reinterpret_cast<const u32x4a4 *>(d + 4 * m + 1);
+#pragma unroll
+        for (uint32_t m = 0; m < kPre; ++m) {
+            if (!(k + 4 <= nw && k + 4 < ndw)) break;
+            const u32x4a4 v = pre[m];
+            h = mix(h, funnel(v.x, cur, bs));
+            h = mix(h, funnel(v.y, v.x, bs));
+            h = mix(h, funnel(v.z, v.y, bs));
+            h = mix(h, funnel(v.w, v.z, bs));
+            cur = v.w;
+            k += 4;
+        }
         // 4 words per step from d[k+1 .. k+4], all inside the buffer's dwords
         for (; k + 4 <= nw && k + 4 < ndw; k += 4) {
             const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + k + 1);
