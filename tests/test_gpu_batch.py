@@ -392,3 +392,25 @@ def test_full_size_c5_shard(torch_dev):
     host = arena.cpu().numpy()
     want = oracle_batch(host, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096, np.uint32), None, False)
     assert np.array_equal(got, want)
+
+
+def test_many_buffers_chunked_sort(torch_dev):
+    """n above one sort pass's 1024 x 4096 buffers (4,194,304): 5,000,000
+    byte-packed buffers of 0-300 B (every small class, chunked length sort),
+    seeded and masked, every CRC vs the oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(5150)
+    n = 5_000_000
+    lens = rng.integers(0, 301, n).astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(offs[-1] + lens[-1]) + 16
+    t = torch.empty(total, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(t, 0, 0xB16)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    got = lvgpu.batch(t, o, ln, sd, masked=True).cpu().numpy().view(np.uint32)
+    want = oracle_batch(t.cpu().numpy(), offs, lens, seeds, True)
+    assert np.array_equal(got, want)
