@@ -5,27 +5,30 @@
 // log_reader.rs:335-336) and the table-block checksum.  Output
 // is bit-identical to crc32c.rs:42-63 (extend + optional mask).
 //
-// Kernel design (DESIGN.md "Kernel"):
+// Kernel design:
 //  * A group of G lanes (G in {1,4,16,64}) owns one buffer at a time; a
 //    wave holds 64/G groups.  Lane i of a group loads the i-th 16-B granule of
 //    every "row" of G granules with one global_load_dwordx4, so a row is one
 //    contiguous, coalesced run of 16*G bytes.  Rows are aligned to the END of
-//    the buffer; missing granules before the buffer start read as zeros
-//    (leading zeros leave a zero CRC register unchanged).
-//  * Per lane: p = R(0, granule) by four slice-by-4 steps; across rows
-//    A = Shift_{16G}(A) ^ p (Horner).  Groups then combine lanes pairwise,
-//    A_i = Shift_{16*2^k}(A_i) ^ A_{i+2^k}, k < log2 G.  The bytes after the
-//    last aligned granule (<16) are folded in by one lane, bytewise.
+//    the buffer, except in the offsets API's G = 16 walk, where they sit on
+//    the absolute 256-B grid (merge_al); granules outside the buffer read as
+//    zeros (leading zeros leave a zero CRC register unchanged).
+//  * Per lane: p = R(0, granule) by four slice-by-4 steps; across batches of
+//    U rows A_i = Shift_{16GU}(A_i) ^ p_i (Horner), then the rows merge and
+//    the lanes combine pairwise, X_l = Shift_{16*2^k}(X_l) ^ X_{l+2^k},
+//    k < log2 G.  The < 16 bytes after the last whole granule fold in as one
+//    shifted granule (fold_tail).
 //  * The seed enters by xoring (seed ^ ~0) into the first 4 buffer bytes:
 //    R(s, w||D) = R(0, (s^w)||D).  Buffers shorter than 4 bytes go bytewise.
 //  * Lookup tables live in LDS.  The slice tables T0..T3 and the row-shift
-//    tables W0..W3 use a "Latin-square" replicated layout: entry e of table k,
-//    copy c sits in dword (4c+k) (+32 for W) of a 256-B row e.  In lookup
-//    instruction i, lane g (of a 32-lane LDS group; c = g&7, q = g>>3) reads
-//    table (q+i)&3, so the 32 lanes of every ds_read_b32 hit 32 distinct
-//    banks: conflict-free random lookups with 64 KiB of tables.  The address
-//    (row e from a state byte, dword from the lane) is ONE v_perm_b32.
-//  * Persistent grid: one 1024-thread workgroup per CU (88 KiB LDS image).
+//    tables use a "Latin-square" replicated layout: entry e of table k, copy
+//    c sits in dword (4c+k) (+32 for the second set) of a 256-B row e.  In
+//    lookup instruction i, lane g (of a 32-lane LDS group; c = g&7, q = g>>3)
+//    reads table (q+i)&3, so the 32 lanes of every ds_read_b32 hit 32
+//    distinct banks: conflict-free random lookups.  The address (row e from a
+//    state byte, dword from the lane) is ONE v_perm_b32.
+//  * Persistent grid: one 1024-thread workgroup per CU; the 152 KiB table
+//    image plus 8 KiB of result staging fill the CU's 160 KiB of LDS.
 //
 // No MFMA: the work is one table lookup per byte, bound by HBM read
 // bandwidth (roofline in DESIGN.md).
@@ -943,14 +946,6 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
         }
     }
 }
-
-// Length classes of the offsets API in ONE persistent launch: every
-// workgroup walks every class (sorted runs of G = 1, 4, 16, 16), smallest
-// buffers first, each class spread over all waves of the grid, so no class
-// leaves CUs idle while another still has work.  (A static split of the grid
-// by estimated class work measured 3-8 % slower: the estimate is never
-// exact, and a class that finishes early idles its CUs.)
-
 
 // ---------------------------------------------------------------------------
 // Wave-uniform walk of length-sorted entries (offsets API).  The K = 64/G
