@@ -123,6 +123,8 @@ int main() {
     char nm[64]; snprintf(nm, 64, "groups nt G=16 U=4 4KiB +%dB", sh);
     run(nm, [&] { hipLaunchKernelGGL((probe_groups<16,4,true>), dim3(cus), dim3(1024), 0, 0, d + sh / 16, nb - 1, 256u, o); });
   }
+  run("groups nt G=8 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<8,4,true>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
+  run("groups nt G=4 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_groups<4,4,true>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("pairs nt G=16 U=2 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<16,2>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("pairs nt G=16 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<16,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
   run("pairs nt G=8 U=4 4KiB wg=cus", [&] { hipLaunchKernelGGL((probe_pairs<8,4>), dim3(cus), dim3(1024), 0, 0, d, nb, 256u, o); });
