@@ -33,39 +33,91 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t bs
     return __builtin_amdgcn_alignbyte(hi, lo, bs);
 }
 
+// One wave's staged key bytes: the 16-B granules spanning its 64 keys.
+constexpr uint32_t kSpanBytes = 4096;
+constexpr uint32_t kSpanPad = 20;  // dwords past the span a masked fast-path read may address
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint64_t o = __shfl_xor(v, m);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint64_t o = __shfl_xor(v, m);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
 __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ base,
                                                    const uint64_t *__restrict__ off,
                                                    const uint32_t *__restrict__ len,
                                                    const uint32_t *__restrict__ seed, uint32_t *__restrict__ out,
                                                    uint32_t n, uint32_t flags) {
+    __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpanBytes / 4 + kSpanPad];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t o = off[i];
-    const uint32_t L = len[i];
-    uint32_t h = (seed ? seed[i] : 0u) ^ (kM * L);  // hash.rs:25
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const bool valid = i < n;
+    const uint64_t o = valid ? off[i] : 0u;
+    const uint32_t L = valid ? len[i] : 0u;
+    uint32_t h = (valid && seed ? seed[i] : 0u) ^ (kM * L);  // hash.rs:25
     const uint32_t bs = static_cast<uint32_t>(o & 3u);
     const uint32_t nw = L >> 2;               // whole words, hash.rs:29
     const uint32_t ndw = (bs + L + 3) >> 2;   // dwords covering the buffer
-    if (L && ndw <= kFastDw) {
-        // Keys of up to ~64 B (cache keys): every dword of the key is
-        // requested at once (whole quads where they fit, single dwords at the
-        // end, zeros past the key), so a key costs one memory latency; the
+    // Keys of a batch are usually packed (cache keys, log keys): the wave
+    // stages the granules spanning its 64 keys through LDS with coalesced
+    // 16-B loads, instead of 64 lanes gathering byte-aligned keys.  Waves
+    // whose keys span more than kSpanBytes read keys straight from memory.
+    const uint64_t lo = wave_min_u64(L ? o : ~0ull);
+    const uint64_t hi = wave_max_u64(L ? o + L : 0ull);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool staged = lo != ~0ull && hi - lo16 <= kSpanBytes;  // wave-uniform
+    if (staged) {
+        const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(base + lo16);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(span[wv]);
+#pragma unroll
+        for (uint32_t k = 0; k < kSpanBytes / 16 / 64; ++k) {
+            const uint32_t c = lane + 64u * k;
+            if (c < nch) dst[c] = __builtin_nontemporal_load(src + c);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (valid && L && ndw <= kFastDw) {
+        // Keys of up to ~64 B (cache keys): every dword of the key is read at
+        // once (from the wave's staged span, or whole quads from memory where
+        // they fit and single dwords at its end), zeros past the key; the
         // chain then runs from registers, predicated per lane.
-        const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
         uint32_t w[kFastDw + 1];
-        w[0] = d[0];
+        if (staged) {
+            const uint32_t *sd = span[wv] + ((o - bs - lo16) >> 2);
 #pragma unroll
-        for (uint32_t m = 0; m < 4; ++m) {
-            const uint32_t b = 4 * m + 1;
-            if (b + 3 < ndw) {
-                const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + b);
-                w[b] = v.x;
-                w[b + 1] = v.y;
-                w[b + 2] = v.z;
-                w[b + 3] = v.w;
-            } else {
+            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = j < ndw ? sd[j] : 0u;
+        } else {
+            const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
+            w[0] = d[0];
 #pragma unroll
-                for (uint32_t t = 0; t < 4; ++t) w[b + t] = b + t < ndw ? d[b + t] : 0u;
+            for (uint32_t m = 0; m < 4; ++m) {
+                const uint32_t b = 4 * m + 1;
+                if (b + 3 < ndw) {
+                    const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + b);
+                    w[b] = v.x;
+                    w[b + 1] = v.y;
+                    w[b + 2] = v.z;
+                    w[b + 3] = v.w;
+                } else {
+#pragma unroll
+                    for (uint32_t t = 0; t < 4; ++t) w[b + t] = b + t < ndw ? d[b + t] : 0u;
+                }
             }
         }
         w[kFastDw] = 0u;
@@ -86,7 +138,7 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
             h *= kM;
             h ^= h >> 24;
         }
-    } else if (L) {
+    } else if (valid && L) {
         const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
         uint32_t cur = d[0];
         uint32_t k = 0;
@@ -134,7 +186,7 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
             h ^= h >> 24;
         }
     }
-    out[i] = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
+    if (valid) out[i] = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
 }
 
 }  // namespace lvh

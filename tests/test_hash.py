@@ -116,3 +116,30 @@ def test_gpu_bad_args(gpu):
     a = torch.zeros(16, dtype=torch.uint8, device=gpu)
     with pytest.raises(LvError):
         H.hash_batch(a, torch.zeros(3, dtype=torch.int64, device=gpu), torch.zeros(2, dtype=torch.int32, device=gpu))
+
+
+@pytest.mark.gpu
+def test_gpu_packed_keys_staged_and_not(gpu):
+    """Byte-packed keys (the staged-span path: a wave's 64 keys read through
+    LDS) of 0..100 B, so some waves hold keys past the 64-B register path and
+    some spans exceed the 4 KiB stage; plus a partial last wave and seeds."""
+    import torch
+    from lvgpu import hash as H
+    L = _oracle()
+    rng = np.random.default_rng(2718)
+    n = 20011
+    lens = rng.integers(0, 101, n).astype(np.uint32)
+    lens[5000:5064] = rng.integers(60, 101, 64)  # one wave past 4 KiB of span
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    offs += 3  # arena-relative misalignment
+    size = int(offs[-1] + lens[-1])
+    arena = rng.integers(0, 256, size=size, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = np.zeros(n, dtype=np.uint32)
+    L.oracle_hash_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, seeds.ctypes.data,
+                        want.ctypes.data, n)
+    a = torch.from_numpy(arena).to(gpu)
+    out = H.hash_batch(a, _dev(gpu, offs, np.int64), _dev(gpu, lens.view(np.int32), np.int32),
+                       _dev(gpu, seeds.view(np.int32), np.int32))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
