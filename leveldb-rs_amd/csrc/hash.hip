@@ -3,10 +3,12 @@
 // The hash is a serial, non-linear chain over 4-byte words
 // (h = ((h + w) * m) ^ (h >> 16)), so unlike CRC32C it cannot be split
 // inside a buffer: one lane owns one buffer.  Its keys are cache keys (tens of
-// bytes), so a launch is bound by metadata + key bytes through HBM; per lane
-// the words are read as dword-aligned 16-B loads funnel-shifted by the
-// buffer's byte misalignment (v_alignbyte_b32), never touching a dword past
-// the buffer's last byte.
+// bytes), so a launch is bound by metadata + key bytes through HBM.  A wave
+// whose 64 keys lie within 4 KiB stages those bytes through LDS with
+// coalesced 16-B loads; otherwise each lane reads its key's dwords from
+// memory.  Either way the words are dword-aligned reads funnel-shifted by the
+// key's byte misalignment (v_alignbyte_b32), never touching a dword past the
+// key's last byte, and keys of <= 64 B run the chain from registers.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
