@@ -34,6 +34,7 @@
 // bandwidth (roofline in DESIGN.md).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -1930,6 +1931,59 @@ int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d) {
 
 extern "C" {
 
+// Host batch with long buffers: one 16-lane group owns a buffer on the GPU,
+// so a buffer longer than kSplitBytes is cut into kChunkBytes pieces that run
+// as independent units (piece 0 with the buffer's seed, the others from a
+// zero register: extend(~0, D) = ~R(0, D)), and the host joins them by
+// linearity, R(s, A||B) = Shift_|B|(R(s, A)) ^ R(0, B), with GF(2) shift
+// matrices (crc32c_gf2.h).  The join is 32-bit arithmetic per piece; every
+// byte is still checksummed on the GPU.
+constexpr uint64_t kSplitBytes = 1ull << 20;
+constexpr uint64_t kChunkBytes = 256ull << 10;
+
+static int batch_host_split(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off,
+                            const uint32_t *h_len, const uint32_t *h_seed, uint32_t *h_out, size_t n,
+                            uint32_t flags, int device) {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len, seed, out;
+    std::vector<size_t> first(n + 1);  // pieces of buffer i: [first[i], first[i+1])
+    for (size_t i = 0; i < n; ++i) {
+        first[i] = off.size();
+        const uint32_t s = h_seed ? h_seed[i] : 0u;
+        if (h_len[i] <= kSplitBytes) {
+            off.push_back(h_off[i]);
+            len.push_back(h_len[i]);
+            seed.push_back(s);
+            continue;
+        }
+        for (uint64_t p = 0; p < h_len[i]; p += kChunkBytes) {
+            off.push_back(h_off[i] + p);
+            len.push_back(static_cast<uint32_t>(std::min<uint64_t>(kChunkBytes, h_len[i] - p)));
+            seed.push_back(p == 0 ? s : 0xffffffffu);
+        }
+    }
+    first[n] = off.size();
+    out.resize(off.size());
+    if (int rc = lv_crc32c_batch_host(h_arena, arena_bytes, off.data(), len.data(), seed.data(), out.data(),
+                                      off.size(), flags & ~LV_CRC_MASK, device))
+        return rc;
+    const lvgpu::Gf2Mat shift_chunk = lvgpu::shift_matrix(kChunkBytes);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t crc = out[first[i]];
+        if (first[i + 1] - first[i] > 1) {
+            uint32_t r = ~crc;  // R(~seed, piece 0)
+            for (size_t k = first[i] + 1; k < first[i + 1]; ++k) {
+                const uint32_t shifted = len[k] == kChunkBytes ? shift_chunk.apply(r)
+                                                               : lvgpu::shift_matrix(len[k]).apply(r);
+                r = shifted ^ ~out[k];  // ^ R(0, piece k)
+            }
+            crc = ~r;
+        }
+        h_out[i] = (flags & LV_CRC_MASK) ? lv_crc32c_mask(crc) : crc;
+    }
+    return LV_OK;
+}
+
 int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint64_t *h_off,
                          const uint32_t *h_len, const uint32_t *h_seed, uint32_t *h_out, size_t n,
                          uint32_t flags, int device) {
@@ -1937,9 +1991,13 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     if (n == 0) return LV_OK;
     if (!h_arena || !h_off || !h_len || !h_out) return set_err(LV_ERR_INVALID, "null host pointer");
     if (n > 0xffffffffull) return set_err(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
-    for (size_t i = 0; i < n; ++i)
+    bool long_buffers = false;
+    for (size_t i = 0; i < n; ++i) {
         if (h_off[i] > arena_bytes || h_len[i] > arena_bytes - h_off[i])
             return set_err(LV_ERR_INVALID, "buffer outside arena");
+        long_buffers |= h_len[i] > kSplitBytes;
+    }
+    if (long_buffers) return batch_host_split(h_arena, arena_bytes, h_off, h_len, h_seed, h_out, n, flags, device);
     LV_HIP(hipSetDevice(device));
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;

@@ -414,3 +414,21 @@ def test_many_buffers_chunked_sort(torch_dev):
     got = lvgpu.batch(t, o, ln, sd, masked=True).cpu().numpy().view(np.uint32)
     want = oracle_batch(t.cpu().numpy(), offs, lens, seeds, True)
     assert np.array_equal(got, want)
+
+
+def test_host_api_long_buffers(gpu):
+    """lv_crc32c_batch_host cuts buffers over 1 MiB into 256 KiB pieces and
+    joins them with GF(2) shifts: long buffers of whole and ragged piece
+    counts, at odd offsets, beside short ones, seeded, masked and not."""
+    rng = np.random.default_rng(1 << 20)
+    arena = rng.integers(0, 256, size=24 << 20, dtype=np.uint8)
+    lens = np.array([(1 << 20) + 1, 4 << 20, (5 << 20) + 12345, 3, 0, 4096, (1 << 20), 7777777],
+                    dtype=np.uint32)
+    offs = np.array([5, 3 << 20, 7, 11, 0, 99, (16 << 20) + 1, (24 << 20) - 7777777], dtype=np.uint64)
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    for masked in (False, True):
+        want = oracle_batch(arena, offs, lens, seeds, masked)
+        got = lvgpu.batch_host(arena, offs, lens, seeds, masked=masked)
+        assert np.array_equal(got, want), masked
+    want = oracle_batch(arena, offs, lens, None, False)
+    assert np.array_equal(lvgpu.batch_host(arena, offs, lens, None), want)
