@@ -45,6 +45,15 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise LvError(f"{LIB_PATH} missing: build it with `make -C leveldb-rs_amd`")
+    # One HIP runtime per process: liblvgpu.so needs libamdhip64.so, and the
+    # first copy loaded serves every later user of that soname.  Loading torch
+    # first binds the library to torch's bundled runtime; loading ours first
+    # would hand torch the system runtime, after which torch.cuda reports no
+    # device (measured on the MI355X image).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     u8p, u32, u64, sz, vp = ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
     L.lv_crc32c_value.restype = u32
