@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU-box pass of every bench line and kernel profile for the round:
 #   bench.py default (C3 strided, headline), C3 offsets, C2, C4, C5,
-#   the C1 CPU sweep, the host-memory E2E path, and rocprofv3 kernel-trace
+#   the C1 CPU sweep, the host-memory E2E path, the WAL / table / hash rows
+#   of SURVEY 8f, and rocprofv3 kernel-trace
 #   stats for C3 (strided) / C2 / C4.  Every GPU step has its own timeout and
 #   the chain stops at the first failure.
 # usage: tools/measure_round.sh OUTDIR
@@ -23,6 +24,9 @@ b c4 --workload c4 --api offsets --cpu-seconds 5 &&
 b c5 --workload c5 --cpu-seconds 5 &&
 timeout -k 10 200 python3 bench.py --e2e > "$out/e2e.json" 2> "$out/e2e.err" &&
 timeout -k 10 300 python3 bench.py --c1 > "$out/c1.json" 2> "$out/c1.err" &&
+timeout -k 10 300 python3 bench.py --wal > "$out/wal.json" 2> "$out/wal.err" &&
+timeout -k 10 300 python3 bench.py --table > "$out/table.json" 2> "$out/table.err" &&
+timeout -k 10 300 python3 bench.py --hash > "$out/hash.json" 2> "$out/hash.err" &&
 p c3 &&
 p c2 --workload c2 --api offsets &&
 p c4 --workload c4 --api offsets &&
