@@ -43,6 +43,10 @@ uint32_t lv_crc32c_extend_sw(uint32_t crc, const uint8_t *data, size_t n);
 /* crc32c.rs:86-118  pub unsafe fn extend_hw(crc: u32, data: &[u8]) -> u32
  * (requires SSE4.2 on the host, as the reference's #[target_feature] does) */
 uint32_t lv_crc32c_extend_hw(uint32_t crc, const uint8_t *data, size_t n);
+/* Not in the reference (an addition for callers that split long buffers):
+ * extend(s, A || B) from crc_a = extend(s, A) and crc_b = value(B), len_b =
+ * |B|: Shift_{len_b}(crc_a) ^ crc_b with GF(2) shift matrices, O(log len_b). */
+uint32_t lv_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
 /* ---- batch API (device) ------------------------------------------------- */
 

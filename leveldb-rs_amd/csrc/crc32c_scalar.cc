@@ -74,6 +74,13 @@ uint32_t lv_crc32c_unmask(uint32_t masked_crc) {
     return (r >> 17) | (r << 15);
 }
 
+// extend(s, A||B) = ~R(~s, A||B) = ~(Shift_|B|(R(~s, A)) ^ R(0, B)), and with
+// R(~s, A) = ~crc_a, R(0, B) = ~crc_b ^ Shift_|B|(~0) this is
+// Shift_|B|(crc_a) ^ crc_b (GF(2)-linear Shift).
+uint32_t lv_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+    return lvgpu::shift_matrix(len_b).apply(crc_a) ^ crc_b;
+}
+
 // Software path (the twin of crc32c.rs:65-84, same value): slice-by-16, the
 // state xored into the first word, the other 12 bytes indexed directly.
 uint32_t lv_crc32c_extend_sw(uint32_t crc, const uint8_t *data, size_t n) {

@@ -64,6 +64,8 @@ def lib() -> ctypes.CDLL:
     for f in ("lv_crc32c_mask", "lv_crc32c_unmask"):
         getattr(L, f).restype = u32
         getattr(L, f).argtypes = [u32]
+    L.lv_crc32c_combine.restype = u32
+    L.lv_crc32c_combine.argtypes = [u32, u32, u64]
     L.lv_crc32c_batch_device.restype = ctypes.c_int
     L.lv_crc32c_batch_device.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp]
     L.lv_crc32c_workspace_bytes.restype = sz
@@ -135,6 +137,12 @@ def mask(crc: int) -> int:
 
 def unmask(masked_crc: int) -> int:
     return lib().lv_crc32c_unmask(masked_crc & 0xFFFFFFFF)
+
+
+def combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """extend(s, A + B) from crc_a = extend(s, A), crc_b = value(B), len_b = len(B)
+    (an addition, not in the reference: for callers that split long buffers)."""
+    return lib().lv_crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
 
 
 # ---- batch (GPU) -----------------------------------------------------------

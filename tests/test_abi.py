@@ -69,3 +69,20 @@ def test_batch_without_gpu_fails_loudly():
     rc = lvgpu.lib().lv_device_init()
     assert rc != 0
     assert lvgpu.lib().lv_last_error()
+
+
+def test_scalar_combine():
+    """lv_crc32c_combine joins the CRCs of a split buffer (an addition for
+    callers that cut long buffers): every split point of random buffers,
+    seeded, and empty parts."""
+    import random
+    rng = random.Random(99)
+    for _ in range(40):
+        d = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 3000)))
+        s = rng.getrandbits(32)
+        cut = rng.randrange(0, len(d) + 1)
+        a, b = d[:cut], d[cut:]
+        assert lvgpu.combine(lvgpu.extend(s, a), lvgpu.value(b), len(b)) == lvgpu.extend(s, d)
+    assert lvgpu.combine(0x1234, lvgpu.value(b""), 0) == 0x1234
+    big = bytes(range(256)) * 4096  # 1 MiB: a long shift
+    assert lvgpu.combine(lvgpu.value(b"head"), lvgpu.value(big), len(big)) == lvgpu.value(b"head" + big)
