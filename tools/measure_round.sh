@@ -27,6 +27,7 @@ timeout -k 10 300 python3 bench.py --c1 > "$out/c1.json" 2> "$out/c1.err" &&
 timeout -k 10 300 python3 bench.py --wal > "$out/wal.json" 2> "$out/wal.err" &&
 timeout -k 10 300 python3 bench.py --table > "$out/table.json" 2> "$out/table.err" &&
 timeout -k 10 300 python3 bench.py --hash > "$out/hash.json" 2> "$out/hash.err" &&
+timeout -k 10 300 python3 bench.py --sweep > "$out/sweep.json" 2> "$out/sweep.err" &&
 p c3 &&
 p c2 --workload c2 --api offsets &&
 p c4 --workload c4 --api offsets &&
