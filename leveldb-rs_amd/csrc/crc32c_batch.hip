@@ -968,9 +968,27 @@ struct RGeo {
     __device__ __forceinline__ uint32_t ng() const { return (alow() + len) >> 4; }  // whole granules from g0
 };
 
+// Max over lanes l ^ m, m = from .. 32.  The 16- and 32-lane steps are
+// gfx950's v_permlane16/32_swap (VALU; each swap returns v at l and at l ^ m
+// in its two results) instead of ds_bpermute round trips through LDS.
+#ifndef LVK_PERMLANE
+#define LVK_PERMLANE 1
+#endif
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int from) {
     for (int m = from; m < 64; m <<= 1) {
-        const uint32_t o = __shfl_xor(v, m);
+        uint32_t o;
+#if LVK_PERMLANE
+        if (m == 16) {
+            const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            o = r[0] > r[1] ? r[0] : r[1];
+        } else if (m == 32) {
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            o = r[0] > r[1] ? r[0] : r[1];
+        } else
+#endif
+        {
+            o = __shfl_xor(v, m);
+        }
         v = o > v ? o : v;
     }
     return __builtin_amdgcn_readfirstlane(v);
