@@ -1683,8 +1683,16 @@ void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off
 
 // Bytes of sort workspace the offsets API needs for n buffers.
 // Sorting workgroups and elements per workgroup for n buffers.
+// Batches under 1M buffers would leave most CUs idle at 4,096 buffers per
+// workgroup: they split into up to kSortMinWgs workgroups of >= 1,024.
+#ifndef LVK_SORT_MIN_WGS
+#define LVK_SORT_MIN_WGS 256
+#endif
 uint64_t sort_wgs(uint64_t n, uint64_t *chunk) {
+    constexpr uint64_t kSortMinWgs = LVK_SORT_MIN_WGS, kSortMinChunk = 1024;
     uint64_t wgs = (n + lvk::kSortChunk - 1) / lvk::kSortChunk;
+    const uint64_t small = std::min(kSortMinWgs, (n + kSortMinChunk - 1) / kSortMinChunk);
+    if (wgs < small) wgs = small;
     if (wgs > lvk::kSortMaxWgs) wgs = lvk::kSortMaxWgs;
     if (wgs == 0) wgs = 1;
     *chunk = (n + wgs - 1) / wgs;
