@@ -184,6 +184,9 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 #ifndef LVK_EXP_NOFOLD
 #define LVK_EXP_NOFOLD 0
 #endif
+#ifndef LVK_STAGGER  // s_sleep(32) units between the start of successive waves (blocks kernel, >= 8 KiB)
+#define LVK_STAGGER 1u
+#endif
 #ifndef LVK_EXP_NOSTAGE
 #define LVK_EXP_NOSTAGE 0
 #endif
@@ -680,6 +683,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     stage_tables(image);
 #endif
     if (wblk0 >= P.n) return;
+    // Blocks of >= 8 KiB: the waves of a CU start ~0.85 us apart.  Waves that
+    // start together walk their blocks in lockstep, so all 16 K concurrent
+    // streams sit at the same offset within their blocks, and at 8-64 KiB
+    // strides that address pattern reads 2-4 % slower (HBM address mapping:
+    // padding the stride has the same effect).  4 KiB blocks run best in
+    // lockstep (a stagger cost 0.5-1 % there).  Strided 8 / 16 / 64 KiB: 76.8 ->
+    // 79.8, 77.7 -> 80.0, 79.8 -> 81.6 % of 8 TB/s; 32 KiB within noise.
+    if (G == 16 && nb >= 8)
+        for (uint32_t k = 0; k < wave * LVK_STAGGER; ++k) __builtin_amdgcn_s_sleep(32);
     const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
     const Lut L = make_lut(lane);
     uint32_t A[U];
