@@ -36,6 +36,10 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t bs
 }
 
 // One wave's staged key bytes: the 16-B granules spanning its 64 keys.
+#ifndef LVH_SPAN_READLANE
+#define LVH_SPAN_READLANE 1
+#endif
+
 constexpr uint32_t kSpanBytes = 4096;
 constexpr uint32_t kSpanPad = 20;  // dwords past the span a masked fast-path read may address
 
@@ -76,10 +80,23 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     // stages the granules spanning its 64 keys through LDS with coalesced
     // 16-B loads, instead of 64 lanes gathering byte-aligned keys.  Waves
     // whose keys span more than kSpanBytes read keys straight from memory.
+#if LVH_SPAN_READLANE
+    // Candidate span from the first and the last lane of the wave (keys are
+    // usually packed in order); the wave stages it only if every key lies
+    // inside it.  Two lane reads and one ballot instead of two 64-bit
+    // six-step shuffle reductions.
+    const uint64_t act = __ballot(valid);
+    const int last = act ? 63 - __builtin_clzll(act) : 0;
+    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool inside = !L || (o >= lo && o + L <= hi);
+    const bool staged = act && hi > lo && hi - lo16 <= kSpanBytes && __all(inside);  // wave-uniform
+#else
     const uint64_t lo = wave_min_u64(L ? o : ~0ull);
     const uint64_t hi = wave_max_u64(L ? o + L : 0ull);
     const uint64_t lo16 = lo & ~15ull;
     const bool staged = lo != ~0ull && hi - lo16 <= kSpanBytes;  // wave-uniform
+#endif
     if (staged) {
         const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

@@ -143,3 +143,41 @@ def test_gpu_packed_keys_staged_and_not(gpu):
     out = H.hash_batch(a, _dev(gpu, offs, np.int64), _dev(gpu, lens.view(np.int32), np.int32),
                        _dev(gpu, seeds.view(np.int32), np.int32))
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.gpu
+def test_gpu_permuted_and_empty_keys_in_span(gpu):
+    """Waves whose keys lie within 4 KiB but out of order (the first lane
+    is not the lowest key, the last lane not the highest end), waves whose
+    first or last keys are empty, and waves reversed end to end: the kernel
+    stages a wave only when every key lies inside the span its first and last
+    lanes name, and must hash all of them exactly either way."""
+    import torch
+    from lvgpu import hash as H
+    L = _oracle()
+    rng = np.random.default_rng(31337)
+    n = 64 * 40 + 17
+    lens = rng.integers(0, 65, n).astype(np.uint32)
+    lens[0:3] = 0                 # first lanes of wave 0 empty
+    lens[64 * 2 - 1] = 0          # last lane of wave 1 empty
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    offs += 5
+    for w in range(0, n // 64):
+        sl = slice(64 * w, 64 * w + 64)
+        if w % 3 == 1:            # shuffled within the wave's span
+            p = rng.permutation(64)
+            offs[sl], lens[sl] = offs[sl][p], lens[sl][p]
+        elif w % 3 == 2:          # reversed: lane 0 holds the highest key
+            offs[sl], lens[sl] = offs[sl][::-1].copy(), lens[sl][::-1].copy()
+    offs[lens == 0] = rng.integers(0, 4, int((lens == 0).sum()))  # empty keys point anywhere
+    size = int((offs + lens).max()) + 1
+    arena = rng.integers(0, 256, size=size, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = np.zeros(n, dtype=np.uint32)
+    L.oracle_hash_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, seeds.ctypes.data,
+                        want.ctypes.data, n)
+    a = torch.from_numpy(arena).to(gpu)
+    out = H.hash_batch(a, _dev(gpu, offs, np.int64), _dev(gpu, lens.view(np.int32), np.int32),
+                       _dev(gpu, seeds.view(np.int32), np.int32))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
