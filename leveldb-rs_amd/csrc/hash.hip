@@ -11,6 +11,7 @@
 // key's last byte, and keys of <= 64 B run the chain from registers.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstring>
 
 #include "../../include/lvgpu/crc32c.h"
@@ -41,6 +42,10 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t bs
 #endif
 
 constexpr uint32_t kSpanBytes = 4096;
+#ifndef LVH_WGS_PER_CU
+#define LVH_WGS_PER_CU 8
+#endif
+constexpr uint64_t kWgsPerCu = LVH_WGS_PER_CU;
 constexpr uint32_t kSpanPad = 20;  // dwords past the span a masked fast-path read may address
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
@@ -61,18 +66,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return v;
 }
 
-__global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ base,
-                                                   const uint64_t *__restrict__ off,
-                                                   const uint32_t *__restrict__ len,
-                                                   const uint32_t *__restrict__ seed, uint32_t *__restrict__ out,
-                                                   uint32_t n, uint32_t flags) {
-    __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpanBytes / 4 + kSpanPad];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const bool valid = i < n;
-    const uint64_t o = valid ? off[i] : 0u;
-    const uint32_t L = valid ? len[i] : 0u;
-    uint32_t h = (valid && seed ? seed[i] : 0u) ^ (kM * L);  // hash.rs:25
+// Hash of this lane's key of one wave-set of 64 keys (metadata already
+// loaded); span is the wave's LDS stage.
+__device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, uint32_t *span, bool valid,
+                                             uint64_t o, uint32_t L, uint32_t sdv, uint32_t lane,
+                                             uint32_t *pout, uint32_t pval, bool pst) {
+    uint32_t h = sdv ^ (kM * L);  // hash.rs:25
     const uint32_t bs = static_cast<uint32_t>(o & 3u);
     const uint32_t nw = L >> 2;               // whole words, hash.rs:29
     const uint32_t ndw = (bs + L + 3) >> 2;   // dwords covering the buffer
@@ -101,15 +100,27 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
         const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 *src = reinterpret_cast<const u32x4 *>(base + lo16);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(span[wv]);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(span);
+        constexpr uint32_t kCh = kSpanBytes / 16 / 64;
+        u32x4 t[kCh];
 #pragma unroll
-        for (uint32_t k = 0; k < kSpanBytes / 16 / 64; ++k) {
+        for (uint32_t k = 0; k < kCh; ++k) {
             const uint32_t c = lane + 64u * k;
-            if (c < nch) dst[c] = __builtin_nontemporal_load(src + c);
+            if (c < nch) t[k] = __builtin_nontemporal_load(src + c);
+        }
+        // the previous set's result leaves after this set's loads: waiting
+        // for them (vmcnt is in order) then does not wait for the store
+        if (pst) *pout = pval;
+#pragma unroll
+        for (uint32_t k = 0; k < kCh; ++k) {
+            const uint32_t c = lane + 64u * k;
+            if (c < nch) dst[c] = t[k];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else if (pst) {
+        *pout = pval;
     }
     if (valid && L && ndw <= kFastDw) {
         // Keys of up to ~64 B (cache keys): every dword of the key is read at
@@ -118,7 +129,7 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
         // chain then runs from registers, predicated per lane.
         uint32_t w[kFastDw + 1];
         if (staged) {
-            const uint32_t *sd = span[wv] + ((o - bs - lo16) >> 2);
+            const uint32_t *sd = span + ((o - bs - lo16) >> 2);
 #pragma unroll
             for (uint32_t j = 0; j < kFastDw; ++j) w[j] = j < ndw ? sd[j] : 0u;
         } else {
@@ -205,7 +216,56 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
             h ^= h >> 24;
         }
     }
-    if (valid) out[i] = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
+    return h;
+}
+
+// Persistent: wave w of the grid hashes wave-sets w, w + W, ... of 64 keys.
+// The next set's metadata is requested before this set's keys, so its
+// latency overlaps theirs: one memory round trip per set instead of two
+// (a one-set-per-wave grid: meta, then span, then compute, 65 -> 71 % of
+// 8 TB/s was the ceiling of that shape).
+__global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ base,
+                                                   const uint64_t *__restrict__ off,
+                                                   const uint32_t *__restrict__ len,
+                                                   const uint32_t *__restrict__ seed, uint32_t *__restrict__ out,
+                                                   uint32_t n, uint32_t flags) {
+    __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpanBytes / 4 + kSpanPad];
+    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
+    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
+    if (set * 64u >= n) return;  // wave-uniform
+    auto meta = [&](uint64_t st, uint64_t &o, uint32_t &L, uint32_t &sd) {
+        const uint64_t i = st * 64u + lane;
+        const bool v = i < n;
+        o = v ? off[i] : 0u;
+        L = v ? len[i] : 0u;
+        sd = v && seed ? seed[i] : 0u;
+    };
+    uint64_t o, on;
+    uint32_t L, sd, Ln, sdn;
+    meta(set, o, L, sd);
+    uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late
+    bool pst = false;
+    for (;;) {
+        const uint64_t nxt = set + W;
+        const bool more = nxt * 64u < n;  // wave-uniform
+        if (more) meta(nxt, on, Ln, sdn);
+        const uint64_t i = set * 64u + lane;
+        const bool valid = i < n;
+        const uint32_t h = hash_set(base, span[wv], valid, o, L, sd, lane, pout, pval, pst);
+        pout = out + (valid ? i : 0u);
+        pval = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
+        pst = valid;
+        if (!more) {
+            if (pst) *pout = pval;
+            break;
+        }
+        __builtin_amdgcn_wave_barrier();  // this set's LDS reads precede the next stage
+        set = nxt;
+        o = on;
+        L = Ln;
+        sd = sdn;
+    }
 }
 
 }  // namespace lvh
@@ -242,7 +302,16 @@ int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const ui
     if (!d_arena || !d_off || !d_len || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
     if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
-    const uint32_t grid = static_cast<uint32_t>((n + 255) / 256);
+    // persistent grid: 8 workgroups (32 waves) per CU at most
+    static std::atomic<int> cus_cache[64];
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) cus = cus_cache[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        if (dev >= 0 && dev < 64) cus_cache[dev].store(cus, std::memory_order_relaxed);
+    }
+    const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * lvh::kWgsPerCu;
+    const uint32_t grid = static_cast<uint32_t>(want < cap ? want : cap);
     hipLaunchKernelGGL(lvh::hash_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_arena, d_off,
                        d_len, d_seed, d_out, static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
