@@ -1693,7 +1693,6 @@ void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off
     }
 }
 
-// Bytes of sort workspace the offsets API needs for n buffers.
 // Sorting workgroups and elements per workgroup for n buffers.
 // At 4,096 buffers per workgroup a batch under 1M buffers leaves most CUs
 // idle in the sort passes: batches under 4M split into up to kSortMinWgs
@@ -1713,7 +1712,8 @@ uint64_t sort_wgs(uint64_t n, uint64_t *chunk) {
     return wgs;
 }
 
-// Header, histogram matrix, n sorted 16-B entries, then n seeds in entry order.
+// Bytes of sort workspace the offsets API needs for n buffers: header,
+// histogram matrix, n sorted 16-B entries, then n seeds in entry order.
 size_t sort_ws_bytes(uint64_t n) {
     uint64_t chunk = 0;
     const uint64_t wgs = sort_wgs(n, &chunk);

@@ -1,3 +1,5 @@
+# A/B of the length sort's workgroup floor (LVK_SORT_MIN_WGS) on C3 via offsets and the table bench.
+# Variants first: tools/build_variant.sh old -DLVK_SORT_MIN_WGS=1; tools/build_variant.sh new -DLVK_SORT_MIN_WGS=256
 set -o pipefail
 R=$(pwd); O=gpurun_out/ab1; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -20 $O/pytest.txt; exit 1; }

@@ -1,4 +1,5 @@
-# A/B of the sort's workgroup floor on C2/C4 (1M buffers): variants new (256) and w1024
+# A/B of the sort's workgroup floor on C2/C4 (1M buffers): variants new (-DLVK_SORT_MIN_WGS=256) and w1024 (=1024),
+# built with tools/build_variant.sh
 set -o pipefail
 R=$(pwd); O=gpurun_out/ab2; mkdir -p $O
 for rep in 1 2; do
