@@ -9,6 +9,9 @@
 // memory.  Either way the words are dword-aligned reads funnel-shifted by the
 // key's byte misalignment (v_alignbyte_b32), never touching a dword past the
 // key's last byte, and keys of <= 64 B run the chain from registers.
+// The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
+// requests the next set's metadata ahead, and stores each result one set
+// late, after the next set's loads, so no wait includes a store.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
