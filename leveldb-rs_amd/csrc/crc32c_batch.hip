@@ -690,9 +690,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     // padding the stride has the same effect).  4 KiB blocks run best in
     // lockstep (a stagger cost 0.5-1 % there).  Strided 8 / 16 / 64 KiB: 76.8 ->
     // 79.8, 77.7 -> 80.0, 79.8 -> 81.6 % of 8 TB/s; 32 KiB within noise.
-    if (G == 16 && nb >= 8)
-        for (uint32_t k = 0; k < wave * LVK_STAGGER; ++k) __builtin_amdgcn_s_sleep(32);
+    // Only waves with >= 64 batches to walk stagger (the last wave's delay,
+    // ~13 us, is then a few batches of its work): a small batch would
+    // otherwise wait out the delay.
     const uint64_t rounds = (P.n - 1 - wblk0) / gstride + 1;
+    if (G == 16 && nb >= 8 && rounds * nb >= 64)
+        for (uint32_t k = 0; k < wave * LVK_STAGGER; ++k) __builtin_amdgcn_s_sleep(32);
     const Lut L = make_lut(lane);
     uint32_t A[U];
     // The flush store's operands live in registers of their own for the whole
