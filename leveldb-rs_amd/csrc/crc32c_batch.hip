@@ -1781,10 +1781,13 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
 
 // Group size for the uniform-block kernel, or -1 when the blocks are not
 // 16-B aligned whole batches for any supported G.
-int pick_block_gi(uint64_t base, uint64_t stride, uint64_t blen, int forced) {
+int pick_block_gi(uint64_t base, uint64_t stride, uint64_t blen, int forced, uint64_t n, int cus) {
     if (blen == 0 || base % 16 || stride % 16) return -1;
     auto fits = [&](int gi) { return blen % (16ull * kGs[gi] * lvk::U) == 0; };
     if (forced >= 0) return fits(forced) ? forced : -1;
+    // Few blocks: 16-lane groups would keep only n/4 of the grid's waves
+    // busy, each walking its blocks alone; 64-lane groups put n waves on them.
+    if (n < 4ull * static_cast<uint64_t>(cus) * lvk::kWaves && fits(3)) return 3;
     for (int gi : {2, 1, 0})
         if (fits(gi)) return gi;
     return -1;
@@ -1905,7 +1908,7 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
     if (int rc = current_ctx(&c)) return rc;
     const int gi = forced_gi(flags);
     // Aligned whole-batch blocks take the uniform-block kernel.
-    const int bgi = pick_block_gi(reinterpret_cast<uint64_t>(d_base), stride, block_len, gi);
+    const int bgi = pick_block_gi(reinterpret_cast<uint64_t>(d_base), stride, block_len, gi, n, c->cus);
     if (bgi >= 0) {
         launch_blocks(*c, bgi, d_base, stride, block_len, n, d_seed, d_out, flags,
                       static_cast<hipStream_t>(stream));

@@ -214,7 +214,7 @@ def test_bad_arguments_raise(torch_dev):
         lvgpu._check(rc)
 
 
-@pytest.mark.parametrize("group", [None, 1, 4, 16])
+@pytest.mark.parametrize("group", [None, 1, 4, 16, 64])
 @pytest.mark.parametrize("block_len,stride_pad,n", [
     (64, 0, 1), (64, 16, 4097), (256, 0, 3001), (256, 48, 777), (1024, 0, 1025), (1024, 32, 64),
     (4096, 0, 262), (4096, 4096, 100), (8192, 16, 513), (65536, 0, 37), (1048576, 0, 3)])
