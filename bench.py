@@ -2,14 +2,21 @@
 """Benchmark: device-resident batched CRC32C on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
+                    [--scaling weak|strong]
 
 One "step" = one batch CRC32C launch over this rank's whole synthetic batch,
 inputs already resident in HBM.  Default workload (N=1 headline, BASELINE.json
 configs[2]): 262,144 SSTable-sized 4 KiB blocks = 1 GiB per GPU, offsets
 i*4096, seed 0, splitmix64 payload generated on the device.  With N>1
-(torchrun) every rank checksums its own shard of the same shape (weak
+(torchrun) every rank checksums its own batch of the same shape (weak
 scaling, no data-path collective; the only collectives are the timing
-barrier and the max-over-ranks of the elapsed time).
+barrier and the max-over-ranks of the elapsed time).  `--scaling strong`
+splits ONE global batch (c5: 16,777,216 x 4 KiB = 64 GiB)
+into contiguous rank ranges instead (lvgpu.shard).
+
+Before the W warmup steps a `settle` phase runs back-to-back launches until
+the chip's idle->busy power transient has passed (reported in the JSON line,
+separate from `warmup`; see settle()).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
 `roofline` (kernel launch duration by HIP events on the launch stream vs the
@@ -67,6 +74,12 @@ def parse():
     p.add_argument("--c1", action="store_true",
                    help="CPU-only config 1: the benches/crc32c.rs sweep (oracle extend_sw/extend_hw and the "
                         "product's scalar drop-ins), one JSON line; no GPU")
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="weak: every rank checksums its own batch of the workload's shape (default); "
+                        "strong: one global batch (c5 = 64 GiB) split into contiguous rank ranges (SURVEY 8e)")
+    p.add_argument("--no-settle", dest="settle", action="store_false",
+                   help="skip the settle phase (back-to-back launches until the idle->busy power transient "
+                        "has passed; reported as `settle`, separate from --warmup)")
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
                    help="auto: measure roofline.traffic in a child rocprofv3 --pmc FETCH_SIZE pass")
     return p.parse_args()
@@ -185,7 +198,7 @@ def measure_traffic(args):
     out = tempfile.mkdtemp(prefix="lvgpu_pmc_", dir="/tmp")
     cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
            sys.executable, os.path.abspath(__file__), "--steps", "10", "--warmup", "60", "--cpu-seconds", "0",
-           "--traffic", "off", "--workload", args.workload, "--api", args.api]
+           "--traffic", "off", "--workload", args.workload, "--api", args.api, "--scaling", args.scaling]
     if args.group:
         cmd += ["--group", str(args.group)]
     if args.blocks:
@@ -619,6 +632,91 @@ def wal_bench(args):
                       "data": "synthetic: Random(301).skewed(17) record sizes, random payload"}), flush=True)
 
 
+def settle(torch, step, stream, min_s=0.3, max_s=3.0, chunk=20, window=5, tol=0.015):
+    """Run back-to-back launches until the launch time has stopped moving.
+
+    An MI355X coming out of idle runs its first ~100 back-to-back 1 GiB
+    launches through a power-management transient: launch time rises from
+    0.167 to ~0.21 ms around launches 10-40 and relaxes back to 0.164 over the
+    next ~100 (tools/ramp_probe.py, profiles/r02/ramp/).  It recurs after 1 s
+    or 3 s of idle on the same arena and does not appear on a freshly
+    allocated arena while the chip is busy, so it is the chip's idle -> busy
+    clock/power state, not first touch of the memory (sysfs mclk/fclk read
+    2000/1250 MHz throughout; sclk DPM does not track it).  The settle phase
+    is kept apart from `warmup` so `steps`/`warmup` stay what the caller
+    asked for: chunks of `chunk` launches are timed by events (two chunks in
+    flight, so the queue never drains) until at least `min_s` has passed and
+    the last `window` chunk times lie within `tol` of each other, or `max_s`."""
+    t0 = time.perf_counter()
+    pend, times = [], []
+    launches = 0
+    while True:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(chunk):
+            step()
+        b.record(stream)
+        launches += chunk
+        pend.append((a, b))
+        if len(pend) < 2:
+            continue
+        a0, b0 = pend.pop(0)
+        b0.synchronize()
+        times.append(a0.elapsed_time(b0) / chunk)
+        el = time.perf_counter() - t0
+        w = times[-window:]
+        if el >= max_s or (el >= min_s and len(w) == window and max(w) <= min(w) * (1 + tol)):
+            break
+    torch.cuda.synchronize()
+    return {"launches": launches, "seconds": round(time.perf_counter() - t0, 3),
+            "first_chunk_ms": round(times[0], 4), "peak_chunk_ms": round(max(times), 4),
+            "last_chunk_ms": round(times[-1], 4),
+            "rule": f">= {min_s} s of back-to-back launches and the last {window} chunks of {chunk} "
+                    f"within {tol * 100:.1f} % (cap {max_s} s)",
+            "why": "idle->busy power transient of the chip (tools/ramp_probe.py); not part of warmup"}
+
+
+def build_shard(torch, lvgpu, args, dev, rank, world):
+    """Strong scaling: ONE global batch, this rank's
+    contiguous slice of it.  c5: 16,777,216 x 4 KiB = 64 GiB; c3: 262,144 x
+    4 KiB; c2/c4: the global length list split by payload bytes.  The rank
+    generates only its slice's bytes of the global splitmix arena (the fill
+    is indexed by global byte), so every rank reads exactly what a single GPU
+    would.  Returns (arena, off, len, shard, description)."""
+    from lvgpu.shard import RankShard
+    import numpy as np
+    if args.workload in ("c3", "c5"):
+        n_total = args.blocks or (262144 if args.workload == "c3" else 16777216)
+        sh = RankShard.uniform(n_total, 4096, rank, world)
+        desc = (f"{args.workload}: global batch {n_total} x 4096 B ({n_total * 4096 / 2**30:.0f} GiB), "
+                f"rank {rank} owns blocks [{sh.lo}, {sh.hi})")
+        pad = 0
+    else:
+        lens = global_lengths(args.workload)
+        sh = RankShard.packed(lens, rank, world)
+        desc = (f"{args.workload}: global batch of {lens.size} buffers split by payload bytes, "
+                f"rank {rank} owns [{sh.lo}, {sh.hi})")
+        pad = 16
+    arena = torch.empty(sh.byte_hi - sh.byte_lo + pad, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, sh.byte_lo, PAYLOAD_SEED)
+    off = torch.from_numpy(sh.local_off.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(sh.lens.view(np.int32)).to(dev)
+    return arena, off, ln, sh, desc
+
+
+def global_lengths(name):
+    """The c2 / c4 length lists (rank-independent, for strong scaling)."""
+    import numpy as np
+    if name == "c2":
+        return wal_unit_lengths(1048576)
+    rng = np.random.default_rng(0xC0FFEE)
+    kk = np.arange(1, 2049, dtype=np.float64)
+    cdf = np.cumsum(kk ** -1.1)
+    cdf /= cdf[-1]
+    k = np.minimum(np.searchsorted(cdf, rng.random(1048576), side="right") + 1, 2048)
+    return (32 * k).astype(np.uint32)
+
+
 def main():
     args = parse()
     if args.wal:
@@ -635,6 +733,7 @@ def main():
         return hash_bench(args)
     import torch
     import lvgpu
+    from lvgpu import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -654,42 +753,40 @@ def main():
     torch.cuda.set_device(dev)
     lvgpu.device_init()
 
-    arena, off, ln, nbytes, desc = build_workload(torch, lvgpu, args.workload, dev, rank, args.blocks)
-    n = off.numel()
-    out = torch.empty(n, dtype=torch.int32, device=dev)
+    if args.scaling == "strong":
+        arena, off, ln, sh, desc = build_shard(torch, lvgpu, args, dev, rank, world)
+        nbytes, n = sh.payload_bytes, sh.n
+    else:
+        arena, off, ln, nbytes, desc = build_workload(torch, lvgpu, args.workload, dev, rank, args.blocks)
+        n = off.numel()
+    out = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
+    strided = args.api == "strided" and args.workload in ("c3", "c5")
 
-    if args.api == "strided" and args.workload in ("c3", "c5"):
+    if n == 0:
+        def step():
+            pass
+    elif strided:
         def step():
             lvgpu.batch_strided(arena, 4096, 4096, n, out=out, stream=stream, group=args.group)
     else:
         def step():
             lvgpu.batch(arena, off, ln, out=out, stream=stream, group=args.group)
 
+    settle_info = settle(torch, step, stream) if args.settle and n else None
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
     # Timed region (value): K steps between barrier + synchronize, nothing
-    # else on the stream.  A timestamp event between launches costs ~3 % of
-    # the step time on MI355X, so the per-launch HIP events for
+    # else on the stream, max over ranks (lvgpu.shard.timed_steps, the code
+    # the gloo test drives).  A timestamp event between launches costs ~3 %
+    # of the step time on MI355X, so the per-launch HIP events for
     # roofline.achieved are taken in a second pass of the same K steps, right
     # after, on the launch stream.
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    el_own = time.perf_counter() - t0  # this rank alone (per_gpu)
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el_own, el = shard.timed_steps(
+        step, args.steps, torch.cuda.synchronize, dist,
+        lambda x: torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu"))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     for s, e in evs:
@@ -703,16 +800,15 @@ def main():
         print("per-launch ms:", " ".join(f"{x:.4f}" for x in kern_seq), file=sys.stderr)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
     # per-GPU figures: each rank's own timed-pass rate and kernel rate
-    own = {"rank": rank, "device": local, "GiB_per_s": round(nbytes * args.steps / 2**30 / el_own, 2),
-           "kernel_GB_per_s": round(nbytes / (kern_avg_ms * 1e-3) / 1e9, 1)}
-    per_rank = [own]
-    if dist:
-        per_rank = [None] * world
-        dist.all_gather_object(per_rank, own)
-
-    total_bytes = nbytes * world
-    value = total_bytes * args.steps / 2**30 / el
+    own = {"rank": rank, "device": local, "payload_bytes": nbytes,
+           "GiB_per_s": round(nbytes * args.steps / 2**30 / el_own, 2),
+           "kernel_GB_per_s": round(nbytes / (kern_avg_ms * 1e-3) / 1e9, 1),
+           "frac_of_8TBps": round(nbytes / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    per_rank = shard.gather_ranks(own, dist, world)
+    agg = shard.aggregate(per_rank, args.steps, el)
+    value = agg["GiB_per_s"]
     achieved_gbs = nbytes / (kern_avg_ms * 1e-3) / 1e9
+    kernel = lvgpu.last_kernel()
 
     result = None
     if rank == 0:
@@ -728,19 +824,22 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 payload generated in HBM)",
             "config": {"workload": desc, "buffers_per_gpu": n, "bytes_per_gpu": nbytes,
-                       "api": ("lv_crc32c_batch_strided" if args.api == "strided" and args.workload in ("c3", "c5")
-                               else "lv_crc32c_batch_device"),
-                       "parallelism": f"dp{world} (independent shards, no collective)"},
+                       "total_bytes_per_step": agg["total_bytes_per_step"],
+                       "api": "lv_crc32c_batch_strided" if strided else "lv_crc32c_batch_device",
+                       "parallelism": (f"dp{world} (independent shards, no collective)" if args.scaling == "weak"
+                                       else f"dp{world} (one global batch split into contiguous rank ranges, "
+                                            f"no collective)")},
             "hbm_peak_frac": round(value * 2**30 / world / 1e9 / HBM_PEAK_GBS, 4),
+            "settle": settle_info,
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic), "traffic_source": tsrc,
-                         "kernel": ("lvk::crc32c_blocks_kernel" if args.api == "strided" and args.workload in ("c3", "c5")
-                                    else "lv_crc32c_batch_device step: lvk::sort_{hist,scan,scatter} + "
-                                         "lvk::crc32c_classes_kernel"),
+                         "kernel": "lvk::" + kernel if strided else
+                                   "lv_crc32c_batch_device step: lvk::sort_{hist,scan,scatter} + "
+                                   "lvk::crc32c_classes_kernel",
                          "kernel_ms_avg": round(kern_avg_ms, 4),
                          "kernel_ms_min": round(kern_ms[0], 4),
                          "kernel_ms_p50": round(kern_ms[len(kern_ms) // 2], 4),
@@ -749,6 +848,7 @@ def main():
                                    "pass of the K timed steps"},
             "cpu_baseline": cpu,
             "per_gpu": per_rank,
+            "load_imbalance": round(agg["imbalance"], 4),
         }
         print(json.dumps(result), flush=True)
     if dist:

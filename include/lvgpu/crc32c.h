@@ -116,6 +116,10 @@ int lv_device_init(void);
 const char *lv_last_error(void);
 /* Library version string. */
 const char *lv_version(void);
+/* Debug query: name of the kernel the calling thread's last batch call
+ * launched ("crc32c_blocks_kernel<16>", "sort+crc32c_classes_kernel", ...;
+ * "" before any).  Lets tests assert which path a geometry takes. */
+const char *lv_crc32c_last_kernel(void);
 
 /* ---- synthetic data (bench / tests) ------------------------------------- */
 

@@ -40,6 +40,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -189,6 +190,12 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 #endif
 #ifndef LVK_EXP_NOSTAGE
 #define LVK_EXP_NOSTAGE 0
+#endif
+// The LVK_EXP_* switches compute WRONG CRCs: a build that sets one must say
+// so explicitly (tools/build_variant.sh passes LVK_EXPERIMENT_BUILD=1 and
+// names the library a variant), so they can never reach the product library.
+#if (LVK_EXP_NOSHIFT || LVK_EXP_NOFOLD || LVK_EXP_NOSTAGE) && !defined(LVK_EXPERIMENT_BUILD)
+#error "LVK_EXP_* timing switches compute wrong CRCs; define LVK_EXPERIMENT_BUILD for an experiment variant"
 #endif
 // NU rows per batch; W4OFF = LDS offset of the Latin row-shift table (the
 // image's W4 = Shift_{64G}, or region B's W2 = Shift_{32G} for NU = 2).
@@ -1492,6 +1499,8 @@ __global__ void fill_bytes_kernel(uint8_t *dst, uint64_t begin, uint64_t nbytes,
 namespace {
 
 thread_local std::string g_err;
+// Kernel the calling thread's last batch call launched (lv_crc32c_last_kernel).
+thread_local const char *g_kernel = "";
 
 int set_err(int code, const std::string &msg) {
     g_err = msg;
@@ -1544,15 +1553,25 @@ const std::vector<uint32_t> &host_image(int gi) {
     return images[gi];
 }
 
+// Library-owned sort workspace of one (device, stream).  Calls on one stream
+// are stream-ordered on the GPU, but two host threads enqueueing on the same
+// stream would interleave their four kernels: `m` is held from the workspace
+// lookup through the last launch of a call, so one call's sort passes are
+// enqueued back to back and a growing hipFree never frees a buffer another
+// thread has been handed but not yet launched on.
+struct StreamWs {
+    std::mutex m;
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+};
+
 struct DevCtx {
     std::mutex m;  // one-time init
     bool ready = false;
     int cus = 0;
     uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
-    // offsets-API sort workspace, one per stream (calls on one stream are
-    // stream-ordered, so reusing its buffer is safe; different streams never share)
-    std::mutex ws_m;
-    std::map<hipStream_t, std::pair<uint8_t *, size_t>> ws;
+    std::mutex ws_m;  // guards the map (entries are never erased)
+    std::map<hipStream_t, std::unique_ptr<StreamWs>> ws;
     // host-path staging (grown on demand), serialised by host_m
     std::mutex host_m;
     uint8_t *d_arena = nullptr;
@@ -1680,6 +1699,9 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
     P.flags = flags;
     P.ent = nullptr;
     P.sseed = nullptr;
+    static const std::string name = std::string("crc32c_batch_kernel<") + std::to_string(G) +
+                                    (STRIDED ? ",strided>" : ",offsets>");
+    g_kernel = name.c_str();
     hipLaunchKernelGGL((lvk::crc32c_batch_kernel<G, STRIDED>), dim3(static_cast<uint32_t>(grid)),
                        dim3(lvk::kThreads), 0, s, P, c.image[gi]);
 }
@@ -1725,19 +1747,26 @@ size_t sort_ws_bytes(uint64_t n) {
 }
 
 // The library-owned workspace of (device, stream), grown on demand (the sort
-// needs no initialised state).
-int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out) {
-    std::lock_guard<std::mutex> lk(c.ws_m);
-    auto &w = c.ws[s];
-    const size_t need = sort_ws_bytes(n);
-    if (w.second < need) {
-        if (w.first) LV_HIP(hipFree(w.first));
-        w.first = nullptr;
-        w.second = 0;
-        LV_HIP(hipMalloc(&w.first, need));
-        w.second = need;
+// needs no initialised state).  Returns with the workspace's lock held in
+// `lk`; the caller keeps it until its last launch has been enqueued.
+int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_lock<std::mutex> *lk) {
+    StreamWs *w = nullptr;
+    {
+        std::lock_guard<std::mutex> mk(c.ws_m);
+        auto &slot = c.ws[s];
+        if (!slot) slot.reset(new StreamWs);
+        w = slot.get();
     }
-    *out = w.first;
+    *lk = std::unique_lock<std::mutex>(w->m);
+    const size_t need = sort_ws_bytes(n);
+    if (w->cap < need) {
+        if (w->p) LV_HIP(hipFree(w->p));
+        w->p = nullptr;
+        w->cap = 0;
+        LV_HIP(hipMalloc(&w->p, need));
+        w->cap = need;
+    }
+    *out = w->p;
     return 0;
 }
 
@@ -1769,7 +1798,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     P.flags = flags;
     P.ent = ent;
     P.sseed = seed ? sseed : nullptr;
-
+    g_kernel = "sort+crc32c_classes_kernel";
     if (seed)
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<true>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0,
                            s, P, c.image[2], ws);
@@ -1813,6 +1842,8 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
     P.ent = nullptr;
     P.sseed = nullptr;
     const uint32_t nb = static_cast<uint32_t>(blen / (16ull * G * lvk::U));
+    static const std::string name = "crc32c_blocks_kernel<" + std::to_string(G) + ">";
+    g_kernel = name.c_str();
     if (seed)
         hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G, true>), dim3(static_cast<uint32_t>(grid)),
                            dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
@@ -1850,7 +1881,9 @@ extern "C" {
 
 const char *lv_last_error(void) { return g_err.c_str(); }
 
-const char *lv_version(void) { return "lvgpu 0.1.0 gfx950"; }
+const char *lv_version(void) { return "lvgpu 0.2.0 gfx950"; }
+
+const char *lv_crc32c_last_kernel(void) { return g_kernel; }
 
 int lv_device_init(void) {
     DevCtx *c = nullptr;
@@ -1872,11 +1905,12 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
         launch_g<false>(*c, gi, d_arena, d_off, d_len, 0, 0, d_seed, d_out, n, flags, s);
         return check_launch();
     }
+    std::unique_lock<std::mutex> ws_lk;  // held through the last launch (library workspace)
     if (d_ws) {
         if (ws_bytes < sort_ws_bytes(n)) return set_err(LV_ERR_INVALID, "workspace too small");
         if (reinterpret_cast<uintptr_t>(d_ws) % 16) return set_err(LV_ERR_INVALID, "workspace must be 16-byte aligned");
         // no initialisation: every workspace word the sort reads, it wrote first
-    } else if (int rc = stream_ws(*c, s, n, &d_ws)) {
+    } else if (int rc = stream_ws(*c, s, n, &d_ws, &ws_lk)) {
         return rc;
     }
     if (int rc = launch_binned(*c, d_ws, d_arena, d_off, d_len, d_seed, d_out, n, flags, s)) return rc;
@@ -1904,6 +1938,7 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
     g_err.clear();
     if (n == 0) return LV_OK;
     if (!d_base || !d_out) return set_err(LV_ERR_INVALID, "null device pointer");
+    if (n > 0xffffffffull) return set_err(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     const int gi = forced_gi(flags);
@@ -1944,7 +1979,10 @@ static int upload_locked(DevCtx &c, const uint8_t *h, size_t bytes, size_t pad) 
     for (size_t pos = 0; pos < bytes; pos += kStageBytes, ++k) {
         const size_t len = bytes - pos < kStageBytes ? bytes - pos : kStageBytes;
         const int slot = static_cast<int>(k & 1);
-        if (k >= 2) LV_HIP(hipEventSynchronize(c.ev[slot]));
+        // the slot's previous H2D (this call's, or an earlier call's that
+        // returned early on an error without synchronizing) must be done;
+        // an event never recorded completes at once
+        LV_HIP(hipEventSynchronize(c.ev[slot]));
         par_memcpy(c.h_stage[slot], h + pos, len);
         LV_HIP(hipMemcpyAsync(c.d_arena + pos, c.h_stage[slot], len, hipMemcpyHostToDevice, s));
         LV_HIP(hipEventRecord(c.ev[slot], s));
@@ -1953,8 +1991,22 @@ static int upload_locked(DevCtx &c, const uint8_t *h, size_t bytes, size_t pad) 
 }
 
 namespace lvgpu_internal {
-int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath *hp) {
+int DeviceGuard::set(int device) {
+    if (prev < 0) {
+        int d = 0;
+        LV_HIP(hipGetDevice(&d));
+        prev = d;
+    }
     LV_HIP(hipSetDevice(device));
+    return LV_OK;
+}
+
+DeviceGuard::~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+}
+
+int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath *hp) {
+    if (int rc = hp->dg.set(device)) return rc;
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     hp->lk = std::unique_lock<std::mutex>(c->host_m);
@@ -2044,7 +2096,8 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
         long_buffers |= h_len[i] > kSplitBytes;
     }
     if (long_buffers) return batch_host_split(h_arena, arena_bytes, h_off, h_len, h_seed, h_out, n, flags, device);
-    LV_HIP(hipSetDevice(device));
+    lvgpu_internal::DeviceGuard dg;  // the caller's current device comes back on return
+    if (int rc = dg.set(device)) return rc;
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     std::lock_guard<std::mutex> lk(c->host_m);
@@ -2064,7 +2117,8 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     if (h_seed) std::memcpy(c->h_meta + n * 12, h_seed, n * 4);
     LV_HIP(hipMemcpyAsync(d_off, c->h_meta, n * (h_seed ? 16 : 12), hipMemcpyHostToDevice, s));
     uint8_t *ws = nullptr;
-    if (int rc = stream_ws(*c, s, n, &ws)) return rc;
+    std::unique_lock<std::mutex> ws_lk;
+    if (int rc = stream_ws(*c, s, n, &ws, &ws_lk)) return rc;
     if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s))
         return rc;
     if (int rc = check_launch()) return rc;

@@ -17,11 +17,25 @@ int set_error(int code, const char *msg);  // lv_last_error plumbing (crc32c_bat
 void clear_error();
 int launch_status();                       // hipGetLastError -> LV status + message
 
+// Selects a device for the calling thread and restores the thread's previous
+// current device when it goes out of scope: the host entry points take a
+// `device` argument, and a drop-in C ABI must not leave the caller's thread
+// pointed at another GPU (crc32c_batch.hip).
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() = default;
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+    int set(int device);  // LV status; the first call saves the current device
+    ~DeviceGuard();
+};
+
 // Host-memory path of one device (crc32c_batch.hip): holds the device's
 // host-path lock while alive.  host_upload copies `bytes` of host memory into
 // the device's cached arena (pinned input: one DMA; pageable: a pipelined
 // pinned staging copy) followed by `pad` zero bytes, on the device's stream.
 struct HostPath {
+    DeviceGuard dg;  // restored after the lock is released
     std::unique_lock<std::mutex> lk;
     void *stream = nullptr;     // hipStream_t
     uint8_t *d_arena = nullptr;

@@ -166,7 +166,9 @@ int lv_sst_verify_blocks_host(const uint8_t *file, uint64_t file_bytes, const ui
             rc = lvgpu_internal::set_error(static_cast<int>(e), (std::string(what) + ": " + hipGetErrorString(e)).c_str());
         return rc == LV_OK;
     };
-    if (hip(hipSetDevice(device), "hipSetDevice") && hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream") &&
+    lvgpu_internal::DeviceGuard dg;  // the caller's current device comes back on return
+    if (int e = dg.set(device)) return e;
+    if (hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream") &&
         hip(hipMalloc(&d_file, file_bytes + 16), "hipMalloc") && hip(hipMalloc(&d_h, n * 16), "hipMalloc") &&
         hip(hipMalloc(&d_st, n * 4), "hipMalloc") &&
         hip(hipMemcpyAsync(d_file, file, file_bytes, hipMemcpyHostToDevice, s), "H2D") &&

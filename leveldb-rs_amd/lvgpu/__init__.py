@@ -18,8 +18,24 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-# LVGPU_LIB selects another build of the same library (A/B kernel experiments)
-LIB_PATH = os.environ.get("LVGPU_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "liblvgpu.so")
+PRODUCT_LIB = os.path.join(os.path.dirname(_PKG), "lib", "liblvgpu.so")
+
+
+def _lib_path() -> str:
+    """The product library, unless an experiment explicitly selects a variant:
+    LVGPU_LIB is honoured only together with LVGPU_EXPERIMENT=1 and only for a
+    build under lib/variants/ (tools/build_variant.sh, sanitizer builds), which
+    never ships to the GPU box (.gpurunignore)."""
+    alt = os.environ.get("LVGPU_LIB")
+    if not alt or os.environ.get("LVGPU_EXPERIMENT") != "1":
+        return PRODUCT_LIB
+    variants = os.path.join(os.path.dirname(_PKG), "lib", "variants")
+    if os.path.dirname(os.path.realpath(alt)) != os.path.realpath(variants):
+        raise RuntimeError(f"LVGPU_LIB must name a build under {variants}")
+    return alt
+
+
+LIB_PATH = _lib_path()
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "lvgpu", "crc32c.h")
 
 MASK = 0x1  # LV_CRC_MASK
@@ -86,6 +102,8 @@ def lib() -> ctypes.CDLL:
     L.lv_last_error.argtypes = []
     L.lv_version.restype = ctypes.c_char_p
     L.lv_version.argtypes = []
+    L.lv_crc32c_last_kernel.restype = ctypes.c_char_p
+    L.lv_crc32c_last_kernel.argtypes = []
     L.lv_fill_splitmix.restype = ctypes.c_int
     L.lv_fill_splitmix.argtypes = [vp, u64, u64, u64, vp]
     _lib = L
@@ -277,3 +295,8 @@ def device_init() -> None:
 
 def version() -> str:
     return lib().lv_version().decode()
+
+
+def last_kernel() -> str:
+    """Kernel the calling thread's last batch call launched (debug query)."""
+    return lib().lv_crc32c_last_kernel().decode()

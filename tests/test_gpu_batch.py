@@ -432,3 +432,63 @@ def test_host_api_long_buffers(gpu):
         assert np.array_equal(got, want), masked
     want = oracle_batch(arena, offs, lens, None, False)
     assert np.array_equal(lvgpu.batch_host(arena, offs, lens, None), want)
+
+
+def test_two_threads_same_stream(torch_dev, arena):
+    """Two host threads call the offsets API on the SAME stream (the default
+    one) with different batch sizes: the library's per-stream sort workspace
+    is locked from lookup through the last launch of a call, so neither
+    call's sort passes interleave with the other's."""
+    import threading
+    torch, dev = torch_dev
+    rng = np.random.default_rng(77)
+    a = torch.frombuffer(bytearray(arena), dtype=torch.uint8).to(dev)
+    cases = []
+    for n in (5000, 23000):
+        lens = rng.integers(0, 9000, size=n).astype(np.uint32)
+        offs = rng.integers(0, len(arena) - 9000, size=n).astype(np.uint64)
+        want = oracle_batch(arena, offs, lens, None, False)
+        o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+        ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+        cases.append((o, ln, want))
+    stream = torch.cuda.current_stream()
+    errors = []
+
+    def worker(k):
+        o, ln, want = cases[k]
+        try:
+            for _ in range(30):
+                out = lvgpu.batch(a, o, ln, stream=stream)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy().view(np.uint32)
+                if not np.array_equal(got, want):
+                    errors.append(k)
+                    return
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+    th = [threading.Thread(target=worker, args=(k,)) for k in (0, 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert errors == []
+
+
+def test_kernel_choice_query(torch_dev):
+    """lv_crc32c_last_kernel names the path a call took: aligned whole-batch
+    blocks run the uniform-block kernel (G by block count), unaligned strided
+    geometry the generic strided kernel, the offsets API the sort + class
+    kernel."""
+    torch, dev = torch_dev
+    t = torch.zeros(4096 * 2048 + 64, dtype=torch.uint8, device=dev)
+    lvgpu.batch_strided(t, 4096, 4096, 2048)
+    assert lvgpu.last_kernel() == "crc32c_blocks_kernel<64>"  # few blocks: 64-lane groups
+    lvgpu.batch_strided(t, 4096, 4096, 2048, group=16)
+    assert lvgpu.last_kernel() == "crc32c_blocks_kernel<16>"
+    lvgpu.batch_strided(t[1:], 4096, 4096, 2048)
+    assert lvgpu.last_kernel().startswith("crc32c_batch_kernel<") and lvgpu.last_kernel().endswith(",strided>")
+    o = torch.arange(16, dtype=torch.int64, device=dev) * 100
+    ln = torch.full((16,), 100, dtype=torch.int32, device=dev)
+    lvgpu.batch(t, o, ln)
+    assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel"
+    torch.cuda.synchronize()

@@ -7,10 +7,10 @@ for v in $vars; do
   L=$R/leveldb-rs_amd/lib/variants/liblvgpu_$v.so
   line="$v"
   for w in c2 c4 c3; do
-    LVGPU_LIB=$L timeout -k 10 200 python3 bench.py --workload $w --api offsets --cpu-seconds 0 --traffic off > $O/${v}_${w}_$rep.json 2>$O/err || exit 1
+    LVGPU_EXPERIMENT=1 LVGPU_LIB=$L timeout -k 10 200 python3 bench.py --workload $w --api offsets --cpu-seconds 0 --traffic off > $O/${v}_${w}_$rep.json 2>$O/err || exit 1
     line="$line $w $(python3 -c "import json; d=json.load(open('$O/${v}_${w}_$rep.json')); print(d['roofline']['frac'])")"
   done
-  LVGPU_LIB=$L timeout -k 10 200 python3 bench.py --table > $O/${v}_table_$rep.json 2>$O/err || exit 1
+  LVGPU_EXPERIMENT=1 LVGPU_LIB=$L timeout -k 10 200 python3 bench.py --table > $O/${v}_table_$rep.json 2>$O/err || exit 1
   line="$line table $(python3 -c "import json; t=json.load(open('$O/${v}_table_$rep.json')); print(t['seal']['frac_of_8TBps'], t['verify']['frac_of_8TBps'])")"
   echo $line
 done; done

@@ -15,7 +15,7 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY" \
            "SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"; do
   i=$((i+1))
-  (cd /tmp && LVGPU_LIB=$lib timeout -k 10 120 rocprofv3 --pmc $set --output-format csv -d "$root/$out/p$i" -o pmc -- \
+  (cd /tmp && LVGPU_EXPERIMENT=1 LVGPU_LIB=$lib timeout -k 10 120 rocprofv3 --pmc $set --output-format csv -d "$root/$out/p$i" -o pmc -- \
      python3 "$root/bench.py" --steps 5 --warmup 20 --cpu-seconds 0 --traffic off "$@") > "$root/$out/p$i.txt" 2>&1 || { echo "pass $i failed"; tail -5 "$root/$out/p$i.txt"; exit 1; }
 done
 python3 - "$root/$out" <<'PY'

@@ -5,6 +5,7 @@
 set -eo pipefail
 root=$(cd "$(dirname "$0")/.." && pwd)
 make -s -C "$root/leveldb-rs_amd" sanitize > /dev/null
+export LVGPU_EXPERIMENT=1
 export LVGPU_LIB="$root/leveldb-rs_amd/lib/variants/liblvgpu_asan.so"
 export LD_PRELOAD="$(gcc -print-file-name=libasan.so)"
 export ASAN_OPTIONS=detect_leaks=0
