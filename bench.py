@@ -382,7 +382,9 @@ def c1_sweep(args):
 
 
 def _event_times(torch, fn, steps, warmup):
-    """Median and mean ms of `fn` by HIP events on the current stream."""
+    """Median and mean ms of `fn` by HIP events on the current stream, after
+    the settle phase (see settle()) and `warmup` calls."""
+    settle(torch, fn, torch.cuda.current_stream())
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()

@@ -47,6 +47,7 @@
 #include <vector>
 
 #include "../../include/lvgpu/crc32c.h"
+#include "../../include/lvgpu/table.h"
 #include "crc32c_gf2.h"
 #include "lv_internal.h"
 
@@ -199,8 +200,13 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 #endif
 // NU rows per batch; W4OFF = LDS offset of the Latin row-shift table (the
 // image's W4 = Shift_{64G}, or region B's W2 = Shift_{32G} for NU = 2).
-template <bool FIRST, int W4K = -1, uint32_t NU = U, uint32_t W4OFF = kRegionA + kHalf>
+// SKIP (FIRST batches only): the leading rows that hold no buffer byte for
+// any group of the wave are not folded (their accumulators start at 0, as a
+// fold of zero granules would leave them).
+template <bool FIRST, int W4K = -1, uint32_t NU = U, uint32_t W4OFF = kRegionA + kHalf, uint32_t SKIP = 0>
 __device__ __forceinline__ void fold_batch(const uint4 (&v)[NU], uint32_t (&A)[NU], const Lut &L) {
+    static_assert(SKIP == 0 || FIRST, "only a first batch skips rows");
+    static_assert(SKIP < NU, "at least one row");
 #if LVK_EXP_NOFOLD  // experiment only: no lookups at all (load-structure bound)
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) A[i] = (FIRST ? 0u : A[i]) ^ xor3(v[i].x, v[i].y, v[i].z) ^ v[i].w;
@@ -209,6 +215,10 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[NU], uint32_t (&A)[N
     uint32_t s[NU], w[NU], w3[NU];
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) s[i] = v[i].x;
+    if constexpr (SKIP > 0) {
+#pragma unroll
+        for (uint32_t i = 0; i < SKIP; ++i) A[i] = 0u;
+    }
     if constexpr (!FIRST && W4K >= 0) {
 #pragma unroll
         for (uint32_t i = 0; i < NU; ++i) {
@@ -241,7 +251,7 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[NU], uint32_t (&A)[N
     for (uint32_t step = 0; step < 4; ++step) {
         uint32_t ad[NU][4];
 #pragma unroll
-        for (uint32_t i = 0; i < NU; ++i) {
+        for (uint32_t i = SKIP; i < NU; ++i) {
             ad[i][0] = lut_addr<0>(s[i], L);
             ad[i][1] = lut_addr<1>(s[i], L);
             ad[i][2] = lut_addr<2>(s[i], L);
@@ -249,11 +259,11 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[NU], uint32_t (&A)[N
         }
         uint32_t t[NU][4];
 #pragma unroll
-        for (uint32_t i = 0; i < NU; ++i)
+        for (uint32_t i = SKIP; i < NU; ++i)
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) t[i][k] = lds_word(ad[i][k] + kRegionA);
 #pragma unroll
-        for (uint32_t i = 0; i < NU; ++i) {
+        for (uint32_t i = SKIP; i < NU; ++i) {
             const uint32_t x = xor3(t[i][0], t[i][1], t[i][2]);
             if (step < 3) {
                 const uint32_t nw = step == 0 ? v[i].y : step == 1 ? v[i].z : v[i].w;
@@ -985,6 +995,7 @@ struct RGeo {
     uint32_t len;
     uint32_t seed;
     uint32_t bid;   // output slot, or ~0u for a lane past the end of the list
+    uint32_t aux;   // per-source extra (table units: in-range flag | type byte << 8)
     __device__ __forceinline__ uint64_t abase() const { return a & ~static_cast<uint64_t>(15); }
     __device__ __forceinline__ uint32_t alow() const { return static_cast<uint32_t>(a) & 15u; }
     __device__ __forceinline__ uint32_t ng() const { return (alow() + len) >> 4; }  // whole granules from g0
@@ -1031,6 +1042,7 @@ __device__ __forceinline__ RGeo load_rgeo(const Params &P, uint64_t e) {
     q.len = v.z;
     q.seed = SEEDED ? P.sseed[ec] : 0u;
     q.bid = valid ? v.w : 0xffffffffu;
+    q.aux = 0;
     return q;
 }
 
@@ -1264,16 +1276,79 @@ __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a
     return X;
 }
 
-__device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q, uint32_t X, const uint4 &tail,
-                                                 uint32_t gl, const Lut &L) {
+// Leading rows of a round's first batch that hold no buffer byte for any
+// group of the wave (wave-uniform, <= NU - 1): the first fold skips them.
+#ifndef LVK_SKIP_PAD
+#define LVK_SKIP_PAD 1
+#endif
+template <int G, uint32_t NU>
+__device__ __forceinline__ uint32_t round_pad(const RGeo &q, uint32_t nbw) {
+    uint32_t padg;
+    if constexpr (LVK_ALIGNED_ROWS && G == 16) {
+        const int32_t p = static_cast<int32_t>(NU * nbw) - al_geo(q).re - 1;
+        padg = p <= 0 ? 0u : static_cast<uint32_t>(p);
+    } else {  // end-aligned rows: row i is empty for every lane iff ng - G*NU*nbw + G*(i+1) - 1 < 0
+        const uint32_t gu = G * NU * nbw, ng = q.ng();
+        padg = gu > ng ? (gu - ng) / G : 0u;
+    }
+    padg = padg < NU - 1 ? padg : NU - 1;
+    return (NU - 1) - wave_max_u32((NU - 1) - padg, G);
+}
+
+template <int W4K, uint32_t NU, uint32_t W4OFF>
+__device__ __forceinline__ void fold_first(const uint4 (&v)[NU], uint32_t (&A)[NU], const Lut &L, uint32_t pad) {
+#if LVK_SKIP_PAD
+    if constexpr (NU == 4) {
+        if (pad == 3) {
+            fold_batch<true, W4K, NU, W4OFF, 3>(v, A, L);
+            return;
+        }
+        if (pad == 2) {
+            fold_batch<true, W4K, NU, W4OFF, 2>(v, A, L);
+            return;
+        }
+        if (pad == 1) {
+            fold_batch<true, W4K, NU, W4OFF, 1>(v, A, L);
+            return;
+        }
+    }
+#endif
+    fold_batch<true, W4K, NU, W4OFF>(v, A, L);
+}
+
+// The raw register R(~seed, buffer) (lane 0 of the group), before the final
+// xor and mask: the tail bytes, then the short-buffer seed.
+__device__ __forceinline__ uint32_t finish_raw(const RGeo &q, uint32_t X, const uint4 &tail, uint32_t gl,
+                                               const Lut &L) {
     X = fold_tail(X, tail, q, L);
     if (gl == 0 && q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for short buffers
         uint32_t s = ~q.seed;
         for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u);
         X ^= s;
     }
-    return final_crc(P, X);
+    return X;
 }
+
+// Entry source and result sink of the sorted walk: the offsets API's
+// length-sorted list.  load() reads entry e; trailer() issues any extra
+// per-unit loads with the tail load; stage() parks a unit's result in the
+// wave's LDS slots (lane 0 of the group); flush() stores the parked results
+// of the last rounds, one global store per lane, every kFlush rounds.
+template <bool SEEDED>
+struct SortedList {
+    static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
+    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const { return load_rgeo<SEEDED>(P, e); }
+    __device__ __forceinline__ uint2 trailer(const RGeo &, uint32_t) const { return make_uint2(0, 0); }
+    __device__ __forceinline__ void stage(const Params &P, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
+                                          uint2) const {
+        g_oidx[wave][slot] = q.bid;
+        g_ocrc[wave][slot] = final_crc(P, X);
+    }
+    __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
+        const uint32_t bi = g_oidx[wave][lane], cv = g_ocrc[wave][lane];
+        if (lane < nslots && bi != 0xffffffffu) P.out[bi] = cv;
+    }
+};
 
 // One wave walks rounds of the sorted list: round rho holds entries
 // rho*K + group (K = 64/G groups).  The rounds come from `next()` (a static
@@ -1285,9 +1360,9 @@ __device__ __forceinline__ uint32_t finish_round(const Params &P, const RGeo &q,
 // loads and spills cost more than the conservative wait counts they remove.)
 // The image is always the G = 16 one: groups of G = 1 and 4 take their
 // row-shift and merge tables from the plain combine tables.
-template <int G, bool SEEDED, class Next>
-__device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, const Lut &L, uint64_t rho,
-                                              Next next) {
+template <int G, class Src, class Next>
+__device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
+                                              uint64_t rho, Next next) {
     constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
     constexpr uint32_t NU = AL ? kAlRows : U;          // rows per batch
     // Latin row shift Shift_{16 G NU}: the image's W4 (NU = 4) or W2 (NU = 2)
@@ -1302,16 +1377,18 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
     if (rho >= nr) return;
     uint64_t rhon = next();
 
-    RGeo q = load_rgeo<SEEDED>(P, rho * K + grp);
+    RGeo q = src.load(P, rho * K + grp);
     // (AL) some group of the round ends before lane 15.  The row geometry
     // (al_geo) is recomputed from q where it is used: fewer live registers.
     bool rot = AL && __any(al_geo(q).e != 15);
     uint32_t nbw = AL ? round_nbw_al<NU>(al_geo(q)) : round_nbw<G>(q);
     uint32_t jfix = AL ? round_jfix_al<NU>(q, nbw) : round_jfix<G>(q, nbw);
+    uint32_t pad = round_pad<G, NU>(q, nbw);
     RGeo qn = q;
-    if (rhon < nr) qn = load_rgeo<SEEDED>(P, rhon * K + grp);
+    if (rhon < nr) qn = src.load(P, rhon * K + grp);
     uint32_t nbwn = 0;
     uint4 tail;
+    uint2 tr;
     uint4 slot0[NU], slot1[NU];
     if constexpr (AL)
         load_rbatch_al<NU>(q, nbw, 0, gl, slot0);
@@ -1332,6 +1409,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
                 load_rbatch<G>(q, nbw, j + 1, gl, nxt);
         } else {
             tail = load_rtail(q, gl);  // consumed after this batch's fold
+            tr = src.trailer(q, gl);
             if (more) {
                 if constexpr (AL) {
                     nbwn = round_nbw_al<NU>(al_geo(qn));
@@ -1351,7 +1429,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
             if (lastj) a3p = j == 0 ? 0u : A[NU - 1];
         }
         if (j == 0)
-            fold_batch<true, W4K, NU, W4OFF>(cur, A, L);
+            fold_first<W4K, NU, W4OFF>(cur, A, L, pad);
         else
             fold_batch<false, W4K, NU, W4OFF>(cur, A, L);
         if (!lastj) {
@@ -1363,16 +1441,14 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
             X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
         else
             X = merge_group<G, W1K, W2K>(A, L);
-        const uint32_t crc = finish_round(P, q, X, tail, gl, L);
-        const uint32_t slot = (c % G) * K + grp;
-        if (gl == 0) {
-            g_oidx[wave][slot] = q.bid;
-            g_ocrc[wave][slot] = crc;
-        }
-        if ((c + 1) % G == 0 || !more) {
+        X = finish_raw(q, X, tail, gl, L);
+        // slots: rounds per flush x groups per wave <= 64
+        constexpr uint32_t kF = Src::kFlush * K <= 64 ? Src::kFlush : 64 / K;
+        const uint32_t slot = (c % kF) * K + grp;
+        if (gl == 0) src.stage(P, wave, slot, q, X, tr);
+        if ((c + 1) % kF == 0 || !more) {
             __builtin_amdgcn_wave_barrier();
-            const uint32_t bi = g_oidx[wave][lane], cv = g_ocrc[wave][lane];
-            if (lane < (c % G + 1) * K && bi != 0xffffffffu) P.out[bi] = cv;
+            src.flush(P, wave, lane, (c % kF + 1) * K);
             __builtin_amdgcn_wave_barrier();
         }
         if (!more) return true;
@@ -1385,8 +1461,9 @@ __device__ __forceinline__ void sorted_stream(const Params &P, uint32_t lane, co
         } else {
             jfix = round_jfix<G>(q, nbw);
         }
+        pad = round_pad<G, NU>(q, nbw);
         rhon = next();
-        if (rhon < nr) qn = load_rgeo<SEEDED>(P, rhon * K + grp);
+        if (rhon < nr) qn = src.load(P, rhon * K + grp);
         j = 0;
         return false;
     };
@@ -1457,10 +1534,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         uint64_t k = 0;
         auto stride = [&]() { return sw + (++k) * nsw; };
         if (cls[4]) {
-            sorted_stream<1, SEEDED>(sub_list(P, cls[0], cls[4]), lane, L, sw, stride);
+            sorted_stream<1>(sub_list(P, cls[0], cls[4]), SortedList<SEEDED>(), lane, L, sw, stride);
             k = 0;
         }
-        if (cls[5]) sorted_stream<4, SEEDED>(sub_list(P, cls[1], cls[5]), lane, L, sw, stride);
+        if (cls[5]) sorted_stream<4>(sub_list(P, cls[1], cls[5]), SortedList<SEEDED>(), lane, L, sw, stride);
     }
     if (n23) {
         auto pool = [&]() -> uint64_t {
@@ -1468,8 +1545,123 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
             if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
             return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
         };
-        sorted_stream<16, SEEDED>(sub_list(P, cls[6] ? cls[2] : cls[3], n23), lane, L, pool(), pool);
+        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23), SortedList<SEEDED>(), lane, L, pool(), pool);
     }
+}
+
+// ---------------------------------------------------------------------------
+// SSTable block trailers in ONE launch (include/lvgpu/table.h).
+// The table's blocks are walked in file order, four per wave round, by the
+// G = 16 aligned-row walk: blocks of one table have similar sizes (block_size
+// plus at most one entry), so consecutive blocks give a near-uniform round
+// with no length sort.  The handles (BlockHandle extents, table/format.rs:
+// 29-50) are read directly, and the trailer work is the epilogue:
+//  * verify: unit = contents || type (size + 1 bytes); the stored LE32 after
+//    it is loaded with the tail and compared after unmask;
+//  * seal: unit = contents; the type byte enters the register by one table
+//    step, R(s, D || t) = T0-step(R(s, D), t), so no byte is written before
+//    it is read, and type + LE32(mask(crc)) are written in the flush.
+// (Round 1 ran units -> 3 sort passes -> class kernel -> trailer kernel.)
+__device__ __forceinline__ bool sst_in_range(uint64_t o, uint64_t sz, uint64_t file_bytes) {
+    return sz < 0xffffffffull && o <= file_bytes && sz <= file_bytes - o && file_bytes - o - sz >= 5u;
+}
+
+template <bool SEAL>
+struct TableUnits {
+    const uint2 *handles;  // {offset, size} u64 pairs per block
+    const uint8_t *types;  // seal: per-block type byte (NULL: 0 = no compression)
+    uint32_t *status;      // verify: LV_SST_BLOCK_* per block
+    uint32_t *crc_out;     // verify: optional crc32c(contents || type)
+    uint64_t file_bytes;
+    static constexpr uint32_t kFlush = 8;  // 32 slots of four words (g_oidx, g_ocrc halves)
+
+    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
+        const bool valid = e < P.n;
+        const uint64_t ec = valid ? e : P.n - 1;
+        const uint2 ho = handles[2 * ec], hs = handles[2 * ec + 1];  // u64 pairs: 8-B alignment is enough
+        const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
+        const bool ok = sst_in_range(o, sz, file_bytes);
+        RGeo q;
+        q.len = ok ? static_cast<uint32_t>(SEAL ? sz : sz + 1) : 0u;
+        q.a = q.len ? P.base + o : P.base;
+        q.seed = 0;
+        q.bid = valid ? static_cast<uint32_t>(ec) : 0xffffffffu;
+        uint32_t t = 0;
+        if (SEAL && types && ok) t = types[ec];
+        q.aux = (ok ? 1u : 0u) | (t << 8);
+        return q;
+    }
+    // verify: the stored masked crc at the unit's end (two aligned dwords)
+    __device__ __forceinline__ uint2 trailer(const RGeo &q, uint32_t gl) const {
+        if (SEAL || gl != 0 || !(q.aux & 1u)) return make_uint2(0, 0);
+        const uint64_t end = q.a + q.len;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(end & ~static_cast<uint64_t>(3));
+        return make_uint2(w[0], (end & 3u) ? w[1] : 0u);
+    }
+    __device__ __forceinline__ void stage(const Params &, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
+                                          uint2 tr) const {
+        const bool ok = q.aux & 1u;
+        if constexpr (SEAL) {
+            const uint32_t t = (q.aux >> 8) & 0xffu;
+            const uint32_t crc = ~byte_step(X, t);
+            const uint64_t at = q.a + q.len;  // type byte, then LE32(mask(crc))
+            g_oidx[wave][slot] = static_cast<uint32_t>(at);
+            g_oidx[wave][32 + slot] = static_cast<uint32_t>(at >> 32);
+            g_ocrc[wave][slot] = mask_crc(crc);
+            g_ocrc[wave][32 + slot] = t | (ok && q.bid != 0xffffffffu ? 0x100u : 0u);
+        } else {
+            const uint32_t crc = ~X;
+            const uint32_t k = static_cast<uint32_t>(q.a + q.len) & 3u;
+            const uint32_t stored = k ? (tr.x >> (8 * k)) | (tr.y << (32 - 8 * k)) : tr.x;
+            const uint32_t r = stored - 0xa282ead8u;  // unmask, crc32c.rs:59-63
+            const uint32_t st = !ok ? LV_SST_BLOCK_OUT_OF_RANGE
+                                    : (((r >> 17) | (r << 15)) == crc ? LV_SST_BLOCK_OK : LV_SST_BLOCK_CHECKSUM_MISMATCH);
+            g_oidx[wave][slot] = q.bid;
+            g_ocrc[wave][slot] = st;
+            g_ocrc[wave][32 + slot] = ok ? crc : 0u;
+        }
+    }
+    __device__ __forceinline__ void flush(const Params &, uint32_t wave, uint32_t lane, uint32_t nslots) const {
+        const uint32_t sl = lane & 31u;
+        if (sl >= nslots) return;
+        if constexpr (SEAL) {
+            if (lane >= 32) return;
+            const uint32_t f = g_ocrc[wave][32 + sl];
+            if (!(f & 0x100u)) return;
+            uint8_t *p = reinterpret_cast<uint8_t *>((static_cast<uint64_t>(g_oidx[wave][32 + sl]) << 32) |
+                                                      g_oidx[wave][sl]);
+            const uint32_t m = g_ocrc[wave][sl];
+            p[0] = static_cast<uint8_t>(f);
+            p[1] = static_cast<uint8_t>(m);
+            p[2] = static_cast<uint8_t>(m >> 8);
+            p[3] = static_cast<uint8_t>(m >> 16);
+            p[4] = static_cast<uint8_t>(m >> 24);
+        } else {
+            const uint32_t bi = g_oidx[wave][sl];
+            if (bi == 0xffffffffu) return;
+            if (lane < 32)
+                status[bi] = g_ocrc[wave][sl];
+            else if (crc_out)
+                crc_out[bi] = g_ocrc[wave][32 + sl];
+        }
+    }
+};
+
+template <bool SEAL>
+__global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
+                                                              TableUnits<SEAL> src) {
+    stage_tables(image);
+    if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const Lut L = make_lut(lane);
+    const uint64_t grid = gridDim.x;
+    auto pool = [&]() -> uint64_t {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
+        return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+    };
+    sorted_stream<16>(P, src, lane, L, pool(), pool);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -2014,6 +2206,29 @@ int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath
     hp->stream = c->stream;
     hp->d_arena = c->d_arena;
     return LV_OK;
+}
+
+// SSTable trailers (csrc/sst.hip): one sst_blocks_kernel launch.
+int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, const uint64_t *d_handles,
+                      const uint8_t *d_types, size_t n, uint32_t *d_status, uint32_t *d_crc, void *stream) {
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    lvk::Params P{};
+    P.base = reinterpret_cast<uint64_t>(d_file);
+    P.n = n;
+    P.flags = 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (n + 3) / 4))), block(lvk::kThreads);
+    if (seal) {
+        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
+        g_kernel = "sst_blocks_kernel<seal>";
+        hipLaunchKernelGGL(lvk::sst_blocks_kernel<true>, grid, block, 0, s, P, c->image[2], u);
+    } else {
+        lvk::TableUnits<false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
+        g_kernel = "sst_blocks_kernel<verify>";
+        hipLaunchKernelGGL(lvk::sst_blocks_kernel<false>, grid, block, 0, s, P, c->image[2], u);
+    }
+    return check_launch();
 }
 
 int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d) {

@@ -41,6 +41,10 @@ struct HostPath {
     uint8_t *d_arena = nullptr;
 };
 int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath *hp);
+// SSTable trailer seal (d_types may be NULL) or verify (d_status, optional
+// d_crc) of n blocks in one launch on the current device (crc32c_batch.hip).
+int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, const uint64_t *d_handles,
+                      const uint8_t *d_types, size_t n, uint32_t *d_status, uint32_t *d_crc, void *stream);
 // Cached device scratch buffer `slot` (0..1) of the HostPath's device, >= bytes.
 int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d);
 }

@@ -169,3 +169,31 @@ def test_gpu_trailer_fixture(gpu, tfix, arena):
     out = d.cpu().numpy().tobytes()
     for (o, ln), (_, _, _, hx) in zip(handles, tfix["trailers"]):
         assert out[o + ln:o + ln + 5].hex() == hx
+
+
+@pytest.mark.gpu
+def test_gpu_table_one_launch_any_order(gpu):
+    """Seal and verify are one kernel launch that walks the handles in the
+    order given (no length sort): shuffled handles, sizes 0-70,000 B mixed
+    (several rows-per-round shapes in one wave), a count that is not a
+    multiple of the 4 blocks of a wave round, random types, crc output."""
+    import lvgpu
+    import torch
+    from lvgpu import table as LT
+    rng = np.random.default_rng(73)
+    sizes = np.concatenate([rng.integers(0, 70000, size=150), rng.integers(4000, 4400, size=151), [0, 1, 2, 3, 4]])
+    file, handles = _make_table(rng, sizes.size, sizes=sizes)
+    perm = rng.permutation(len(handles))
+    handles = [handles[i] for i in perm]
+    types = rng.integers(0, 256, size=len(handles)).astype(np.uint8)
+    d = torch.frombuffer(bytearray(file), dtype=torch.uint8).to(gpu)
+    h = torch.tensor(handles, dtype=torch.int64, device=gpu)
+    LT.seal_blocks(d, h, torch.from_numpy(types).to(gpu))
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<seal>"
+    want = _oracle_seal(file, handles, types.tolist())
+    assert d.cpu().numpy().tobytes() == want
+    st, crc = LT.verify_blocks(d, h, out_crc=True)
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<verify>"
+    assert st.cpu().numpy().tolist() == [0] * len(handles)
+    got = crc.cpu().numpy().view(np.uint32).tolist()
+    assert got == [W.value(want[o:o + sz + 1]) for o, sz in handles]
