@@ -1215,7 +1215,8 @@ __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) {
         int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
-        d = d < 0 ? 0 : (d > dmax ? dmax : d);
+        d = d > dmax ? dmax : d;  // upper clamp first: a buffer with no whole granule has dmax = -1
+        d = d < 0 ? 0 : d;
         const uint64_t ad = ab + (static_cast<uint32_t>(d) << 4);
         v[i] = (LVK_AL_RT_LAST && i == NU - 1) ? load16_rt(ad) : load16(ad);
     }
@@ -1583,7 +1584,9 @@ struct TableUnits {
         const bool ok = sst_in_range(o, sz, file_bytes);
         RGeo q;
         q.len = ok ? static_cast<uint32_t>(SEAL ? sz : sz + 1) : 0u;
-        q.a = q.len ? P.base + o : P.base;
+        // in range: the block's own offset even when empty (its trailer goes
+        // there; its loads stay inside the file); otherwise the file start
+        q.a = ok ? P.base + o : P.base;
         q.seed = 0;
         q.bid = valid ? static_cast<uint32_t>(ec) : 0xffffffffu;
         uint32_t t = 0;
