@@ -341,6 +341,8 @@ struct Params {
     uint64_t stride;
     uint32_t blen;
     uint32_t flags;
+    uint64_t plen;    // long-block split (blocks kernel, PIECES): bytes per piece
+    uint32_t pshift;  // log2 pieces per block
     const uint4 *ent;       // optional: sorted entries {off lo, off hi, len, buffer index}
     const uint32_t *sseed;  // optional: seeds in sorted-entry order
 };
@@ -670,7 +672,11 @@ __device__ __forceinline__ uint32_t final_crc(const Params &P, uint32_t X) {
 // batch waits with the count of that path (vmcnt(2)..(0) after a 4-load
 // prefetch) and so for the prefetch itself, serialising load and compute in
 // every step.
-template <int G, bool SEEDED>
+// PIECES: the long-block split of the strided API.  Virtual block v is piece
+// v & (2^pshift - 1) of block v >> pshift (plen bytes each); piece 0 takes
+// the block's seed, the others start from a zero register, and the output is
+// the raw register R (no final xor, no mask) for combine_pieces_kernel.
+template <int G, bool SEEDED, bool PIECES = false>
 __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint32_t nb,
                                                                  const uint4 *__restrict__ image) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -685,13 +691,28 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     // Rounds of blocks are wave-uniform: the wave runs while its first group
     // has a block; groups past the end are masked.
     const uint64_t wblk0 = (static_cast<uint64_t>(blockIdx.x) * kW + wave) * kGroups;
-    auto block_ptr = [&](uint64_t k) { return P.base + (k < P.n ? k : 0) * P.stride + 16u * gl; };
-    auto seed_ld = [&](uint64_t k) { return ~P.seed[k < P.n ? k : 0]; };
+    const uint64_t pmask = (1ull << P.pshift) - 1;
+    auto block_ptr = [&](uint64_t k) {
+        const uint64_t kk = k < P.n ? k : 0;
+        if constexpr (PIECES) return P.base + (kk >> P.pshift) * P.stride + (kk & pmask) * P.plen + 16u * gl;
+        return P.base + kk * P.stride + 16u * gl;
+    };
+    // the word xored into lane 0's first word of block k: ~seed (0 -> ~0)
+    // for a whole block or a first piece, 0 for a later piece (raw R(0, .))
+    auto seed_ld = [&](uint64_t k) -> uint32_t {
+        const uint64_t kk = k < P.n ? k : 0;
+        if constexpr (PIECES) {
+            const uint32_t sd = SEEDED ? ~P.seed[kk >> P.pshift] : 0xffffffffu;
+            return (kk & pmask) ? 0u : sd;
+        }
+        return ~P.seed[kk];
+    };
+    constexpr bool kVarS0 = SEEDED || PIECES;
 
     // The first batch (and seed) is requested before the table image is
     // staged, so its HBM latency overlaps the staging.
     uint64_t ptr = block_ptr(blk);
-    uint32_t s0 = SEEDED ? seed_ld(blk) : 0xffffffffu;
+    uint32_t s0 = kVarS0 ? seed_ld(blk) : 0xffffffffu;
     uint32_t s0n = s0;
     uint4 slot0[U], slot1[U];
 #pragma unroll
@@ -730,7 +751,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         // no next batch: a dummy read of the arena's first row, the same lines
         // for every wave (L2 hits)
         const uint64_t lptr = more ? nptr : P.base + 16u * gl;
-        if constexpr (SEEDED) s0n = seed_ld(blk + gstride);
+        if constexpr (kVarS0) s0n = seed_ld(blk + gstride);
 #pragma unroll
         for (uint32_t i = 0; i < U; ++i) nxt[i] = load16(lptr + kRow * i);
         if (j == 0) {
@@ -743,7 +764,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
             // round r's K results -> LDS slot (r % G)*K + group; one store of
             // the wave's 64 slots every G rounds (and after the last round)
             const uint32_t X = merge_group<G, -1, -1, true>(A, L);
-            if (gl == 0) g_ocrc[wave][(r % G) * kGroups + lane / G] = final_crc(P, X);
+            if (gl == 0) g_ocrc[wave][(r % G) * kGroups + lane / G] = PIECES ? X : final_crc(P, X);
             if ((r + 1) % G == 0 || r + 1 == rounds) {
                 __builtin_amdgcn_wave_barrier();
                 const uint64_t r0 = r - r % G;
@@ -754,7 +775,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
                 __builtin_amdgcn_wave_barrier();
             }
             blk += gstride;
-            if constexpr (SEEDED) s0 = s0n;
+            if constexpr (kVarS0) s0 = s0n;
         }
         ptr = nptr;
     };
@@ -1667,6 +1688,50 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
     sorted_stream<16>(P, src, lane, L, pool(), pool);
 }
 
+// Joins the raw piece registers of the long-block split: block b's pieces
+// R_k = raw[b*s + k], k < s (s a power of two <= 1024), give
+//   R(~seed, block) = XOR_k Shift_{(s-1-k) plen}(R_k)
+// (linearity, DESIGN "CRC algebra").  One wave per block: lane l < min(s, 64)
+// runs Horner over its pieces k = l + 64 m with Shift_{64 plen}, then shifts
+// by (min(s, 64) - 1 - l) plen; an xor over the wave, then ~ and the mask.
+// mats: 65 GF(2) matrices of 32 column images, Shift_{j plen} for j < 64 and
+// Shift_{64 plen} (built on the host, crc32c_gf2.h).
+__device__ __forceinline__ uint32_t gf2_apply(const uint32_t *m, uint32_t v) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) r ^= (v >> j & 1u) ? m[j] : 0u;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__restrict__ raw, uint64_t n, uint32_t s,
+                                                             const uint32_t *__restrict__ mats,
+                                                             uint32_t *__restrict__ out, uint32_t flags) {
+    __shared__ uint32_t M[65 * 32];
+    for (uint32_t i = threadIdx.x; i < 65 * 32; i += blockDim.x) M[i] = mats[i];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = s < 64 ? s : 64, reps = s <= 64 ? 1 : s / 64;
+    const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (blockDim.x / 64);
+    for (uint64_t b = static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6); b < n; b += nw) {
+        uint32_t acc = 0;
+        if (lane < w) {
+            uint32_t rv[16];  // all loads first: one memory latency per block
+#pragma unroll
+            for (uint32_t m = 0; m < 16; ++m) rv[m] = m < reps ? raw[b * s + lane + 64 * m] : 0u;
+#pragma unroll
+            for (uint32_t m = 0; m < 16; ++m)
+                if (m < reps) acc = (m ? gf2_apply(M + 64 * 32, acc) : 0u) ^ rv[m];
+            acc = gf2_apply(M + (w - 1 - lane) * 32, acc);
+        }
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) acc ^= __shfl_xor(acc, k);
+        if (lane == 0) {
+            const uint32_t crc = ~acc;
+            out[b] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+        }
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1767,6 +1832,9 @@ struct DevCtx {
     uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
     std::mutex ws_m;  // guards the map (entries are never erased)
     std::map<hipStream_t, std::unique_ptr<StreamWs>> ws;
+    // long-block split: Shift matrices per piece length (immutable once built)
+    std::mutex mats_m;
+    std::map<uint64_t, uint32_t *> piece_mats;
     // host-path staging (grown on demand), serialised by host_m
     std::mutex host_m;
     uint8_t *d_arena = nullptr;
@@ -1882,7 +1950,7 @@ void launch_one(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *o
     uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
     if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
     if (grid == 0) grid = 1;
-    lvk::Params P;
+    lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(arena);
     P.off = off;
     P.len = len;
@@ -1944,7 +2012,7 @@ size_t sort_ws_bytes(uint64_t n) {
 // The library-owned workspace of (device, stream), grown on demand (the sort
 // needs no initialised state).  Returns with the workspace's lock held in
 // `lk`; the caller keeps it until its last launch has been enqueued.
-int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_lock<std::mutex> *lk) {
+int stream_ws_bytes(DevCtx &c, hipStream_t s, size_t need, uint8_t **out, std::unique_lock<std::mutex> *lk) {
     StreamWs *w = nullptr;
     {
         std::lock_guard<std::mutex> mk(c.ws_m);
@@ -1953,7 +2021,6 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_l
         w = slot.get();
     }
     *lk = std::unique_lock<std::mutex>(w->m);
-    const size_t need = sort_ws_bytes(n);
     if (w->cap < need) {
         if (w->p) LV_HIP(hipFree(w->p));
         w->p = nullptr;
@@ -1965,6 +2032,48 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_l
     return 0;
 }
 
+int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_lock<std::mutex> *lk) {
+    return stream_ws_bytes(c, s, sort_ws_bytes(n), out, lk);
+}
+
+// Shift_{j plen} (j < 64) and Shift_{64 plen} as 65 GF(2) matrices of 32
+// column images, on the device (combine_pieces_kernel); built once per plen.
+int piece_mats(DevCtx &c, uint64_t plen, const uint32_t **out) {
+    std::lock_guard<std::mutex> lk(c.mats_m);
+    uint32_t *&d = c.piece_mats[plen];
+    if (!d) {
+        std::vector<uint32_t> h(65 * 32);
+        const lvgpu::Gf2Mat step = lvgpu::shift_matrix(plen);
+        lvgpu::Gf2Mat m = lvgpu::shift_matrix(0);
+        for (int j = 0; j <= 64; ++j) {
+            for (int b = 0; b < 32; ++b) h[j * 32 + b] = m.col[b];
+            m = m.then(step);
+        }
+        uint32_t *p = nullptr;
+        LV_HIP(hipMalloc(&p, h.size() * 4));
+        LV_HIP(hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        d = p;
+    }
+    *out = d;
+    return 0;
+}
+
+// Long-block split of the strided API: log2 of the pieces per block, or 0.
+// A batch of few long blocks keeps only n of the grid's 16-lane groups busy
+// (one group walks a block), so blocks of >= 8 KiB are cut into 2^k pieces
+// of >= 4 KiB (whole 1 KiB batches of the G = 16 blocks kernel) until the
+// pieces fill one pass of the grid; combine_pieces_kernel joins them.
+uint32_t pick_split(uint64_t base, uint64_t stride, uint64_t blen, uint64_t n, int forced, int cus) {
+    if (forced >= 0 || base % 16 || stride % 16) return 0;
+    const uint64_t want = 4ull * static_cast<uint64_t>(cus) * lvk::kWaves;
+    uint32_t ps = 0;
+    while ((n << ps) < want && ps < 10) {
+        const uint64_t s2 = 2ull << ps;
+        if (blen % s2 || (blen / s2) % 1024 || blen / s2 < 4096) break;
+        ++ps;
+    }
+    return ps;
+}
 // Length-sorted launch of the offsets API, four kernels and no host sync:
 // per-workgroup histograms, their column scan (+ key starts), the scatter
 // into sorted entries, then the persistent class kernel.
@@ -1981,7 +2090,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
                        static_cast<uint32_t>(wgs), ws);
     hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed);
-    lvk::Params P;
+    lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(arena);
     P.off = off;
     P.len = len;
@@ -2024,7 +2133,7 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
     uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
     if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
     if (grid == 0) grid = 1;
-    lvk::Params P;
+    lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(base);
     P.off = nullptr;
     P.len = nullptr;
@@ -2137,6 +2246,37 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     const int gi = forced_gi(flags);
+    hipStream_t hs = static_cast<hipStream_t>(stream);
+    const uint32_t ps = pick_split(reinterpret_cast<uint64_t>(d_base), stride, block_len, n, gi, c->cus);
+    if (ps > 0) {
+        const uint64_t nv = static_cast<uint64_t>(n) << ps, plen = block_len >> ps;
+        const uint32_t *mats = nullptr;
+        if (int rc = piece_mats(*c, plen, &mats)) return rc;
+        uint8_t *scr = nullptr;
+        std::unique_lock<std::mutex> ws_lk;  // held through both launches
+        if (int rc = stream_ws_bytes(*c, hs, nv * 4, &scr, &ws_lk)) return rc;
+        lvk::Params P{};
+        P.base = reinterpret_cast<uint64_t>(d_base);
+        P.seed = d_seed;
+        P.out = reinterpret_cast<uint32_t *>(scr);
+        P.n = nv;
+        P.stride = stride;
+        P.blen = static_cast<uint32_t>(plen);
+        P.plen = plen;
+        P.pshift = ps;
+        const uint64_t grid = std::min<uint64_t>(c->cus, (nv + 63) / 64);
+        const uint32_t nb = static_cast<uint32_t>(plen / (16ull * 16 * lvk::U));
+        if (d_seed)
+            hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, true, true>), dim3(static_cast<uint32_t>(grid)),
+                               dim3(lvk::kThreads), 0, hs, P, nb, c->image[2]);
+        else
+            hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true>), dim3(static_cast<uint32_t>(grid)),
+                               dim3(lvk::kThreads), 0, hs, P, nb, c->image[2]);
+        hipLaunchKernelGGL(lvk::combine_pieces_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(1024, (n + 3) / 4))),
+                           dim3(256), 0, hs, P.out, static_cast<uint64_t>(n), 1u << ps, mats, d_out, flags);
+        g_kernel = "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel";
+        return check_launch();
+    }
     // Aligned whole-batch blocks take the uniform-block kernel.
     const int bgi = pick_block_gi(reinterpret_cast<uint64_t>(d_base), stride, block_len, gi, n, c->cus);
     if (bgi >= 0) {

@@ -492,3 +492,49 @@ def test_kernel_choice_query(torch_dev):
     lvgpu.batch(t, o, ln)
     assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel"
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n,blen,seeded,masked", [(1, 16 << 20, False, False), (3, 1 << 20, True, True),
+                                                  (64, 16 << 20, True, False), (1024, 65536, False, True),
+                                                  (5, 8192, True, False), (200, 12288, False, False),
+                                                  (7, 3 << 20, True, True)])
+def test_strided_long_block_split(torch_dev, n, blen, seeded, masked):
+    """Few long blocks through lv_crc32c_batch_strided: each block is cut into
+    2^k pieces that fill the grid and the piece registers are joined on the
+    device (combine_pieces_kernel) -- the reference bench's 1 MiB and 16 MiB
+    buffers (benches/crc32c.rs:59-60) and 1,024 x 64 KiB, bit-exact."""
+    torch, dev = torch_dev
+    stride = blen + (0 if n % 2 else 4096)
+    base = torch.empty(stride * n + 64, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(base, 0, 0x51D + n)
+    rng = np.random.default_rng(n)
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out = lvgpu.batch_strided(base, stride, blen, n, seed=sd, masked=masked)
+    assert lvgpu.last_kernel() == "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel"
+    got = out.cpu().numpy().view(np.uint32)
+    host = base.cpu().numpy().tobytes()
+    want = oracle_batch(host, np.arange(n, dtype=np.uint64) * stride, np.full(n, blen, np.uint32), seeds, masked)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("sizes", [[1 << 20], [16 << 20], [16 << 20, 1 << 20, 37, 0, 70001, 5 << 20]])
+def test_offsets_api_long_buffers(torch_dev, sizes):
+    """The reference bench's largest buffers (benches/crc32c.rs:59-60: 1 MiB,
+    16 MiB) through the device offsets API, alone and mixed with short ones,
+    at odd start offsets, seeded and masked."""
+    torch, dev = torch_dev
+    offs, pos = [], 3
+    for sz in sizes:
+        offs.append(pos)
+        pos += sz + 5
+    arena = torch.empty(pos + 64, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, 0xB16)
+    rng = np.random.default_rng(len(sizes))
+    seeds = rng.integers(0, 2**32, size=len(sizes), dtype=np.uint64).astype(np.uint32)
+    o = torch.tensor(offs, dtype=torch.int64, device=dev)
+    ln = torch.tensor(sizes, dtype=torch.int32, device=dev)
+    out = lvgpu.batch(arena, o, ln, torch.from_numpy(seeds.view(np.int32)).to(dev), masked=True)
+    got = out.cpu().numpy().view(np.uint32)
+    want = oracle_batch(arena.cpu().numpy().tobytes(), offs, sizes, seeds, True)
+    assert np.array_equal(got, want)
