@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--no-settle", dest="settle", action="store_false",
                    help="skip the settle phase (back-to-back launches until the idle->busy power transient "
                         "has passed; reported as `settle`, separate from --warmup)")
+    p.add_argument("--long", action="store_true",
+                   help="few long buffers through both device APIs (1,024 x 64 KiB, 64 x 16 MiB, 16 x 1 MiB, "
+                        "1 x 16 MiB); one JSON line")
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
                    help="auto: measure roofline.traffic in a child rocprofv3 --pmc FETCH_SIZE pass")
     return p.parse_args()
@@ -455,6 +458,58 @@ def sweep_bench(args):
     return res
 
 
+def long_bench(args):
+    """Few long buffers (verdict r01: intra-buffer parallelism; the reference
+    bench's 1 MiB / 16 MiB buffers, benches/crc32c.rs:59-60): 1,024 x 64 KiB,
+    64 x 16 MiB, 16 x 1 MiB and 1 x 16 MiB blocks in HBM through the strided
+    API (long-block split + device-side combine) and the offsets API.
+    HIP-event mean per call (all kernels of the call); 4 buffers of each
+    configuration checked against the oracle in the run."""
+    import numpy as np
+    import torch
+    import lvgpu
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    lvgpu.device_init()
+    L = W.lib()
+    rows = []
+    for n, bl in ((1024, 64 << 10), (64, 16 << 20), (16, 1 << 20), (1, 16 << 20)):
+        arena = torch.empty(n * bl + 64, dtype=torch.uint8, device=dev)
+        lvgpu.fill_splitmix(arena, 0, PAYLOAD_SEED)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        o = torch.arange(n, dtype=torch.int64, device=dev) * bl
+        ln = torch.full((n,), bl, dtype=torch.int32, device=dev)
+        ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
+        row = {"blocks": n, "block_bytes": bl}
+        for api, fn in (("strided", lambda: lvgpu.batch_strided(arena, bl, bl, n, out=out)),
+                        ("offsets", lambda: lvgpu.batch_ws(arena, o, ln, ws, out=out))):
+            _, avg = _event_times(torch, fn, max(20, min(args.steps, 100)), max(10, min(args.warmup, 50)))
+            fn()
+            kern = lvgpu.last_kernel()
+            torch.cuda.synchronize()
+            k = min(n, 4)
+            host = arena[:k * bl].cpu().numpy()
+            want = np.zeros(k, dtype=np.uint32)
+            ho = np.arange(k, dtype=np.uint64) * bl
+            hl = np.full(k, bl, dtype=np.uint32)
+            L.oracle_batch(host.ctypes.data, ho.ctypes.data, hl.ctypes.data, None, want.ctypes.data, k, 0)
+            if not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
+                raise SystemExit(f"long-buffer parity check failed ({api}, {n} x {bl})")
+            gbs = n * bl / (avg * 1e-3) / 1e9
+            row[api] = {"GB_per_s": round(gbs, 1), "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 4),
+                        "us_avg": round(avg * 1e3, 2), "kernels": kern}
+        rows.append(row)
+        print(json.dumps(row), file=sys.stderr, flush=True)
+        del arena, out, o, ln, ws
+    res = {"metric": "few long buffers, device-resident batched CRC32C", "unit": "GB/s", "results": rows,
+           "timing": "HIP events around each call (every kernel of the call), mean after settle + warmup",
+           "data": "synthetic splitmix64 payload in HBM"}
+    print(json.dumps(res), flush=True)
+    return res
+
+
 def table_bench(args):
     """SURVEY 8f row 3 in HBM: lv_sst_seal_blocks_device writes the
     type(1) || mask(crc32c(contents || type)) trailer of every block of a table
@@ -733,6 +788,8 @@ def main():
         return table_bench(args)
     if args.hash:
         return hash_bench(args)
+    if args.long:
+        return long_bench(args)
     import torch
     import lvgpu
     from lvgpu import shard
