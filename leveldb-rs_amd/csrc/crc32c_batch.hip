@@ -345,6 +345,8 @@ struct Params {
     uint32_t pshift;  // log2 pieces per block
     const uint4 *ent;       // optional: sorted entries {off lo, off hi, len, buffer index}
     const uint32_t *sseed;  // optional: seeds in sorted-entry order
+    uint64_t nplain;        // sorted walk: entries [nplain, n) are long-buffer pieces
+    uint32_t *part;         // piece registers (long-buffer split of the offsets API)
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of
@@ -825,10 +827,20 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     return c * kBuckets + (kBuckets - 1 - nb);
 }
 
-// Sort workspace, 16-B aligned.  Header (u32 words): [0, 256) unused;
-// [256, 264) class start x4, count x4; [264, 520) per-key totals; [520, 528)
-// unused.  Then the per-workgroup histogram matrix M[wgs][256],
-// then n sorted 16-B entries, then n seeds in entry order.
+// Sort workspace, 16-B aligned.  Header (u32 words): [0, 4) the long-buffer
+// split's piece and long-buffer counters and the batch's payload bytes (u64);
+// [4, 256) unused; [256, 264) class start x4, count x4; [264, 520) per-key
+// totals; [520, 528) unused.  Then the per-workgroup histogram matrix
+// M[wgs][256], the per-workgroup payload sums (u64), n + kPieceBudget sorted
+// 16-B entries (the pieces of split long buffers follow the n sorted ones),
+// as many seeds in entry order, kPieceBudget piece registers and
+// kPieceBudget / 2 long-buffer records {buffer, first piece, pieces, log2 piece}.
+constexpr uint32_t kWsPieces = 0;
+constexpr uint32_t kWsLongs = 1;
+constexpr uint32_t kWsBytes = 2;
+constexpr uint32_t kPieceBudget = 65536;  // piece entries per call (each split buffer takes <= kMaxPieces)
+constexpr uint32_t kMaxPieces = 256;
+constexpr uint32_t kPieceFlag = 0x80000000u;  // output slot flag of a piece entry (slot < kPieceBudget)
 constexpr uint32_t kWsCls = kKeys;
 constexpr uint32_t kWsTot = kKeys + 8;
 constexpr uint32_t kWsHeader = kWsTot + kKeys + 8;  // 528 words, 16-B multiple
@@ -872,11 +884,18 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t *h, uint32_t k, bool val
 // as row blockIdx.x of M.  No global atomics: same-address device atomics
 // from hundreds of workgroups serialize (one key for a uniform batch).
 __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__restrict__ len, uint64_t n,
-                                                          uint64_t chunk, uint32_t *__restrict__ M) {
+                                                          uint64_t chunk, uint32_t *__restrict__ M,
+                                                          uint32_t *__restrict__ ws, uint64_t *__restrict__ wgb) {
     static_assert(kSortThreads == kKeys, "one thread per key");
     __shared__ uint32_t h[kKeys];
+    __shared__ uint64_t bsum[kSortThreads / 64];
     const uint32_t t = threadIdx.x, lane = t & 63u;
     h[t] = 0;
+    if (blockIdx.x == 0 && t == 0) {  // counters of the long-buffer split (read by later launches)
+        ws[kWsPieces] = 0;
+        ws[kWsLongs] = 0;
+    }
+    uint64_t mybytes = 0;
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortChunk) {
@@ -888,12 +907,17 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__rest
         }
 #pragma unroll
         for (uint32_t e = 0; e < kSortE; ++e) {
+            mybytes += l[e];
             if (b0 + e * kSortThreads >= hi) break;  // block-uniform
             wave_count(h, sort_key(l[e]), b0 + e * kSortThreads + t < hi, lane);
         }
     }
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) mybytes += __shfl_xor(mybytes, k);
+    if (lane == 0) bsum[t >> 6] = mybytes;
     __syncthreads();
     M[static_cast<uint64_t>(blockIdx.x) * kKeys + t] = h[t];
+    if (t == 0) wgb[blockIdx.x] = bsum[0] + bsum[1] + bsum[2] + bsum[3];
 }
 
 // Pass 2: column scan of M.  Workgroup b owns keys [16b, 16b+16); thread
@@ -904,8 +928,22 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__rest
 // scatter workgroup after the kernel boundary (a device-scope release here
 // writes back the L2 and cost more than this whole pass).
 __global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__ M, uint32_t wgs,
-                                                          uint32_t *__restrict__ ws) {
+                                                          uint32_t *__restrict__ ws, const uint64_t *__restrict__ wgb) {
     __shared__ uint32_t part[64][16];
+    __shared__ uint64_t bsum[kScanThreads / 64];
+    if (blockIdx.x == 0) {  // the batch's payload bytes (sizes the long-buffer split's pieces)
+        uint64_t b = threadIdx.x < wgs ? wgb[threadIdx.x] : 0u;
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) b += __shfl_xor(b, k);
+        if ((threadIdx.x & 63u) == 0) bsum[threadIdx.x >> 6] = b;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t tot = 0;
+            for (uint32_t w = 0; w < kScanThreads / 64; ++w) tot += bsum[w];
+            ws[kWsBytes] = static_cast<uint32_t>(tot);
+            ws[kWsBytes + 1] = static_cast<uint32_t>(tot >> 32);
+        }
+    }
     const uint32_t t = threadIdx.x, kl = t & 15u, sub = t >> 4;
     const uint32_t k = blockIdx.x * 16u + kl;
     const uint32_t R = (wgs + 63u) / 64u;  // <= 16
@@ -956,13 +994,61 @@ __device__ __forceinline__ uint32_t key_starts(const uint32_t *ws, uint32_t *sc)
 // reads and CRC stores within one 4096-buffer window).  Entries carry
 // off/len/index so the CRC kernel reads one 16-B record per buffer; seeds are
 // permuted alongside.
+// Long-buffer split of the offsets API (verdict r01: a batch of a few long
+// buffers left most of the grid idle, one 16-lane group walking each).  A
+// buffer longer than the larger of 16 KiB and twice its piece length is cut
+// into m <= kMaxPieces pieces of P = 2^p bytes, aligned to its END (piece 0
+// holds the ragged rest), with P the smallest power of two >= 4 KiB, >=
+// L / kMaxPieces and >= (payload bytes of the batch) / 16,384 (one pass of
+// the grid's 16-lane groups): buffers that are long relative to the batch
+// are split, C2/C4-sized ones are not.  The pieces go after the n sorted
+// entries (claimed with a device counter, at most kPieceBudget per call;
+// a buffer that does not fit stays whole), the walk stores their raw
+// registers, and combine_long_kernel joins them.  The buffer's own sorted
+// entry becomes an empty one with no output.
+__device__ __forceinline__ uint32_t ceil_log2(uint64_t x) {
+    return x <= 1 ? 0u : 64u - static_cast<uint32_t>(__clzll(static_cast<long long>(x - 1)));
+}
+
+__device__ __forceinline__ bool split_long(uint64_t o, uint32_t L, uint32_t s, uint32_t i, uint64_t n,
+                                           uint64_t total, uint32_t *__restrict__ ws, uint4 *__restrict__ ent,
+                                           uint32_t *__restrict__ sseed, bool seeded, uint4 *__restrict__ longs) {
+    if (!longs || L <= 16384u) return false;  // (no split list: splitting is off for this call)
+    uint32_t p = ceil_log2(total / 16384u);
+    const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + kMaxPieces - 1) / kMaxPieces);
+    p = p > pl ? p : pl;
+    p = p > 12u ? p : 12u;
+    const uint64_t P = 1ull << p;
+    if (L <= 2 * P) return false;
+    const uint32_t m = static_cast<uint32_t>((L + P - 1) >> p);
+    const uint32_t base = atomicAdd(&ws[kWsPieces], m);
+    if (base + static_cast<uint64_t>(m) > kPieceBudget) {  // over budget: blank the claimed slots in range
+        for (uint32_t k = base; k < kPieceBudget && k < base + m; ++k) ent[n + k] = make_uint4(0, 0, 0, 0xffffffffu);
+        return false;
+    }
+    const uint32_t li = atomicAdd(&ws[kWsLongs], 1u);
+    longs[li] = make_uint4(i, base, m, p);
+    const uint64_t first = L - (static_cast<uint64_t>(m) - 1) * P;  // piece 0: [0, first)
+    for (uint32_t k = 0; k < m; ++k) {
+        const uint64_t st = k ? first + (k - 1) * P : 0;
+        const uint64_t a = o + st;
+        // every piece is walked like a seed-0 buffer except piece 0, which
+        // takes the buffer's seed: piece k > 0 yields R(~0, piece), and
+        // combine_long_kernel removes the constant Shift_P(~0)
+        ent[n + base + k] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                       static_cast<uint32_t>(k ? P : first), (base + k) | kPieceFlag);
+        if (seeded) sseed[n + base + k] = k ? 0u : s;
+    }
+    return true;
+}
+
 __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__restrict__ off,
                                                              const uint32_t *__restrict__ len, uint64_t n,
                                                              uint64_t chunk, uint32_t *__restrict__ ws,
                                                              const uint32_t *__restrict__ M,
                                                              uint4 *__restrict__ ent,
                                                              const uint32_t *__restrict__ seed,
-                                                             uint32_t *__restrict__ sseed) {
+                                                             uint32_t *__restrict__ sseed, uint4 *__restrict__ longs) {
     __shared__ uint32_t cur[kKeys];
     __shared__ uint32_t sc[kKeys];
     const uint32_t t = threadIdx.x, lane = t & 63u;
@@ -975,6 +1061,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
         ws[kWsCls + 4 + c] = sc[t + kBuckets - 1] - ks;
     }
     __syncthreads();
+    const uint64_t total = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortChunk) {
         uint32_t lb[kSortE];
@@ -993,9 +1080,13 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
             const bool valid = i < hi;
             const uint32_t pos = wave_claim(cur, sort_key(lb[e]), valid, lane);
             if (valid) {
-                ent[pos] = make_uint4(static_cast<uint32_t>(ob[e]), static_cast<uint32_t>(ob[e] >> 32), lb[e],
-                                      static_cast<uint32_t>(i));
-                if (seed) sseed[pos] = seed[i];
+                const uint32_t sd = seed ? seed[i] : 0u;
+                const bool split = split_long(ob[e], lb[e], sd, static_cast<uint32_t>(i), n, total, ws, ent, sseed,
+                                              seed != nullptr, longs);
+                // a split buffer's own entry: empty, no output (combine_long_kernel stores it)
+                ent[pos] = make_uint4(static_cast<uint32_t>(ob[e]), static_cast<uint32_t>(ob[e] >> 32),
+                                      split ? 0u : lb[e], split ? 0xffffffffu : static_cast<uint32_t>(i));
+                if (seed) sseed[pos] = sd;
             }
         }
     }
@@ -1361,14 +1452,23 @@ struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const { return load_rgeo<SEEDED>(P, e); }
     __device__ __forceinline__ uint2 trailer(const RGeo &, uint32_t) const { return make_uint2(0, 0); }
+    // A piece parks its raw register for combine_long_kernel; its output slot
+    // is its piece slot with the top bit set (piece slots are < kPieceBudget,
+    // and a list with pieces has buffer indices < 2^31: launch_binned).
     __device__ __forceinline__ void stage(const Params &P, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
                                           uint2) const {
+        const bool piece = P.nplain < P.n && q.bid != 0xffffffffu && (q.bid & kPieceFlag);
         g_oidx[wave][slot] = q.bid;
-        g_ocrc[wave][slot] = final_crc(P, X);
+        g_ocrc[wave][slot] = piece ? X : final_crc(P, X);
     }
     __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
         const uint32_t bi = g_oidx[wave][lane], cv = g_ocrc[wave][lane];
-        if (lane < nslots && bi != 0xffffffffu) P.out[bi] = cv;
+        if (lane >= nslots || bi == 0xffffffffu) return;
+        // piece slots (flagged in the entry) occur only in the pieces' sub-list (P.nplain < P.n)
+        if (P.nplain < P.n && (bi & kPieceFlag))
+            P.part[bi & ~kPieceFlag] = cv;
+        else
+            P.out[bi] = cv;
     }
 };
 
@@ -1495,12 +1595,15 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     }
 }
 
-// The sorted sub-list [start, start+count).
-__device__ __forceinline__ Params sub_list(const Params &P0, uint32_t start, uint32_t count) {
+// The sorted sub-list [start, start+count) followed by `pieces` piece
+// entries (the long-buffer split; they sit right after the n sorted entries,
+// i.e. after the last class).
+__device__ __forceinline__ Params sub_list(const Params &P0, uint32_t start, uint32_t count, uint32_t pieces = 0) {
     Params P = P0;
     P.ent = P0.ent + start;
     P.sseed = P0.sseed ? P0.sseed + start : nullptr;
-    P.n = count;
+    P.n = static_cast<uint64_t>(count) + pieces;
+    P.nplain = count;
     return P;
 }
 
@@ -1545,6 +1648,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t grid = gridDim.x;
     const uint32_t n23 = cls[6] + cls[7];
+    // pieces of split long buffers (walked after classes 2+3; every split
+    // buffer is class 3, so n23 > 0 whenever there are pieces)
+    const uint32_t np = P.part ? min(ws[kWsPieces], kPieceBudget) : 0u;
     // With no large buffers at all, every wave walks the small classes.
 #if LVK_SMALL_ALL
     const uint32_t nsmall = n23 ? kSmallWaves : kWaves;
@@ -1567,7 +1673,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
             if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
             return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
         };
-        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23), SortedList<SEEDED>(), lane, L, pool(), pool);
+        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), SortedList<SEEDED>(), lane, L, pool(),
+                          pool);
     }
 }
 
@@ -1732,6 +1839,61 @@ __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__r
     }
 }
 
+// Joins the pieces of the offsets API's split long buffers (sort_scatter,
+// split_long): long record {buffer, first piece slot, m, p}, pieces of
+// P = 2^p bytes aligned to the buffer end; piece 0's register is
+// R_0 = R(~seed, piece 0) and piece k > 0 was walked as a seed-0 buffer,
+// part = R(~0, piece k) = R(0, piece k) ^ Shift_P(~0) (the seed trick), so
+// R_k = part ^ Shift_P(~0) and R(~seed, buffer) = XOR_k Shift_{(m-1-k) P}(R_k).  One wave
+// per buffer: lane l < 64 runs Horner over pieces k = l + 64 j with
+// Shift_{64 P} = Shift_{2^(p+6)}, then shifts by (m - 1 - k_last) P through
+// the base matrices Shift_{2^(p+b)} of its set bits b; an xor over the wave.
+// base: Shift_{2^i} bytes, i < kBaseMats, as GF(2) matrices (32 columns).
+constexpr uint32_t kBaseMats = 48;
+__global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__restrict__ ws,
+                                                           const uint4 *__restrict__ longs,
+                                                           const uint32_t *__restrict__ part,
+                                                           const uint32_t *__restrict__ base,
+                                                           uint32_t *__restrict__ out, uint32_t flags) {
+    __shared__ uint32_t M[kBaseMats * 32];
+    const uint32_t nl = ws[kWsLongs];
+    if (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64) >= nl) return;  // block-uniform
+    for (uint32_t i = threadIdx.x; i < kBaseMats * 32; i += blockDim.x) M[i] = base[i];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * (blockDim.x / 64);
+    for (uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < nl; w += nw) {
+        const uint4 r = longs[w];  // {buffer, first, m, p}
+        uint32_t acc = 0;
+        if (lane < r.z) {
+            uint32_t rv[4];  // m <= kMaxPieces = 256: <= 4 pieces per lane, loads first
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) rv[j] = lane + 64 * j < r.z ? part[r.y + lane + 64 * j] : 0u;
+            const uint32_t c = gf2_apply(M + r.w * 32, 0xffffffffu);  // Shift_P(~0)
+            rv[0] ^= lane ? c : 0u;
+#pragma unroll
+            for (uint32_t j = 1; j < 4; ++j) rv[j] ^= c;
+            uint32_t klast = lane;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (lane + 64 * j < r.z) {
+                    acc = (j ? gf2_apply(M + (r.w + 6) * 32, acc) : 0u) ^ rv[j];
+                    klast = lane + 64 * j;
+                }
+            const uint32_t d = r.z - 1 - klast;  // < 64
+#pragma unroll
+            for (uint32_t b = 0; b < 6; ++b)
+                if (d >> b & 1u) acc = gf2_apply(M + (r.w + b) * 32, acc);
+        }
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) acc ^= __shfl_xor(acc, k);
+        if (lane == 0) {
+            const uint32_t crc = ~acc;
+            out[r.x] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+        }
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1830,6 +1992,7 @@ struct DevCtx {
     bool ready = false;
     int cus = 0;
     uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t *base_mats = nullptr;  // Shift_{2^i}, i < lvk::kBaseMats (combine_long_kernel)
     std::mutex ws_m;  // guards the map (entries are never erased)
     std::map<hipStream_t, std::unique_ptr<StreamWs>> ws;
     // long-block split: Shift matrices per piece length (immutable once built)
@@ -1922,6 +2085,16 @@ int current_ctx(DevCtx **out) {
             LV_HIP(hipMalloc(&c.image[i], im.size() * 4));
             LV_HIP(hipMemcpy(c.image[i], im.data(), im.size() * 4, hipMemcpyHostToDevice));
         }
+        {
+            std::vector<uint32_t> bm(lvk::kBaseMats * 32);
+            lvgpu::Gf2Mat m = lvgpu::shift_matrix(1);
+            for (uint32_t i = 0; i < lvk::kBaseMats; ++i) {
+                for (int j = 0; j < 32; ++j) bm[i * 32 + j] = m.col[j];
+                m = m.then(m);  // Shift_{2^(i+1)}
+            }
+            LV_HIP(hipMalloc(&c.base_mats, bm.size() * 4));
+            LV_HIP(hipMemcpy(c.base_mats, bm.data(), bm.size() * 4, hipMemcpyHostToDevice));
+        }
         c.ready = true;
     }
     *out = &c;
@@ -2002,12 +2175,29 @@ uint64_t sort_wgs(uint64_t n, uint64_t *chunk) {
 
 // Bytes of sort workspace the offsets API needs for n buffers: header,
 // histogram matrix, n sorted 16-B entries, then n seeds in entry order.
-size_t sort_ws_bytes(uint64_t n) {
+// Byte offsets of the workspace regions (layout in lvk, "Sort workspace").
+struct WsLayout {
+    size_t m, wgb, ent, sseed, part, longs, total;
+};
+
+constexpr size_t al16(size_t x) { return (x + 15) & ~static_cast<size_t>(15); }
+
+WsLayout ws_layout(uint64_t n) {
     uint64_t chunk = 0;
     const uint64_t wgs = sort_wgs(n, &chunk);
-    return lvk::kWsHeader * sizeof(uint32_t) + wgs * lvk::kKeys * sizeof(uint32_t) +
-           n * (sizeof(uint4) + sizeof(uint32_t));
+    const uint64_t ne = n + lvk::kPieceBudget;
+    WsLayout w;
+    w.m = lvk::kWsHeader * sizeof(uint32_t);
+    w.wgb = w.m + al16(wgs * lvk::kKeys * sizeof(uint32_t));
+    w.ent = w.wgb + al16(wgs * sizeof(uint64_t));
+    w.sseed = w.ent + ne * sizeof(uint4);
+    w.part = w.sseed + al16(ne * sizeof(uint32_t));
+    w.longs = w.part + al16(lvk::kPieceBudget * sizeof(uint32_t));
+    w.total = w.longs + (lvk::kPieceBudget / 2) * sizeof(uint4);
+    return w;
 }
+
+size_t sort_ws_bytes(uint64_t n) { return ws_layout(n).total; }
 
 // The library-owned workspace of (device, stream), grown on demand (the sort
 // needs no initialised state).  Returns with the workspace's lock held in
@@ -2082,14 +2272,20 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     uint32_t *ws = reinterpret_cast<uint32_t *>(ws_bytes);
     uint64_t chunk = 0;
     const uint64_t wgs = sort_wgs(n, &chunk);
-    uint32_t *M = ws + lvk::kWsHeader;
-    uint4 *ent = reinterpret_cast<uint4 *>(M + wgs * lvk::kKeys);
-    uint32_t *sseed = reinterpret_cast<uint32_t *>(ent + n);
+    const WsLayout lay = ws_layout(n);
+    uint32_t *M = reinterpret_cast<uint32_t *>(ws_bytes + lay.m);
+    uint64_t *wgb = reinterpret_cast<uint64_t *>(ws_bytes + lay.wgb);
+    uint4 *ent = reinterpret_cast<uint4 *>(ws_bytes + lay.ent);
+    uint32_t *sseed = reinterpret_cast<uint32_t *>(ws_bytes + lay.sseed);
+    uint32_t *part = reinterpret_cast<uint32_t *>(ws_bytes + lay.part);
+    // long-buffer split (sort_scatter / combine_long_kernel); off for batches
+    // whose buffer indices reach the piece flag bit
+    uint4 *longs = n < lvk::kPieceFlag ? reinterpret_cast<uint4 *>(ws_bytes + lay.longs) : nullptr;
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
-    hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M);
+    hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M, ws, wgb);
     hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
-                       static_cast<uint32_t>(wgs), ws);
-    hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed);
+                       static_cast<uint32_t>(wgs), ws, wgb);
+    hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed, longs);
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(arena);
     P.off = off;
@@ -2102,6 +2298,8 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     P.flags = flags;
     P.ent = ent;
     P.sseed = seed ? sseed : nullptr;
+    P.nplain = n;
+    P.part = longs ? part : nullptr;
     g_kernel = "sort+crc32c_classes_kernel";
     if (seed)
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<true>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0,
@@ -2109,6 +2307,10 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     else
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<false>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads),
                            0, s, P, c.image[2], ws);
+    // joins split long buffers (exits at once when the sort split none)
+    if (longs)
+        hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(64), dim3(256), 0, s, ws, longs, part, c.base_mats, out,
+                           flags);
     return 0;
 }
 
