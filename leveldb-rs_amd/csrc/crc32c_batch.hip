@@ -1018,6 +1018,7 @@ __device__ __forceinline__ bool split_long(uint64_t o, uint32_t L, uint32_t s, u
     const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + kMaxPieces - 1) / kMaxPieces);
     p = p > pl ? p : pl;
     p = p > 12u ? p : 12u;
+    p = p < 24u ? p : 24u;  // L < 2^32: 16 MiB pieces keep m <= 256 (and base matrices < kBaseMats)
     const uint64_t P = 1ull << p;
     if (L <= 2 * P) return false;
     const uint32_t m = static_cast<uint32_t>((L + P - 1) >> p);
