@@ -839,7 +839,7 @@ constexpr uint32_t kWsPieces = 0;
 constexpr uint32_t kWsLongs = 1;
 constexpr uint32_t kWsBytes = 2;
 constexpr uint32_t kPieceBudget = 65536;  // piece entries per call (each split buffer takes <= kMaxPieces)
-constexpr uint32_t kMaxPieces = 256;
+constexpr uint32_t kMaxPieces = 1024;
 constexpr uint32_t kPieceFlag = 0x80000000u;  // output slot flag of a piece entry (slot < kPieceBudget)
 constexpr uint32_t kWsCls = kKeys;
 constexpr uint32_t kWsTot = kKeys + 8;
@@ -1010,37 +1010,74 @@ __device__ __forceinline__ uint32_t ceil_log2(uint64_t x) {
     return x <= 1 ? 0u : 64u - static_cast<uint32_t>(__clzll(static_cast<long long>(x - 1)));
 }
 
-__device__ __forceinline__ bool split_long(uint64_t o, uint32_t L, uint32_t s, uint32_t i, uint64_t n,
+// Called by every lane of a wave (valid: the lane holds buffer i).  Counter
+// claims are wave-aggregated (one device atomic per wave and counter: the
+// same-address atomics of one per buffer serialized, ~40 us for 1,024
+// buffers) and each split buffer's pieces are written by the whole wave.
+// Returns true on lanes whose buffer was split.
+__device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, uint32_t s, uint32_t i, uint64_t n,
                                            uint64_t total, uint32_t *__restrict__ ws, uint4 *__restrict__ ent,
-                                           uint32_t *__restrict__ sseed, bool seeded, uint4 *__restrict__ longs) {
-    if (!longs || L <= 16384u) return false;  // (no split list: splitting is off for this call)
-    uint32_t p = ceil_log2(total / 16384u);
-    const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + kMaxPieces - 1) / kMaxPieces);
-    p = p > pl ? p : pl;
-    p = p > 12u ? p : 12u;
-    p = p < 24u ? p : 24u;  // L < 2^32: 16 MiB pieces keep m <= 256 (and base matrices < kBaseMats)
-    const uint64_t P = 1ull << p;
-    if (L <= 2 * P) return false;
-    const uint32_t m = static_cast<uint32_t>((L + P - 1) >> p);
-    const uint32_t base = atomicAdd(&ws[kWsPieces], m);
-    if (base + static_cast<uint64_t>(m) > kPieceBudget) {  // over budget: blank the claimed slots in range
-        for (uint32_t k = base; k < kPieceBudget && k < base + m; ++k) ent[n + k] = make_uint4(0, 0, 0, 0xffffffffu);
-        return false;
+                                           uint32_t *__restrict__ sseed, bool seeded, uint4 *__restrict__ longs,
+                                           uint32_t lane) {
+    if (!longs) return false;  // splitting is off for this call (wave-uniform)
+    uint32_t m = 0, p = 0;
+    if (valid && L > 16384u) {
+        p = ceil_log2(total / 16384u);
+        const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + kMaxPieces - 1) / kMaxPieces);
+        p = p > pl ? p : pl;
+        p = p > 12u ? p : 12u;
+        p = p < 22u ? p : 22u;  // L < 2^32: 4 MiB pieces keep m <= 1024 (and base matrices < kBaseMats)
+        if (L > (2ull << p)) m = static_cast<uint32_t>((L + (1ull << p) - 1) >> p);
     }
-    const uint32_t li = atomicAdd(&ws[kWsLongs], 1u);
-    longs[li] = make_uint4(i, base, m, p);
-    const uint64_t first = L - (static_cast<uint64_t>(m) - 1) * P;  // piece 0: [0, first)
-    for (uint32_t k = 0; k < m; ++k) {
-        const uint64_t st = k ? first + (k - 1) * P : 0;
-        const uint64_t a = o + st;
-        // every piece is walked like a seed-0 buffer except piece 0, which
-        // takes the buffer's seed: piece k > 0 yields R(~0, piece), and
-        // combine_long_kernel removes the constant Shift_P(~0)
-        ent[n + base + k] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
-                                       static_cast<uint32_t>(k ? P : first), (base + k) | kPieceFlag);
-        if (seeded) sseed[n + base + k] = k ? 0u : s;
+    const uint64_t want = __ballot(m > 0);
+    if (!want) return false;  // wave-uniform
+    uint32_t incl = m;  // inclusive prefix of m over the wave
+#pragma unroll
+    for (uint32_t k = 1; k < 64; k <<= 1) {
+        const uint32_t t = __shfl_up(incl, k);
+        if (lane >= k) incl += t;
     }
-    return true;
+    const uint32_t tot = __shfl(incl, 63);
+    const uint32_t nlong = static_cast<uint32_t>(__popcll(want));
+    uint32_t pb = 0, lb = 0;
+    if (lane == 0) {
+        pb = atomicAdd(&ws[kWsPieces], tot);
+        lb = atomicAdd(&ws[kWsLongs], nlong);
+    }
+    pb = __shfl(pb, 0);
+    lb = __shfl(lb, 0);
+    const uint32_t base = pb + incl - m;
+    const bool fits = m > 0 && static_cast<uint64_t>(base) + m <= kPieceBudget;
+    if (m > 0) {  // long record (m = 0 if over budget: combine_long_kernel skips it)
+        const uint32_t li = lb + static_cast<uint32_t>(__popcll(want & ((1ull << lane) - 1ull)));
+        longs[li] = make_uint4(i, base, fits ? m : 0u, p);
+    }
+    // the wave writes every claimed buffer's piece entries (or blanks for
+    // claims past the budget, so every slot below min(counter, budget) is set)
+    for (uint64_t todo = want; todo; todo &= todo - 1) {
+        const int j = __ffsll(static_cast<long long>(todo)) - 1;
+        const uint32_t mj = __shfl(m, j), bj = __shfl(base, j), pj = __shfl(p, j), Lj = __shfl(L, j),
+                       sj = __shfl(s, j);
+        const uint64_t oj = __shfl(o, j);
+        const bool fj = static_cast<uint64_t>(bj) + mj <= kPieceBudget;
+        const uint64_t P = 1ull << pj;
+        const uint64_t first = Lj - (static_cast<uint64_t>(mj) - 1) * P;  // piece 0: [0, first)
+        for (uint32_t k = lane; k < mj; k += 64) {
+            const uint32_t slot = bj + k;
+            if (fj) {
+                // every piece is walked like a seed-0 buffer except piece 0,
+                // which takes the buffer's seed: piece k > 0 yields R(~0, piece)
+                // and combine_long_kernel removes the constant Shift_P(~0)
+                const uint64_t a = oj + (k ? first + (k - 1) * P : 0);
+                ent[n + slot] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                           static_cast<uint32_t>(k ? P : first), slot | kPieceFlag);
+                if (seeded) sseed[n + slot] = k ? 0u : sj;
+            } else if (slot < kPieceBudget) {
+                ent[n + slot] = make_uint4(0, 0, 0, 0xffffffffu);
+            }
+        }
+    }
+    return fits;
 }
 
 __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__restrict__ off,
@@ -1080,10 +1117,10 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
             const uint64_t i = r0 + t;
             const bool valid = i < hi;
             const uint32_t pos = wave_claim(cur, sort_key(lb[e]), valid, lane);
+            const uint32_t sd = (seed && valid) ? seed[i] : 0u;
+            const bool split = split_wave(valid, ob[e], lb[e], sd, static_cast<uint32_t>(i), n, total, ws, ent, sseed,
+                                          seed != nullptr, longs, lane);
             if (valid) {
-                const uint32_t sd = seed ? seed[i] : 0u;
-                const bool split = split_long(ob[e], lb[e], sd, static_cast<uint32_t>(i), n, total, ws, ent, sseed,
-                                              seed != nullptr, longs);
                 // a split buffer's own entry: empty, no output (combine_long_kernel stores it)
                 ent[pos] = make_uint4(static_cast<uint32_t>(ob[e]), static_cast<uint32_t>(ob[e] >> 32),
                                       split ? 0u : lb[e], split ? 0xffffffffu : static_cast<uint32_t>(i));
@@ -1841,7 +1878,7 @@ __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__r
 }
 
 // Joins the pieces of the offsets API's split long buffers (sort_scatter,
-// split_long): long record {buffer, first piece slot, m, p}, pieces of
+// split_wave): long record {buffer, first piece slot, m, p}, pieces of
 // P = 2^p bytes aligned to the buffer end; piece 0's register is
 // R_0 = R(~seed, piece 0) and piece k > 0 was walked as a seed-0 buffer,
 // part = R(~0, piece k) = R(0, piece k) ^ Shift_P(~0) (the seed trick), so
@@ -1865,18 +1902,20 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
     for (uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < nl; w += nw) {
         const uint4 r = longs[w];  // {buffer, first, m, p}
+        if (r.z == 0) continue;    // a claim past the piece budget: the buffer was walked whole
         uint32_t acc = 0;
         if (lane < r.z) {
-            uint32_t rv[4];  // m <= kMaxPieces = 256: <= 4 pieces per lane, loads first
+            constexpr uint32_t kJ = kMaxPieces / 64;  // pieces per lane, loads first
+            uint32_t rv[kJ];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) rv[j] = lane + 64 * j < r.z ? part[r.y + lane + 64 * j] : 0u;
+            for (uint32_t j = 0; j < kJ; ++j) rv[j] = lane + 64 * j < r.z ? part[r.y + lane + 64 * j] : 0u;
             const uint32_t c = gf2_apply(M + r.w * 32, 0xffffffffu);  // Shift_P(~0)
             rv[0] ^= lane ? c : 0u;
 #pragma unroll
-            for (uint32_t j = 1; j < 4; ++j) rv[j] ^= c;
+            for (uint32_t j = 1; j < kJ; ++j) rv[j] ^= c;
             uint32_t klast = lane;
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j)
+            for (uint32_t j = 0; j < kJ; ++j)
                 if (lane + 64 * j < r.z) {
                     acc = (j ? gf2_apply(M + (r.w + 6) * 32, acc) : 0u) ^ rv[j];
                     klast = lane + 64 * j;
