@@ -39,6 +39,17 @@ typedef struct lv_wal_scan lv_wal_scan;
  * the GPU, CRCs every record and copies the results back.  Returns NULL on
  * error (lv_last_error()).  Records are in log order. */
 lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int device);
+/* Device-resident scan of a log already in HBM (8-byte aligned), with no
+ * host synchronisation: every 32 KiB block's header chain is walked inside
+ * the length sort's passes and every [type || payload] unit is checksummed,
+ * four kernel launches on `stream`.  Records go to d_hdr_off / d_crc /
+ * d_info in log order (the lv_wal_scan arrays below), at most `cap` of them;
+ * *d_count (device memory) receives the number of records.  If that number
+ * exceeds cap, nothing else is written: call again with a larger capacity.
+ * d_workspace: >= lv_wal_scan_workspace_bytes(bytes, cap) bytes, 16-B aligned. */
+size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap);
+int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
+                       size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream);
 /* Number of physical records reached by the blocks' header chains. */
 size_t lv_wal_scan_count(const lv_wal_scan *scan);
 /* Header offsets (ascending), value([type||payload]) (0 unless status OK),

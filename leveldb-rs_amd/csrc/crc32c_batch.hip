@@ -48,6 +48,7 @@
 
 #include "../../include/lvgpu/crc32c.h"
 #include "../../include/lvgpu/table.h"
+#include "../../include/lvgpu/wal.h"
 #include "crc32c_gf2.h"
 #include "lv_internal.h"
 
@@ -1010,6 +1011,11 @@ __device__ __forceinline__ uint32_t ceil_log2(uint64_t x) {
     return x <= 1 ? 0u : 64u - static_cast<uint32_t>(__clzll(static_cast<long long>(x - 1)));
 }
 
+// Per-wave staging of the claiming lanes' geometry (sort_scatter's 4 waves).
+__shared__ uint4 g_split[kSortThreads / 64][64];     // {offset lo, hi, length, seed}
+__shared__ uint32_t g_split_pre[kSortThreads / 64][64];  // inclusive prefix of the piece counts
+__shared__ uint32_t g_split_p[kSortThreads / 64][64];    // log2 piece length
+
 // Called by every lane of a wave (valid: the lane holds buffer i).  Counter
 // claims are wave-aggregated (one device atomic per wave and counter: the
 // same-address atomics of one per buffer serialized, ~40 us for 1,024
@@ -1053,30 +1059,41 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
         longs[li] = make_uint4(i, base, fits ? m : 0u, p);
     }
     // the wave writes every claimed buffer's piece entries (or blanks for
-    // claims past the budget, so every slot below min(counter, budget) is set)
-    for (uint64_t todo = want; todo; todo &= todo - 1) {
-        const int j = __ffsll(static_cast<long long>(todo)) - 1;
-        const uint32_t mj = __shfl(m, j), bj = __shfl(base, j), pj = __shfl(p, j), Lj = __shfl(L, j),
-                       sj = __shfl(s, j);
-        const uint64_t oj = __shfl(o, j);
-        const bool fj = static_cast<uint64_t>(bj) + mj <= kPieceBudget;
-        const uint64_t P = 1ull << pj;
-        const uint64_t first = Lj - (static_cast<uint64_t>(mj) - 1) * P;  // piece 0: [0, first)
-        for (uint32_t k = lane; k < mj; k += 64) {
-            const uint32_t slot = bj + k;
-            if (fj) {
-                // every piece is walked like a seed-0 buffer except piece 0,
-                // which takes the buffer's seed: piece k > 0 yields R(~0, piece)
-                // and combine_long_kernel removes the constant Shift_P(~0)
-                const uint64_t a = oj + (k ? first + (k - 1) * P : 0);
-                ent[n + slot] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
-                                           static_cast<uint32_t>(k ? P : first), slot | kPieceFlag);
-                if (seeded) sseed[n + slot] = k ? 0u : sj;
-            } else if (slot < kPieceBudget) {
-                ent[n + slot] = make_uint4(0, 0, 0, 0xffffffffu);
-            }
+    // claims past the budget, so every slot below min(counter, budget) is
+    // set), lane-parallel over the wave's pieces: the claiming lanes park
+    // their geometry in LDS and each slot finds its buffer by a binary search
+    // over the wave's inclusive prefix (a loop over the buffers with
+    // broadcasts ran ~75 us for 1,024 split buffers)
+    const uint32_t w = threadIdx.x >> 6;
+    g_split[w][lane] = make_uint4(static_cast<uint32_t>(o), static_cast<uint32_t>(o >> 32), L, s);
+    g_split_pre[w][lane] = incl;
+    g_split_p[w][lane] = p;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t u = lane; u < tot; u += 64) {
+        uint32_t j = 0;  // first lane with incl > u
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1)
+            if (g_split_pre[w][j + st - 1] <= u) j += st;
+        const uint32_t mj = g_split_pre[w][j] - (j ? g_split_pre[w][j - 1] : 0u);
+        const uint32_t k = u - (g_split_pre[w][j] - mj);  // piece index within buffer j
+        const uint32_t slot = pb + u;
+        const bool fj = static_cast<uint64_t>(pb) + g_split_pre[w][j] <= kPieceBudget;
+        if (fj) {
+            const uint4 gj = g_split[w][j];
+            const uint64_t P = 1ull << g_split_p[w][j];
+            const uint64_t first = gj.z - (static_cast<uint64_t>(mj) - 1) * P;  // piece 0: [0, first)
+            // every piece is walked like a seed-0 buffer except piece 0,
+            // which takes the buffer's seed: piece k > 0 yields R(~0, piece)
+            // and combine_long_kernel removes the constant Shift_P(~0)
+            const uint64_t a = ((static_cast<uint64_t>(gj.y) << 32) | gj.x) + (k ? first + (k - 1) * P : 0);
+            ent[n + slot] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                       static_cast<uint32_t>(k ? P : first), slot | kPieceFlag);
+            if (seeded) sseed[n + slot] = k ? 0u : gj.w;
+        } else if (slot < kPieceBudget) {
+            ent[n + slot] = make_uint4(0, 0, 0, 0xffffffffu);
         }
     }
+    __builtin_amdgcn_wave_barrier();
     return fits;
 }
 
@@ -1125,6 +1142,175 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
                 ent[pos] = make_uint4(static_cast<uint32_t>(ob[e]), static_cast<uint32_t>(ob[e] >> 32),
                                       split ? 0u : lb[e], split ? 0xffffffffu : static_cast<uint32_t>(i));
                 if (seed) sseed[pos] = sd;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// WAL scan with the framing fused into the sort passes (the
+// reader side, log_reader.rs:271-364).  Records never straddle a 32 KiB block
+// (log_writer.rs:67-80), so every block's header chain can be walked on its
+// own, exactly as read_physical_record frames it (log_reader.rs:271-331):
+// stop when fewer than HEADER_SIZE bytes remain, at a length that overruns
+// the block (BAD_LENGTH) or at a ZERO/0 header (ZERO).  wal_hist walks each
+// block (one thread per block) and counts the records' CRC units
+// [type || payload] (log_reader.rs:336) into the length-sort histogram, plus
+// the records per block; sort_scan is shared; wal_scatter walks the chains
+// again and writes every record straight into its sorted slot, plus its log-
+// order header offset and info word.  The class kernel then checksums the
+// units.  Four launches, no host synchronisation (round 1: count pass, hipCUB
+// scan, host readback of the total, emit pass, then the whole offsets API).
+constexpr uint32_t kWalBlock = 32768;  // log_format.rs:63
+constexpr uint32_t kWalHeader = 7;     // log_format.rs:66
+
+// The 7 header bytes at pos as the low 56 bits (log 8-B aligned): aligned
+// words, each read only if it holds a byte of the log (an aligned word never
+// crosses a page), and a funnel shift.
+__device__ __forceinline__ uint64_t wal_load8(const uint8_t *log, uint64_t size, uint64_t pos) {
+    const uint64_t a = pos & ~7ull;
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(log + a);
+    const uint64_t lo = a < size ? w[0] : 0ull;
+    const uint32_t sh = static_cast<uint32_t>(pos & 7u) * 8u;
+    if (!sh) return lo;
+    const uint64_t hi = a + 8 < size ? w[1] : 0ull;
+    return (lo >> sh) | (hi << (64u - sh));
+}
+
+// One step of a block's header chain: the record at pos (status, unit
+// length) and the position after it; `more` says whether another header fits.
+struct WalRec {
+    uint32_t len, type, status, ulen;
+};
+
+__device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, uint64_t start, uint32_t blen,
+                                             uint32_t pos) {
+    const uint64_t h = wal_load8(log, size, start + pos);  // crc(4) | length(2) | type(1)
+    WalRec r;
+    r.len = static_cast<uint32_t>(h >> 32) & 0xffffu;
+    r.type = static_cast<uint32_t>(h >> 48) & 0xffu;
+    r.status = LV_WAL_REC_OK;
+    if (kWalHeader + r.len > blen - pos)
+        r.status = LV_WAL_REC_BAD_LENGTH;  // log_reader.rs:312-324
+    else if (r.type == 0 && r.len == 0)
+        r.status = LV_WAL_REC_ZERO;        // log_reader.rs:326-331
+    r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
+    return r;
+}
+
+__global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
+                                                         uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ M,
+                                                         uint64_t *__restrict__ wgrec, uint32_t *__restrict__ blkcnt) {
+    __shared__ uint32_t h[kKeys];
+    __shared__ uint64_t wsum[kSortThreads / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    h[t] = 0;
+    __syncthreads();
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
+    uint64_t mine = 0;
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
+        const uint64_t b = b0 + t;
+        const uint64_t start = b * kWalBlock;
+        const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
+        uint32_t pos = 0, cnt = 0;
+        bool active = blen >= kWalHeader;
+        while (__any(active)) {  // wave-uniform: the longest chain of the wave
+            uint32_t key = 0;
+            const bool rec = active;
+            if (active) {
+                const WalRec r = wal_record(log, size, start, blen, pos);
+                key = sort_key(r.ulen);
+                ++cnt;
+                pos += kWalHeader + r.len;
+                active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
+            }
+            wave_count(h, key, rec, lane);
+        }
+        if (b < hi) blkcnt[b] = cnt;
+        mine += cnt;
+    }
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) mine += __shfl_xor(mine, k);
+    if (lane == 0) wsum[t >> 6] = mine;
+    __syncthreads();
+    M[static_cast<uint64_t>(blockIdx.x) * kKeys + t] = h[t];
+    if (t == 0) wgrec[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // sort_scan sums these
+}
+
+// Output of the WAL scan, in log order (lv_wal_scan_device).
+struct WalOut {
+    uint64_t *hdr_off;
+    uint32_t *info;  // type | status << 8 | length << 16
+    uint64_t *count;
+    uint64_t cap;
+};
+
+__global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__restrict__ log, uint64_t size,
+                                                            uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ ws,
+                                                            const uint32_t *__restrict__ M,
+                                                            const uint64_t *__restrict__ wgrec,
+                                                            const uint32_t *__restrict__ blkcnt,
+                                                            uint4 *__restrict__ ent, WalOut o) {
+    __shared__ uint32_t cur[kKeys];
+    __shared__ uint32_t sc[kKeys];
+    __shared__ uint64_t red[kSortThreads];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const uint64_t total = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];  // records
+    const bool over = total > o.cap;  // nothing is written past the capacity: the caller retries
+    const uint32_t mrow = M[static_cast<uint64_t>(blockIdx.x) * kKeys + t];
+    const uint32_t ks = key_starts(ws, sc);
+    cur[t] = ks + mrow;
+    if (blockIdx.x == 0 && t % kBuckets == 0) {  // per-class [start, count) for the CRC kernel
+        const uint32_t c = t / kBuckets;
+        ws[kWsCls + c] = over ? 0u : ks;
+        ws[kWsCls + 4 + c] = over ? 0u : sc[t + kBuckets - 1] - ks;
+    }
+    if (blockIdx.x == 0 && t == 0) *o.count = total;
+    // this workgroup's first record in log order: the records of the ones before
+    uint64_t pre = 0;
+    for (uint32_t v = t; v < blockIdx.x; v += kSortThreads) pre += wgrec[v];
+    red[t] = pre;
+    __syncthreads();
+    for (uint32_t d = kSortThreads / 2; d >= 1; d >>= 1) {
+        if (t < d) red[t] += red[t + d];
+        __syncthreads();
+    }
+    uint64_t run = red[0];
+    __syncthreads();
+    if (over) return;  // block-uniform
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
+        const uint64_t b = b0 + t;
+        const uint32_t c = b < hi ? blkcnt[b] : 0u;
+        red[t] = c;  // exclusive scan of the block counts (Hillis-Steele in LDS)
+        __syncthreads();
+        for (uint32_t d = 1; d < kSortThreads; d <<= 1) {
+            const uint64_t x = t >= d ? red[t - d] : 0u;
+            __syncthreads();
+            red[t] += x;
+            __syncthreads();
+        }
+        uint64_t rid = run + red[t] - c;  // log-order index of this block's first record
+        run += red[kSortThreads - 1];
+        __syncthreads();
+        const uint64_t start = b * kWalBlock;
+        const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
+        uint32_t pos = 0;
+        bool active = blen >= kWalHeader;
+        while (__any(active)) {
+            WalRec r{};
+            const bool rec = active;
+            if (active) r = wal_record(log, size, start, blen, pos);
+            const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
+            if (rec) {
+                const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
+                ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
+                                       static_cast<uint32_t>(rid));
+                o.hdr_off[rid] = start + pos;
+                o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
+                ++rid;
+                pos += kWalHeader + r.len;
+                active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
             }
         }
     }
@@ -2477,6 +2663,80 @@ int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, con
     if (!d_workspace) return set_err(LV_ERR_INVALID, "null workspace");
     return batch_device_impl(d_arena, d_off, d_len, d_seed, d_out, n, flags, stream,
                              static_cast<uint8_t *>(d_workspace), workspace_bytes);
+}
+
+// ---- WAL scan of a log in HBM (include/lvgpu/wal.h) ----
+static uint64_t wal_wgs(uint64_t nblocks, uint64_t *chunk) {
+    uint64_t wgs = (nblocks + lvk::kSortThreads - 1) / lvk::kSortThreads;
+    wgs = std::max<uint64_t>(1, std::min<uint64_t>(wgs, lvk::kSortMaxWgs));
+    *chunk = (nblocks + wgs - 1) / wgs;
+    return wgs;
+}
+
+struct WalWs {
+    size_t m, wgrec, blk, ent, total;
+};
+
+static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
+    const uint64_t nblocks = (bytes + lvk::kWalBlock - 1) / lvk::kWalBlock;
+    uint64_t chunk = 0;
+    const uint64_t wgs = wal_wgs(nblocks, &chunk);
+    WalWs w;
+    w.m = lvk::kWsHeader * sizeof(uint32_t);
+    w.wgrec = w.m + al16(wgs * lvk::kKeys * sizeof(uint32_t));
+    w.blk = w.wgrec + al16(wgs * sizeof(uint64_t));
+    w.ent = w.blk + al16(nblocks * sizeof(uint32_t));
+    w.total = w.ent + cap * sizeof(uint4);
+    return w;
+}
+
+size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) { return wal_ws_layout(bytes, cap).total; }
+
+int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
+                       size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream) {
+    g_err.clear();
+    if (!d_count) return set_err(LV_ERR_INVALID, "null count pointer");
+    if ((!d_log && bytes) || (cap && (!d_hdr_off || !d_crc || !d_info)) || !d_workspace)
+        return set_err(LV_ERR_INVALID, "null device pointer");
+    if (reinterpret_cast<uintptr_t>(d_log) % 8) return set_err(LV_ERR_INVALID, "log must be 8-byte aligned");
+    if (reinterpret_cast<uintptr_t>(d_workspace) % 16) return set_err(LV_ERR_INVALID, "workspace must be 16-byte aligned");
+    if (bytes / lvk::kWalHeader >= 0xffffffffull || cap > 0xffffffffull)
+        return set_err(LV_ERR_INVALID, "log too large for one scan");
+    const WalWs lay = wal_ws_layout(bytes, cap);
+    if (workspace_bytes < lay.total) return set_err(LV_ERR_INVALID, "workspace too small");
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t nblocks = (bytes + lvk::kWalBlock - 1) / lvk::kWalBlock;
+    if (nblocks == 0) {
+        LV_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), s));
+        return LV_OK;
+    }
+    uint8_t *wb = static_cast<uint8_t *>(d_workspace);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(wb);
+    uint32_t *M = reinterpret_cast<uint32_t *>(wb + lay.m);
+    uint64_t *wgrec = reinterpret_cast<uint64_t *>(wb + lay.wgrec);
+    uint32_t *blk = reinterpret_cast<uint32_t *>(wb + lay.blk);
+    uint4 *ent = reinterpret_cast<uint4 *>(wb + lay.ent);
+    uint64_t chunk = 0;
+    const uint64_t wgs = wal_wgs(nblocks, &chunk);
+    const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
+    hipLaunchKernelGGL(lvk::wal_hist, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk);
+    hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
+                       static_cast<uint32_t>(wgs), ws, wgrec);
+    lvk::WalOut o{d_hdr_off, d_info, d_count, cap};
+    hipLaunchKernelGGL(lvk::wal_scatter, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws, M, wgrec,
+                       blk, ent, o);
+    lvk::Params P{};
+    P.base = reinterpret_cast<uint64_t>(d_log);
+    P.out = d_crc;
+    P.n = cap;
+    P.nplain = cap;
+    P.ent = ent;
+    hipLaunchKernelGGL(lvk::crc32c_classes_kernel<false>, dim3(static_cast<uint32_t>(c->cus)), dim3(lvk::kThreads), 0,
+                       s, P, c->image[2], ws);
+    g_kernel = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel";
+    return check_launch();
 }
 
 int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t block_len, size_t n,

@@ -1,6 +1,7 @@
 """Python mirror of the WAL record layer over the C ABI in include/lvgpu/wal.h.
 
     Scan.host(log, device)            GPU framing + CRC of every physical record
+    scan_device(log_tensor, cap)      the same for a log already in HBM, no host sync
     Reader(log, scan, reporter, checksum, initial_offset)
                                       Reader::new / read_record / last_record_offset
                                       (log_reader.rs:75-120, :99)
@@ -48,6 +49,10 @@ def _bind():
     L.lv_wal_reader_last_record_offset.argtypes = [vp]
     L.lv_wal_reader_free.restype = None
     L.lv_wal_reader_free.argtypes = [vp]
+    L.lv_wal_scan_workspace_bytes.restype = sz
+    L.lv_wal_scan_workspace_bytes.argtypes = [sz, sz]
+    L.lv_wal_scan_device.restype = ctypes.c_int
+    L.lv_wal_scan_device.argtypes = [vp, sz, vp, vp, vp, sz, vp, vp, sz, vp]
     L.lv_wal_encode_host.restype = ctypes.c_int
     L.lv_wal_encode_host.argtypes = [vp, vp, vp, sz, u64, vp, sz, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]
     _bound = True
@@ -109,6 +114,34 @@ class Scan:
         if getattr(self, "_h", None):
             _bind().lv_wal_scan_free(self._h)
             self._h = None
+
+
+def scan_device(log, cap: int, workspace=None, stream=None):
+    """lv_wal_scan_device over a uint8 CUDA tensor holding the log (8-B
+    aligned): returns (hdr_off int64, crc int32, info int32, count int64[1])
+    CUDA tensors, asynchronous on `stream`.  count[0] > cap means the capacity
+    was too small and nothing else was written."""
+    import torch
+    from . import _dev_ptr, _stream_ptr
+    L = _bind()
+    dev = log.device
+    hdr = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+    crc = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    info = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    count = torch.empty(1, dtype=torch.int64, device=dev)
+    need = L.lv_wal_scan_workspace_bytes(log.numel(), cap)
+    if workspace is None:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    rc = L.lv_wal_scan_device(_dev_ptr(log, "log"), log.numel(), _dev_ptr(hdr, "hdr"), _dev_ptr(crc, "crc"),
+                              _dev_ptr(info, "info"), cap, _dev_ptr(count, "count"), _dev_ptr(workspace, "workspace"),
+                              workspace.numel(), _stream_ptr(stream))
+    if rc != 0:
+        _err("lv_wal_scan_device")
+    return hdr, crc, info, count
+
+
+def scan_workspace_bytes(nbytes: int, cap: int) -> int:
+    return int(_bind().lv_wal_scan_workspace_bytes(nbytes, cap))
 
 
 class Reader:
