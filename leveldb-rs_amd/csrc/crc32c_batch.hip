@@ -1156,13 +1156,21 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
 // the block (BAD_LENGTH) or at a ZERO/0 header (ZERO).  wal_hist walks each
 // block (one thread per block) and counts the records' CRC units
 // [type || payload] (log_reader.rs:336) into the length-sort histogram, plus
-// the records per block; sort_scan is shared; wal_scatter walks the chains
-// again and writes every record straight into its sorted slot, plus its log-
-// order header offset and info word.  The class kernel then checksums the
+// the records per block, and keeps each block's first kHdrCache headers; sort_scan
+// is shared; wal_scatter takes those headers from the cache (one independent
+// load each instead of a dependent chain step), walks on only for blocks
+// with more records, and writes every record straight into its sorted slot,
+// plus its log-order header offset and info word.  The class kernel then checksums the
 // units.  Four launches, no host synchronisation (round 1: count pass, hipCUB
 // scan, host readback of the total, emit pass, then the whole offsets API).
 constexpr uint32_t kWalBlock = 32768;  // log_format.rs:63
 constexpr uint32_t kWalHeader = 7;     // log_format.rs:66
+constexpr uint32_t kHdrCache = 16;     // headers per block wal_hist keeps for wal_scatter
+
+// A cached header: position in its block | length << 16 | type << 32.
+__device__ __forceinline__ uint64_t hdr_pack(uint32_t pos, uint32_t len, uint32_t type) {
+    return pos | (static_cast<uint64_t>(len) << 16) | (static_cast<uint64_t>(type) << 32);
+}
 
 // The 7 header bytes at pos as the low 56 bits (log 8-B aligned): aligned
 // words, each read only if it holds a byte of the log (an aligned word never
@@ -1200,7 +1208,8 @@ __device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, 
 
 __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
                                                          uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ M,
-                                                         uint64_t *__restrict__ wgrec, uint32_t *__restrict__ blkcnt) {
+                                                         uint64_t *__restrict__ wgrec, uint32_t *__restrict__ blkcnt,
+                                                         uint64_t *__restrict__ hcache) {
     __shared__ uint32_t h[kKeys];
     __shared__ uint64_t wsum[kSortThreads / 64];
     const uint32_t t = threadIdx.x, lane = t & 63u;
@@ -1220,6 +1229,7 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
             if (active) {
                 const WalRec r = wal_record(log, size, start, blen, pos);
                 key = sort_key(r.ulen);
+                if (cnt < kHdrCache) hcache[b * kHdrCache + cnt] = hdr_pack(pos, r.len, r.type);
                 ++cnt;
                 pos += kWalHeader + r.len;
                 active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
@@ -1250,7 +1260,8 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
                                                             const uint32_t *__restrict__ M,
                                                             const uint64_t *__restrict__ wgrec,
                                                             const uint32_t *__restrict__ blkcnt,
-                                                            uint4 *__restrict__ ent, WalOut o) {
+                                                            const uint64_t *__restrict__ hcache, uint4 *__restrict__ ent,
+                                                            WalOut o) {
     __shared__ uint32_t cur[kKeys];
     __shared__ uint32_t sc[kKeys];
     __shared__ uint64_t red[kSortThreads];
@@ -1295,8 +1306,39 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
         __syncthreads();
         const uint64_t start = b * kWalBlock;
         const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
+        uint64_t hc[kHdrCache];  // all cached headers requested at once
+#pragma unroll
+        for (uint32_t k = 0; k < kHdrCache; ++k) hc[k] = k < c ? hcache[b * kHdrCache + k] : 0u;
         uint32_t pos = 0;
-        bool active = blen >= kWalHeader;
+        bool active = c > 0;
+        // the first kHdrCache records of every block, from the cache (k is
+        // wave-uniform: every lane of the wave is at its block's k-th record)
+#pragma unroll
+        for (uint32_t k = 0; k < kHdrCache; ++k) {
+            if (!__any(active)) break;  // wave-uniform
+            WalRec r{};
+            const bool rec = active;
+            if (active) {
+                pos = static_cast<uint32_t>(hc[k]) & 0xffffu;
+                r.len = static_cast<uint32_t>(hc[k] >> 16) & 0xffffu;
+                r.type = static_cast<uint32_t>(hc[k] >> 32) & 0xffu;
+                r.status = kWalHeader + r.len > blen - pos ? LV_WAL_REC_BAD_LENGTH
+                                                           : (r.type == 0 && r.len == 0 ? LV_WAL_REC_ZERO : LV_WAL_REC_OK);
+                r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
+            }
+            const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
+            if (rec) {
+                const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
+                ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
+                                       static_cast<uint32_t>(rid));
+                o.hdr_off[rid] = start + pos;
+                o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
+                ++rid;
+                pos += kWalHeader + r.len;
+                active = k + 1 < c;
+            }
+        }
+        // blocks with more records walk on from there
         while (__any(active)) {
             WalRec r{};
             const bool rec = active;
@@ -2674,7 +2716,7 @@ static uint64_t wal_wgs(uint64_t nblocks, uint64_t *chunk) {
 }
 
 struct WalWs {
-    size_t m, wgrec, blk, ent, total;
+    size_t m, wgrec, blk, hc, ent, total;
 };
 
 static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
@@ -2685,7 +2727,8 @@ static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
     w.m = lvk::kWsHeader * sizeof(uint32_t);
     w.wgrec = w.m + al16(wgs * lvk::kKeys * sizeof(uint32_t));
     w.blk = w.wgrec + al16(wgs * sizeof(uint64_t));
-    w.ent = w.blk + al16(nblocks * sizeof(uint32_t));
+    w.hc = w.blk + al16(nblocks * sizeof(uint32_t));
+    w.ent = w.hc + nblocks * lvk::kHdrCache * sizeof(uint64_t);
     w.total = w.ent + cap * sizeof(uint4);
     return w;
 }
@@ -2717,16 +2760,18 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     uint32_t *M = reinterpret_cast<uint32_t *>(wb + lay.m);
     uint64_t *wgrec = reinterpret_cast<uint64_t *>(wb + lay.wgrec);
     uint32_t *blk = reinterpret_cast<uint32_t *>(wb + lay.blk);
+    uint64_t *hc = reinterpret_cast<uint64_t *>(wb + lay.hc);
     uint4 *ent = reinterpret_cast<uint4 *>(wb + lay.ent);
     uint64_t chunk = 0;
     const uint64_t wgs = wal_wgs(nblocks, &chunk);
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
-    hipLaunchKernelGGL(lvk::wal_hist, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk);
+    hipLaunchKernelGGL(lvk::wal_hist, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk,
+                       hc);
     hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
                        static_cast<uint32_t>(wgs), ws, wgrec);
     lvk::WalOut o{d_hdr_off, d_info, d_count, cap};
     hipLaunchKernelGGL(lvk::wal_scatter, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws, M, wgrec,
-                       blk, ent, o);
+                       blk, hc, ent, o);
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(d_log);
     P.out = d_crc;
