@@ -1172,28 +1172,50 @@ __device__ __forceinline__ uint64_t hdr_pack(uint32_t pos, uint32_t len, uint32_
     return pos | (static_cast<uint64_t>(len) << 16) | (static_cast<uint64_t>(type) << 32);
 }
 
-// The 7 header bytes at pos as the low 56 bits (log 8-B aligned): aligned
-// words, each read only if it holds a byte of the log (an aligned word never
-// crosses a page), and a funnel shift.
-__device__ __forceinline__ uint64_t wal_load8(const uint8_t *log, uint64_t size, uint64_t pos) {
-    const uint64_t a = pos & ~7ull;
-    const uint64_t *w = reinterpret_cast<const uint64_t *>(log + a);
-    const uint64_t lo = a < size ? w[0] : 0ull;
-    const uint32_t sh = static_cast<uint32_t>(pos & 7u) * 8u;
-    if (!sh) return lo;
-    const uint64_t hi = a + 8 < size ? w[1] : 0ull;
-    return (lo >> sh) | (hi << (64u - sh));
-}
+// A thread's 64-B window of the log in LDS (a slot of 17 dwords: the 17th
+// stays 0).  Chains of short records keep several headers per window, so
+// the walk's dependent step is an LDS read instead of an L2/HBM round trip;
+// a header outside the window reloads it (four 16-B loads, each only if its
+// granule holds a log byte: an aligned granule never crosses a page).
+__shared__ uint32_t g_hwin[kSortThreads][17];
+
+struct HdrWindow {
+    uint64_t wa = ~0ull;  // log offset of the window (16-B aligned)
+
+    // The 8 bytes at log offset p (bytes past the log read as 0).
+    __device__ __forceinline__ uint64_t get(const uint8_t *log, uint64_t size, uint64_t p, uint32_t *slot) {
+        if (wa == ~0ull || p < wa || p + 8 > wa + 64) {
+            wa = p & ~15ull;
+            const uint4 *g = reinterpret_cast<const uint4 *>(log + wa);
+            uint4 v[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) v[q] = wa + 16 * q < size ? g[q] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                slot[4 * q] = v[q].x;
+                slot[4 * q + 1] = v[q].y;
+                slot[4 * q + 2] = v[q].z;
+                slot[4 * q + 3] = v[q].w;
+            }
+            slot[16] = 0;
+        }
+        const uint32_t r = static_cast<uint32_t>(p - wa), d = r >> 2, sh = r & 3u;
+        const uint32_t d0 = slot[d], d1 = slot[d + 1], d2 = slot[d + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        return lo | (static_cast<uint64_t>(hi) << 32);
+    }
+};
 
 // One step of a block's header chain: the record at pos (status, unit
-// length) and the position after it; `more` says whether another header fits.
+// length); the next header is at pos + HEADER_SIZE + len.
 struct WalRec {
     uint32_t len, type, status, ulen;
 };
 
 __device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, uint64_t start, uint32_t blen,
-                                             uint32_t pos) {
-    const uint64_t h = wal_load8(log, size, start + pos);  // crc(4) | length(2) | type(1)
+                                             uint32_t pos, HdrWindow &win, uint32_t *slot) {
+    const uint64_t h = win.get(log, size, start + pos, slot);  // crc(4) | length(2) | type(1)
     WalRec r;
     r.len = static_cast<uint32_t>(h >> 32) & 0xffffu;
     r.type = static_cast<uint32_t>(h >> 48) & 0xffu;
@@ -1217,17 +1239,19 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
     uint64_t mine = 0;
+    uint32_t *slot = g_hwin[t];
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
         const uint64_t b = b0 + t;
         const uint64_t start = b * kWalBlock;
         const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
         uint32_t pos = 0, cnt = 0;
+        HdrWindow win;
         bool active = blen >= kWalHeader;
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             uint32_t key = 0;
             const bool rec = active;
             if (active) {
-                const WalRec r = wal_record(log, size, start, blen, pos);
+                const WalRec r = wal_record(log, size, start, blen, pos, win, slot);
                 key = sort_key(r.ulen);
                 if (cnt < kHdrCache) hcache[b * kHdrCache + cnt] = hdr_pack(pos, r.len, r.type);
                 ++cnt;
@@ -1339,10 +1363,11 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
             }
         }
         // blocks with more records walk on from there
+        HdrWindow win;
         while (__any(active)) {
             WalRec r{};
             const bool rec = active;
-            if (active) r = wal_record(log, size, start, blen, pos);
+            if (active) r = wal_record(log, size, start, blen, pos, win, g_hwin[t]);
             const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
             if (rec) {
                 const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
