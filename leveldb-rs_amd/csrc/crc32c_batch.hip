@@ -1180,16 +1180,17 @@ __device__ __forceinline__ uint64_t hdr_pack(uint32_t pos, uint32_t len, uint32_
 __shared__ uint32_t g_hwin[kSortThreads][17];
 
 struct HdrWindow {
-    uint64_t wa = ~0ull;  // log offset of the window (16-B aligned)
+    uint64_t wa = ~0ull;  // address of the window (16-B aligned in memory, not relative to the log)
 
     // The 8 bytes at log offset p (bytes past the log read as 0).
     __device__ __forceinline__ uint64_t get(const uint8_t *log, uint64_t size, uint64_t p, uint32_t *slot) {
-        if (wa == ~0ull || p < wa || p + 8 > wa + 64) {
-            wa = p & ~15ull;
-            const uint4 *g = reinterpret_cast<const uint4 *>(log + wa);
+        const uint64_t end = reinterpret_cast<uint64_t>(log) + size, ap = reinterpret_cast<uint64_t>(log) + p;
+        if (wa == ~0ull || ap < wa || ap + 8 > wa + 64) {
+            wa = ap & ~15ull;
             uint4 v[4];
 #pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) v[q] = wa + 16 * q < size ? g[q] : make_uint4(0, 0, 0, 0);
+            for (uint32_t q = 0; q < 4; ++q)
+                v[q] = wa + 16 * q < end ? *reinterpret_cast<const uint4 *>(wa + 16 * q) : make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (uint32_t q = 0; q < 4; ++q) {
                 slot[4 * q] = v[q].x;
@@ -1199,7 +1200,7 @@ struct HdrWindow {
             }
             slot[16] = 0;
         }
-        const uint32_t r = static_cast<uint32_t>(p - wa), d = r >> 2, sh = r & 3u;
+        const uint32_t r = static_cast<uint32_t>(ap - wa), d = r >> 2, sh = r & 3u;
         const uint32_t d0 = slot[d], d1 = slot[d + 1], d2 = slot[d + 2];
         const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
         const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
