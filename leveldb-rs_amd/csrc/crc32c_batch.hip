@@ -1165,48 +1165,29 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
 // scan, host readback of the total, emit pass, then the whole offsets API).
 constexpr uint32_t kWalBlock = 32768;  // log_format.rs:63
 constexpr uint32_t kWalHeader = 7;     // log_format.rs:66
-constexpr uint32_t kHdrCache = 16;     // headers per block wal_hist keeps for wal_scatter
+constexpr uint32_t kHdrCache = 64;     // headers per block wal_hist keeps for wal_scatter
+constexpr uint32_t kHdrChunk = 8;      // cached headers wal_scatter requests at once
 
 // A cached header: position in its block | length << 16 | type << 32.
 __device__ __forceinline__ uint64_t hdr_pack(uint32_t pos, uint32_t len, uint32_t type) {
     return pos | (static_cast<uint64_t>(len) << 16) | (static_cast<uint64_t>(type) << 32);
 }
 
-// A thread's 64-B window of the log in LDS (a slot of 17 dwords: the 17th
-// stays 0).  Chains of short records keep several headers per window, so
-// the walk's dependent step is an LDS read instead of an L2/HBM round trip;
-// a header outside the window reloads it (four 16-B loads, each only if its
-// granule holds a log byte: an aligned granule never crosses a page).
-__shared__ uint32_t g_hwin[kSortThreads][17];
-
-struct HdrWindow {
-    uint64_t wa = ~0ull;  // address of the window (16-B aligned in memory, not relative to the log)
-
-    // The 8 bytes at log offset p (bytes past the log read as 0).
-    __device__ __forceinline__ uint64_t get(const uint8_t *log, uint64_t size, uint64_t p, uint32_t *slot) {
-        const uint64_t end = reinterpret_cast<uint64_t>(log) + size, ap = reinterpret_cast<uint64_t>(log) + p;
-        if (wa == ~0ull || ap < wa || ap + 8 > wa + 64) {
-            wa = ap & ~15ull;
-            uint4 v[4];
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q)
-                v[q] = wa + 16 * q < end ? *reinterpret_cast<const uint4 *>(wa + 16 * q) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                slot[4 * q] = v[q].x;
-                slot[4 * q + 1] = v[q].y;
-                slot[4 * q + 2] = v[q].z;
-                slot[4 * q + 3] = v[q].w;
-            }
-            slot[16] = 0;
-        }
-        const uint32_t r = static_cast<uint32_t>(ap - wa), d = r >> 2, sh = r & 3u;
-        const uint32_t d0 = slot[d], d1 = slot[d + 1], d2 = slot[d + 2];
-        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
-        return lo | (static_cast<uint64_t>(hi) << 32);
-    }
-};
+// The 8 bytes at log offset pos (bytes past the log read as 0): aligned
+// 8-B words, each read only if it holds a byte of the log (an aligned word
+// never crosses a page), and a funnel shift.  (A per-thread 64-B LDS window
+// of the log, which would keep several short records' headers per load,
+// measured slower: wal_hist 36.6 -> 41.6 us.  The chains that bound the
+// walk are hops over longer records, one HBM round trip each.)
+__device__ __forceinline__ uint64_t wal_load8(const uint8_t *log, uint64_t size, uint64_t pos) {
+    const uint64_t a = pos & ~7ull;
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(log + a);
+    const uint64_t lo = a < size ? w[0] : 0ull;
+    const uint32_t sh = static_cast<uint32_t>(pos & 7u) * 8u;
+    if (!sh) return lo;
+    const uint64_t hi = a + 8 < size ? w[1] : 0ull;
+    return (lo >> sh) | (hi << (64u - sh));
+}
 
 // One step of a block's header chain: the record at pos (status, unit
 // length); the next header is at pos + HEADER_SIZE + len.
@@ -1215,8 +1196,8 @@ struct WalRec {
 };
 
 __device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, uint64_t start, uint32_t blen,
-                                             uint32_t pos, HdrWindow &win, uint32_t *slot) {
-    const uint64_t h = win.get(log, size, start + pos, slot);  // crc(4) | length(2) | type(1)
+                                             uint32_t pos) {
+    const uint64_t h = wal_load8(log, size, start + pos);  // crc(4) | length(2) | type(1)
     WalRec r;
     r.len = static_cast<uint32_t>(h >> 32) & 0xffffu;
     r.type = static_cast<uint32_t>(h >> 48) & 0xffu;
@@ -1240,19 +1221,17 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
     uint64_t mine = 0;
-    uint32_t *slot = g_hwin[t];
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
         const uint64_t b = b0 + t;
         const uint64_t start = b * kWalBlock;
         const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
         uint32_t pos = 0, cnt = 0;
-        HdrWindow win;
         bool active = blen >= kWalHeader;
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             uint32_t key = 0;
             const bool rec = active;
             if (active) {
-                const WalRec r = wal_record(log, size, start, blen, pos, win, slot);
+                const WalRec r = wal_record(log, size, start, blen, pos);
                 key = sort_key(r.ulen);
                 if (cnt < kHdrCache) hcache[b * kHdrCache + cnt] = hdr_pack(pos, r.len, r.type);
                 ++cnt;
@@ -1331,22 +1310,31 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
         __syncthreads();
         const uint64_t start = b * kWalBlock;
         const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
-        uint64_t hc[kHdrCache];  // all cached headers requested at once
-#pragma unroll
-        for (uint32_t k = 0; k < kHdrCache; ++k) hc[k] = k < c ? hcache[b * kHdrCache + k] : 0u;
         uint32_t pos = 0;
         bool active = c > 0;
-        // the first kHdrCache records of every block, from the cache (k is
-        // wave-uniform: every lane of the wave is at its block's k-th record)
+        // the first kHdrCache records of every block, from the cache, in
+        // chunks of kHdrChunk requested one chunk ahead (k is wave-uniform:
+        // every lane of the wave is at its block's k-th record)
+        uint64_t hc[kHdrChunk], hn[kHdrChunk];
 #pragma unroll
-        for (uint32_t k = 0; k < kHdrCache; ++k) {
+        for (uint32_t q = 0; q < kHdrChunk; ++q) hc[q] = q < c ? hcache[b * kHdrCache + q] : 0u;
+        for (uint32_t k0 = 0; k0 < kHdrCache; k0 += kHdrChunk) {
+            if (!__any(active)) break;  // wave-uniform
+#pragma unroll
+            for (uint32_t q = 0; q < kHdrChunk; ++q) {
+                const uint32_t k = k0 + kHdrChunk + q;
+                hn[q] = k < c && k < kHdrCache ? hcache[b * kHdrCache + k] : 0u;
+            }
+#pragma unroll
+        for (uint32_t q = 0; q < kHdrChunk; ++q) {
+            const uint32_t k = k0 + q;
             if (!__any(active)) break;  // wave-uniform
             WalRec r{};
             const bool rec = active;
             if (active) {
-                pos = static_cast<uint32_t>(hc[k]) & 0xffffu;
-                r.len = static_cast<uint32_t>(hc[k] >> 16) & 0xffffu;
-                r.type = static_cast<uint32_t>(hc[k] >> 32) & 0xffu;
+                pos = static_cast<uint32_t>(hc[q]) & 0xffffu;
+                r.len = static_cast<uint32_t>(hc[q] >> 16) & 0xffffu;
+                r.type = static_cast<uint32_t>(hc[q] >> 32) & 0xffu;
                 r.status = kWalHeader + r.len > blen - pos ? LV_WAL_REC_BAD_LENGTH
                                                            : (r.type == 0 && r.len == 0 ? LV_WAL_REC_ZERO : LV_WAL_REC_OK);
                 r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
@@ -1363,12 +1351,14 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
                 active = k + 1 < c;
             }
         }
+#pragma unroll
+            for (uint32_t q = 0; q < kHdrChunk; ++q) hc[q] = hn[q];
+        }
         // blocks with more records walk on from there
-        HdrWindow win;
         while (__any(active)) {
             WalRec r{};
             const bool rec = active;
-            if (active) r = wal_record(log, size, start, blen, pos, win, g_hwin[t]);
+            if (active) r = wal_record(log, size, start, blen, pos);
             const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
             if (rec) {
                 const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336

@@ -11,7 +11,10 @@
 // key's last byte, and keys of <= 64 B run the chain from registers.
 // The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
 // requests the next set's metadata ahead, and stores each result one set
-// late, after the next set's loads, so no wait includes a store.
+// late, after the next set's loads, so no wait includes a store.  (A
+// two-deep form -- the next set's span in flight in registers while this
+// set hashes from LDS, metadata two sets ahead, 64 VGPRs at 8 waves/SIMD --
+// measured 106 vs 117 G keys/s, three interleaved reps: not kept.)
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -271,210 +274,6 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     }
 }
 
-// ---- Two-deep pipeline (LVH_PIPE2): the next set's span is in flight while
-// this set hashes.  Per set: write the span that arrived (registers) to the
-// wave's LDS stage, request the next set's span into the same registers,
-// then read this set's keys from LDS and run the chains.  The metadata runs
-// two sets ahead.  Sets whose keys do not fit one staged span take the
-// one-deep path (hash_set).  8 waves per SIMD: <= 64 VGPRs.
-constexpr uint32_t kCh = kSpanBytes / 16 / 64;  // 16-B granules per lane of a staged span
-
-struct SpanPlan {
-    uint64_t lo16;
-    uint32_t nch;
-    bool staged;
-};
-
-__device__ __forceinline__ SpanPlan span_plan(bool valid, uint64_t o, uint32_t L) {
-    const uint64_t act = __ballot(valid);
-    const int last = act ? 63 - __builtin_clzll(act) : 0;
-    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
-    SpanPlan sp;
-    sp.lo16 = lo & ~15ull;
-    const bool inside = !L || (o >= lo && o + L <= hi);
-    sp.staged = act && hi > lo && hi - sp.lo16 <= kSpanBytes && __all(inside);  // wave-uniform
-    sp.nch = sp.staged ? static_cast<uint32_t>((hi - sp.lo16 + 15) >> 4) : 0u;
-    return sp;
-}
-
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void span_load(const uint8_t *base, const SpanPlan &sp, uint32_t lane, u32x4v (&t)[kCh]) {
-    const u32x4v *src = reinterpret_cast<const u32x4v *>(base + sp.lo16);
-#pragma unroll
-    for (uint32_t k = 0; k < kCh; ++k) {
-        const uint32_t c = lane + 64u * k;
-        if (c < sp.nch) t[k] = __builtin_nontemporal_load(src + c);
-    }
-}
-
-__device__ __forceinline__ void span_store(uint32_t *span, const SpanPlan &sp, uint32_t lane, const u32x4v (&t)[kCh]) {
-    u32x4v *dst = reinterpret_cast<u32x4v *>(span);
-#pragma unroll
-    for (uint32_t k = 0; k < kCh; ++k) {
-        const uint32_t c = lane + 64u * k;
-        if (c < sp.nch) dst[c] = t[k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Hash of this lane's key read from memory (hash.rs:20-51): dword-aligned
-// reads funnel-shifted by the misalignment, 4 words per step.
-__device__ __forceinline__ uint32_t hash_mem(const uint8_t *__restrict__ base, bool valid, uint64_t o, uint32_t L,
-                                             uint32_t sdv) {
-    uint32_t h = sdv ^ (kM * L);  // hash.rs:25
-    if (!valid || !L) return h;
-    const uint32_t bs = static_cast<uint32_t>(o & 3u);
-    const uint32_t nw = L >> 2;
-    const uint32_t ndw = (bs + L + 3) >> 2;
-    const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
-    uint32_t cur = d[0];
-    uint32_t k = 0;
-    for (; k + 4 <= nw && k + 4 < ndw; k += 4) {
-        const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + k + 1);
-        h = mix(h, funnel(v.x, cur, bs));
-        h = mix(h, funnel(v.y, v.x, bs));
-        h = mix(h, funnel(v.z, v.y, bs));
-        h = mix(h, funnel(v.w, v.z, bs));
-        cur = v.w;
-    }
-    for (; k < nw; ++k) {
-        const uint32_t hi = k + 1 < ndw ? d[k + 1] : 0u;
-        h = mix(h, funnel(hi, cur, bs));
-        cur = hi;
-    }
-    const uint32_t diff = L - 4 * nw;  // hash.rs:38-48
-    if (diff) {
-        const uint32_t hi = nw + 1 < ndw ? d[nw + 1] : 0u;
-        const uint32_t t = funnel(hi, cur, bs);
-        if (diff >= 3) h += ((t >> 16) & 0xffu) << 16;
-        if (diff >= 2) h += ((t >> 8) & 0xffu) << 8;
-        h += t & 0xffu;
-        h *= kM;
-        h ^= h >> 24;
-    }
-    return h;
-}
-
-// Hash of this lane's key from the staged span (keys of <= 64 B plus
-// misalignment, streamed from LDS one dword ahead); longer keys from memory.
-__device__ __forceinline__ uint32_t hash_staged(const uint8_t *__restrict__ base, const uint32_t *span, uint64_t lo16,
-                                                bool valid, uint64_t o, uint32_t L, uint32_t sdv) {
-    const uint32_t bs = static_cast<uint32_t>(o & 3u);
-    const uint32_t ndw = (bs + L + 3) >> 2;
-    if (!valid || !L || ndw > kFastDw) return hash_mem(base, valid, o, L, sdv);
-    uint32_t h = sdv ^ (kM * L);  // hash.rs:25
-    const uint32_t nw = L >> 2;
-    uint32_t tw = 0;
-    const uint32_t *sd = span + ((o - bs - lo16) >> 2);
-    uint32_t prev = sd[0];
-    // two halves of LDS reads, so at most ~9 key dwords are live beside the
-    // next set's span registers (8 waves per SIMD: <= 64 VGPRs)
-#pragma unroll
-    for (uint32_t half = 0; half < 2; ++half) {
-        constexpr uint32_t kH = (kFastDw + 1) / 2;
-        uint32_t w[kH];
-#pragma unroll
-        for (uint32_t q = 0; q < kH; ++q) {
-            const uint32_t j = half * kH + q;
-            w[q] = (j < kFastDw && j + 1 < ndw) ? sd[j + 1] : 0u;
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < kH; ++q) {
-            const uint32_t j = half * kH + q;
-            if (j >= kFastDw) break;
-            const uint32_t wj = funnel(w[q], prev, bs);
-            if (j < nw)
-                h = mix(h, wj);
-            else if (j == nw)
-                tw = wj;
-            prev = w[q];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    const uint32_t diff = L - 4 * nw;  // hash.rs:38-48
-    if (diff) {
-        if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
-        if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;
-        h += tw & 0xffu;
-        h *= kM;
-        h ^= h >> 24;
-    }
-    return h;
-}
-
-__global__ void __launch_bounds__(256, 8) hash_kernel2(const uint8_t *__restrict__ base,
-                                                      const uint64_t *__restrict__ off,
-                                                      const uint32_t *__restrict__ len,
-                                                      const uint32_t *__restrict__ seed, uint32_t *__restrict__ out,
-                                                      uint32_t n, uint32_t flags) {
-    __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpanBytes / 4 + kSpanPad];
-    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
-    if (set * 64u >= n) return;  // wave-uniform
-    auto meta = [&](uint64_t st, uint64_t &o, uint32_t &L, uint32_t &sd) {
-        const uint64_t i = st * 64u + lane;
-        const bool v = i < n;
-        o = v ? off[i] : 0u;
-        L = v ? len[i] : 0u;
-        sd = v && seed ? seed[i] : 0u;
-    };
-    uint64_t o0, o1 = 0, o2 = 0;
-    uint32_t L0, sd0, L1 = 0, sd1 = 0, L2 = 0, sd2 = 0;
-    meta(set, o0, L0, sd0);
-    bool more1 = (set + W) * 64u < n;
-    if (more1) meta(set + W, o1, L1, sd1);
-    SpanPlan sp0 = span_plan(set * 64u + lane < n, o0, L0);
-    u32x4v t[kCh];
-    if (sp0.staged) span_load(base, sp0, lane, t);
-    uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late
-    bool pst = false;
-    for (;;) {
-        const bool more2 = more1 && (set + 2 * W) * 64u < n;  // wave-uniform
-        if (more2) meta(set + 2 * W, o2, L2, sd2);
-        const uint64_t i = set * 64u + lane;
-        const bool valid = i < n;
-        uint32_t h;
-        if (sp0.staged) {
-            span_store(span[wv], sp0, lane, t);  // waits for this set's span only
-            SpanPlan sp1{0, 0, false};
-            if (more1) {
-                sp1 = span_plan((set + W) * 64u + lane < n, o1, L1);
-                if (sp1.staged) span_load(base, sp1, lane, t);  // the next set's span, in flight below
-            }
-            if (pst) *pout = pval;
-            h = hash_staged(base, span[wv], sp0.lo16, valid, o0, L0, sd0);
-            sp0 = sp1;
-        } else {  // keys scattered or spanning > 4 KiB: each lane reads its key
-            if (pst) *pout = pval;
-            h = hash_mem(base, valid, o0, L0, sd0);
-            if (more1) {
-                sp0 = span_plan((set + W) * 64u + lane < n, o1, L1);
-                if (sp0.staged) span_load(base, sp0, lane, t);
-            }
-        }
-        pout = out + (valid ? i : 0u);
-        pval = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
-        pst = valid;
-        if (!more1) {
-            if (pst) *pout = pval;
-            break;
-        }
-        __builtin_amdgcn_wave_barrier();  // this set's LDS reads precede the next stage
-        set += W;
-        o0 = o1;
-        L0 = L1;
-        sd0 = sd1;
-        o1 = o2;
-        L1 = L2;
-        sd1 = sd2;
-        more1 = more2;
-    }
-}
-
 }  // namespace lvh
 
 extern "C" {
@@ -519,15 +318,8 @@ int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const ui
     }
     const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * lvh::kWgsPerCu;
     const uint32_t grid = static_cast<uint32_t>(want < cap ? want : cap);
-#ifndef LVH_PIPE2
-#define LVH_PIPE2 1
-#endif
-    if (LVH_PIPE2)
-        hipLaunchKernelGGL(lvh::hash_kernel2, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_arena,
-                           d_off, d_len, d_seed, d_out, static_cast<uint32_t>(n), flags);
-    else
-        hipLaunchKernelGGL(lvh::hash_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_arena,
-                           d_off, d_len, d_seed, d_out, static_cast<uint32_t>(n), flags);
+    hipLaunchKernelGGL(lvh::hash_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_arena, d_off,
+                       d_len, d_seed, d_out, static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
 }
 
