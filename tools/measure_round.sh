@@ -1,10 +1,12 @@
 #!/bin/bash
 # One GPU-box pass of every bench line and kernel profile for the round:
-#   bench.py default (C3 strided, headline), C3 offsets, C2, C4, C5,
-#   the C1 CPU sweep, the host-memory E2E path, the WAL / table / hash rows
-#   of SURVEY 8f, and rocprofv3 kernel-trace
-#   stats for C3 (strided) / C2 / C4.  Every GPU step has its own timeout and
-#   the chain stops at the first failure.
+#   bench.py default (C3 strided, headline) at the driver's flags and at the
+#   bench defaults, C3 offsets, C2, C4, C5 (8 GiB per GPU) and C5 strong (the
+#   64 GiB global batch), the C1 CPU sweep, the host-memory E2E path, the WAL
+#   (host and device-resident) / table / hash rows of SURVEY 8f, the 4-64 KiB
+#   sweep, few-long-buffer batches, and rocprofv3 kernel-trace stats for C3
+#   (strided) / C2 / C4 / the WAL device scan.  Every GPU step has its own
+#   timeout and the chain stops at the first failure.
 # usage: tools/measure_round.sh OUTDIR
 set -o pipefail
 out=${1:-gpurun_out/round}
@@ -17,18 +19,25 @@ p() { local name=$1; shift
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_$name" -o "$name" -- \
          python3 "$root/bench.py" --steps 50 --warmup 100 --cpu-seconds 0 --traffic off "$@") > "$out/prof_$name.log" 2>&1 &&
       python3 tools/kstats_steady.py "$(ls "$out/prof_$name"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_${name}_steady.json" > /dev/null; }
+b default_driver --steps 20 --warmup 5 &&
 b default &&
 b c3_offsets --workload c3 --api offsets --cpu-seconds 5 &&
 b c2 --workload c2 --api offsets --cpu-seconds 5 &&
 b c4 --workload c4 --api offsets --cpu-seconds 5 &&
 b c5 --workload c5 --cpu-seconds 5 &&
+b c5_strong --workload c5 --scaling strong --steps 20 --warmup 5 --cpu-seconds 5 &&
 timeout -k 10 200 python3 bench.py --e2e > "$out/e2e.json" 2> "$out/e2e.err" &&
 timeout -k 10 300 python3 bench.py --c1 > "$out/c1.json" 2> "$out/c1.err" &&
 timeout -k 10 300 python3 bench.py --wal > "$out/wal.json" 2> "$out/wal.err" &&
 timeout -k 10 300 python3 bench.py --table > "$out/table.json" 2> "$out/table.err" &&
 timeout -k 10 300 python3 bench.py --hash > "$out/hash.json" 2> "$out/hash.err" &&
 timeout -k 10 300 python3 bench.py --sweep > "$out/sweep.json" 2> "$out/sweep.err" &&
+timeout -k 10 300 python3 bench.py --wal-device > "$out/wal_device.json" 2> "$out/wal_device.err" &&
+timeout -k 10 300 python3 bench.py --long > "$out/long.json" 2> "$out/long.err" &&
 p c3 &&
 p c2 --workload c2 --api offsets &&
 p c4 --workload c4 --api offsets &&
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_wal" -o wal -- \
+   python3 "$root/bench.py" --wal-device --steps 50 --warmup 20) > "$out/prof_wal.log" 2>&1 &&
+python3 tools/kstats_steady.py "$(ls "$out/prof_wal"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_wal_steady.json" > /dev/null &&
 echo "all steps done"
