@@ -579,21 +579,20 @@ __device__ __forceinline__ void group_stream(const Params &P, uint64_t gid, uint
 // Copy the 152 KiB table image into LDS: every thread issues all of its
 // (<= 10) 16-B loads before the first LDS store, so the copy costs about one
 // L2 round trip rather than ten.
-template <int kT = kThreads>
 __device__ __forceinline__ void stage_tables(const uint4 *__restrict__ image) {
     constexpr int kVec = kImageWords / 4;
-    constexpr int kPer = (kVec + kT - 1) / kT;
+    constexpr int kPer = (kVec + kThreads - 1) / kThreads;
     uint4 *l4 = reinterpret_cast<uint4 *>(g_lds);
     g_u32x4 *src = reinterpret_cast<g_u32x4 *>(reinterpret_cast<uint64_t>(image));
     u32x4 r[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int i = threadIdx.x + k * kT;
+        const int i = threadIdx.x + k * kThreads;
         if (i < kVec) r[k] = src[i];
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int i = threadIdx.x + k * kT;
+        const int i = threadIdx.x + k * kThreads;
         if (i < kVec) l4[i] = to_uint4(r[k]);
     }
     __syncthreads();
@@ -1659,13 +1658,8 @@ __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a
         const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
         const uint32_t x23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
         X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
-    } else if constexpr (NU == 6) {  // W2(W2(W1(h0)^h1) ^ (W1(h2)^h3)) ^ (W1(h4)^h5)
-        const uint32_t p01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
-        const uint32_t p23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
-        const uint32_t p45 = lookup4<kRegionB>(early ? A[3] : A[4], L) ^ (early ? A[4] : A[5]);
-        X = lookup4<kRegionB + kHalf>(lookup4<kRegionB + kHalf>(p01, L) ^ p23, L) ^ p45;
     } else {  // NU = 2: W1(h0) ^ h1
-        static_assert(NU == 2, "aligned rows: 2, 4 or 6 rows per batch");
+        static_assert(NU == 2, "aligned rows: 2 or 4 rows per batch");
         X = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
     }
     if (rot) X = __shfl(X, static_cast<int32_t>((lane & ~15u) | ((gl + static_cast<uint32_t>(g.e) + 1u) & 15u)));
@@ -1699,16 +1693,6 @@ __device__ __forceinline__ uint32_t round_pad(const RGeo &q, uint32_t nbw) {
 template <int W4K, uint32_t NU, uint32_t W4OFF>
 __device__ __forceinline__ void fold_first(const uint4 (&v)[NU], uint32_t (&A)[NU], const Lut &L, uint32_t pad) {
 #if LVK_SKIP_PAD
-    if constexpr (NU == 6) {
-        switch (pad) {
-        case 5: fold_batch<true, W4K, NU, W4OFF, 5>(v, A, L); return;
-        case 4: fold_batch<true, W4K, NU, W4OFF, 4>(v, A, L); return;
-        case 3: fold_batch<true, W4K, NU, W4OFF, 3>(v, A, L); return;
-        case 2: fold_batch<true, W4K, NU, W4OFF, 2>(v, A, L); return;
-        case 1: fold_batch<true, W4K, NU, W4OFF, 1>(v, A, L); return;
-        default: break;
-        }
-    }
     if constexpr (NU == 4) {
         if (pad == 3) {
             fold_batch<true, W4K, NU, W4OFF, 3>(v, A, L);
@@ -1780,16 +1764,13 @@ struct SortedList {
 // loads and spills cost more than the conservative wait counts they remove.)
 // The image is always the G = 16 one: groups of G = 1 and 4 take their
 // row-shift and merge tables from the plain combine tables.
-// ALR: rows per batch of the G = 16 aligned walk (the table kernel runs 6
-// on its own image, whose W4 is Shift_1536).
-template <int G, class Src, class Next, uint32_t ALR = kAlRows>
+template <int G, class Src, class Next>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {
     constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
-    constexpr uint32_t NU = AL ? ALR : U;              // rows per batch
-    // Latin row shift Shift_{16 G NU}: the image's W4 (NU = 4, or 6 on the
-    // table image) or region B's W2 (NU = 2)
-    constexpr uint32_t W4OFF = NU == 2 ? kRegionB + kHalf : kRegionA + kHalf;
+    constexpr uint32_t NU = AL ? kAlRows : U;          // rows per batch
+    // Latin row shift Shift_{16 G NU}: the image's W4 (NU = 4) or W2 (NU = 2)
+    constexpr uint32_t W4OFF = NU == 4 ? kRegionA + kHalf : kRegionB + kHalf;
     constexpr uint32_t K = 64 / G;
     constexpr int W4K = G == 16 ? -1 : (G == 4 ? 4 : 2);  // Shift_{64G}
     constexpr int W1K = G == 16 ? -1 : (G == 4 ? 2 : 0);  // Shift_{16G}
@@ -2079,20 +2060,10 @@ struct TableUnits {
     }
 };
 
-// 12 waves per CU and 6-row batches: a 4,097-4,352-B unit spans 17-18 rows
-// of 256 B, three 6-row batches instead of five 4-row ones, and the time of
-// the walk tracks batch-steps more than bytes (tools/table_shape_probe.py).
-// The two extra rows per register slot need 12 waves' register budget.
-#ifndef LVK_TABLE_ROWS
-#define LVK_TABLE_ROWS 6
-#endif
-constexpr uint32_t kTableRows = LVK_TABLE_ROWS;
-constexpr int kTableThreads = kTableRows > 4 ? 768 : kThreads;
-
 template <bool SEAL>
-__global__ __launch_bounds__(kTableThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
-                                                                   TableUnits<SEAL> src) {
-    stage_tables<kTableThreads>(image);
+__global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
+                                                              TableUnits<SEAL> src) {
+    stage_tables(image);
     if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -2103,7 +2074,7 @@ __global__ __launch_bounds__(kTableThreads) void sst_blocks_kernel(Params P, con
         if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
         return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
     };
-    sorted_stream<16, TableUnits<SEAL>, decltype(pool), kTableRows>(P, src, lane, L, pool(), pool);
+    sorted_stream<16>(P, src, lane, L, pool(), pool);
 }
 
 // Joins the raw piece registers of the long-block split: block b's pieces
@@ -2253,19 +2224,17 @@ int set_err(int code, const std::string &msg) {
 constexpr int kGs[4] = {1, 4, 16, 64};
 
 // Host copy of the LDS image for each G (index into kGs); layout in lvk.
-// gi = 4: the SST table kernel's image, the G = 16 image with W4 =
-// Shift_{16*16*6} (6-row batches).
 const std::vector<uint32_t> &host_image(int gi) {
-    static std::vector<uint32_t> images[5];
+    static std::vector<uint32_t> images[4];
     static std::once_flag once;
     std::call_once(once, [] {
         uint32_t T[4][256], C[6][4][256];
         lvgpu::slice_tables(T);
         for (int k = 0; k < 6; ++k) lvgpu::shift_tables(16ull << k, C[k]);
-        for (int i = 0; i < 5; ++i) {
-            const uint64_t G = static_cast<uint64_t>(kGs[i < 4 ? i : 2]);
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t G = static_cast<uint64_t>(kGs[i]);
             uint32_t W4[4][256], W1[4][256], W2[4][256];
-            lvgpu::shift_tables(16ull * G * (i < 4 ? lvk::U : lvk::kTableRows), W4);
+            lvgpu::shift_tables(16ull * G * lvk::U, W4);
             lvgpu::shift_tables(16ull * G, W1);
             lvgpu::shift_tables(32ull * G, W2);
             std::vector<uint32_t> &im = images[i];
@@ -2306,7 +2275,7 @@ struct DevCtx {
     std::mutex m;  // one-time init
     bool ready = false;
     int cus = 0;
-    uint4 *image[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
     uint32_t *base_mats = nullptr;  // Shift_{2^i}, i < lvk::kBaseMats (combine_long_kernel)
     std::mutex ws_m;  // guards the map (entries are never erased)
     std::map<hipStream_t, std::unique_ptr<StreamWs>> ws;
@@ -2395,7 +2364,7 @@ int current_ctx(DevCtx **out) {
         hipDeviceProp_t prop;
         LV_HIP(hipGetDeviceProperties(&prop, dev));
         c.cus = prop.multiProcessorCount;
-        for (int i = 0; i < 5; ++i) {
+        for (int i = 0; i < 4; ++i) {
             const auto &im = host_image(i);
             LV_HIP(hipMalloc(&c.image[i], im.size() * 4));
             LV_HIP(hipMemcpy(c.image[i], im.data(), im.size() * 4, hipMemcpyHostToDevice));
@@ -2955,15 +2924,15 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     P.n = n;
     P.flags = 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (n + 3) / 4))), block(lvk::kTableThreads);
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (n + 3) / 4))), block(lvk::kThreads);
     if (seal) {
         lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
         g_kernel = "sst_blocks_kernel<seal>";
-        hipLaunchKernelGGL(lvk::sst_blocks_kernel<true>, grid, block, 0, s, P, c->image[4], u);
+        hipLaunchKernelGGL(lvk::sst_blocks_kernel<true>, grid, block, 0, s, P, c->image[2], u);
     } else {
         lvk::TableUnits<false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
         g_kernel = "sst_blocks_kernel<verify>";
-        hipLaunchKernelGGL(lvk::sst_blocks_kernel<false>, grid, block, 0, s, P, c->image[4], u);
+        hipLaunchKernelGGL(lvk::sst_blocks_kernel<false>, grid, block, 0, s, P, c->image[2], u);
     }
     return check_launch();
 }
