@@ -2092,11 +2092,13 @@ __device__ __forceinline__ uint32_t gf2_apply(const uint32_t *m, uint32_t v) {
     return r;
 }
 
+// Matrices sit in LDS at a stride of 33 words: lanes applying different
+// matrices (j = w - 1 - lane) then read 32 distinct banks.
 __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__restrict__ raw, uint64_t n, uint32_t s,
                                                              const uint32_t *__restrict__ mats,
                                                              uint32_t *__restrict__ out, uint32_t flags) {
-    __shared__ uint32_t M[65 * 32];
-    for (uint32_t i = threadIdx.x; i < 65 * 32; i += blockDim.x) M[i] = mats[i];
+    __shared__ uint32_t M[65 * 33];
+    for (uint32_t i = threadIdx.x; i < 65 * 32; i += blockDim.x) M[(i >> 5) * 33 + (i & 31u)] = mats[i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = s < 64 ? s : 64, reps = s <= 64 ? 1 : s / 64;
@@ -2104,13 +2106,13 @@ __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__r
     for (uint64_t b = static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6); b < n; b += nw) {
         uint32_t acc = 0;
         if (lane < w) {
-            uint32_t rv[16];  // all loads first: one memory latency per block
-#pragma unroll
-            for (uint32_t m = 0; m < 16; ++m) rv[m] = m < reps ? raw[b * s + lane + 64 * m] : 0u;
-#pragma unroll
-            for (uint32_t m = 0; m < 16; ++m)
-                if (m < reps) acc = (m ? gf2_apply(M + 64 * 32, acc) : 0u) ^ rv[m];
-            acc = gf2_apply(M + (w - 1 - lane) * 32, acc);
+            uint32_t nx = raw[b * s + lane];
+            for (uint32_t m = 0; m < reps; ++m) {  // wave-uniform count (an unrolled 16 ran dead shift bodies)
+                const uint32_t cur = nx;
+                if (m + 1 < reps) nx = raw[b * s + lane + 64 * (m + 1)];
+                acc = (m ? gf2_apply(M + 64 * 33, acc) : 0u) ^ cur;
+            }
+            acc = gf2_apply(M + (w - 1 - lane) * 33, acc);
         }
 #pragma unroll
         for (int k = 32; k >= 1; k >>= 1) acc ^= __shfl_xor(acc, k);
@@ -2149,21 +2151,21 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
         if (r.z == 0) continue;    // a claim past the piece budget: the buffer was walked whole
         uint32_t acc = 0;
         if (lane < r.z) {
-            constexpr uint32_t kJ = kMaxPieces / 64;  // pieces per lane, loads first
-            uint32_t rv[kJ];
-#pragma unroll
-            for (uint32_t j = 0; j < kJ; ++j) rv[j] = lane + 64 * j < r.z ? part[r.y + lane + 64 * j] : 0u;
             const uint32_t c = gf2_apply(M + r.w * 32, 0xffffffffu);  // Shift_P(~0)
-            rv[0] ^= lane ? c : 0u;
-#pragma unroll
-            for (uint32_t j = 1; j < kJ; ++j) rv[j] ^= c;
+            // a runtime (wave-uniform) row count: an unrolled loop over the
+            // 16 possible rows ran its shift bodies with no lane active
+            const uint32_t rows = (r.z + 63) / 64;
+            uint32_t nx = part[r.y + lane];
             uint32_t klast = lane;
-#pragma unroll
-            for (uint32_t j = 0; j < kJ; ++j)
-                if (lane + 64 * j < r.z) {
-                    acc = (j ? gf2_apply(M + (r.w + 6) * 32, acc) : 0u) ^ rv[j];
-                    klast = lane + 64 * j;
+            for (uint32_t j = 0; j < rows; ++j) {
+                const uint32_t k = lane + 64 * j;
+                const uint32_t cur = nx ^ (k ? c : 0u);
+                if (k + 64 < r.z) nx = part[r.y + k + 64];  // the next row's piece, in flight during the shift
+                if (k < r.z) {
+                    acc = (j ? gf2_apply(M + (r.w + 6) * 32, acc) : 0u) ^ cur;
+                    klast = k;
                 }
+            }
             const uint32_t d = r.z - 1 - klast;  // < 64
 #pragma unroll
             for (uint32_t b = 0; b < 6; ++b)
@@ -2447,7 +2449,11 @@ void launch_g(const DevCtx &c, int gi, const uint8_t *arena, const uint64_t *off
 #define LVK_SORT_MIN_WGS 1024
 #endif
 uint64_t sort_wgs(uint64_t n, uint64_t *chunk) {
-    constexpr uint64_t kSortMinWgs = LVK_SORT_MIN_WGS, kSortMinChunk = 1024;
+    constexpr uint64_t kSortMinWgs = LVK_SORT_MIN_WGS;
+    // small batches: >= 1 workgroup per 64 buffers (one wave each), so the
+    // long-buffer split's piece writes spread over the grid (1,024 x 64 KiB:
+    // one sorting workgroup wrote all 16,384 pieces, 33 us)
+    const uint64_t kSortMinChunk = n < 65536 ? 64 : 1024;
     uint64_t wgs = (n + lvk::kSortChunk - 1) / lvk::kSortChunk;
     const uint64_t small = std::min(kSortMinWgs, (n + kSortMinChunk - 1) / kSortMinChunk);
     if (wgs < small) wgs = small;
