@@ -1061,19 +1061,19 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
     // the wave writes every claimed buffer's piece entries (or blanks for
     // claims past the budget, so every slot below min(counter, budget) is
     // set), lane-parallel over the wave's pieces: the claiming lanes park
-    // their geometry in LDS and each slot finds its buffer by a binary search
-    // over the wave's inclusive prefix (a loop over the buffers with
-    // broadcasts ran ~75 us for 1,024 split buffers)
+    // their geometry in LDS; lane l writes slots l, l + 64, ... and walks a
+    // cursor over the wave's inclusive prefix (slots only grow, so the
+    // cursor moves ~once per slot: a loop over the buffers with broadcasts
+    // ran ~75 us for 1,024 split buffers, a binary search per slot -- six
+    // dependent LDS reads -- ~90 us for 64 x 256 pieces)
     const uint32_t w = threadIdx.x >> 6;
     g_split[w][lane] = make_uint4(static_cast<uint32_t>(o), static_cast<uint32_t>(o >> 32), L, s);
     g_split_pre[w][lane] = incl;
     g_split_p[w][lane] = p;
     __builtin_amdgcn_wave_barrier();
+    uint32_t j = 0;  // first lane with incl > u (u grows, so j only moves forward)
     for (uint32_t u = lane; u < tot; u += 64) {
-        uint32_t j = 0;  // first lane with incl > u
-#pragma unroll
-        for (uint32_t st = 32; st >= 1; st >>= 1)
-            if (g_split_pre[w][j + st - 1] <= u) j += st;
+        while (g_split_pre[w][j] <= u) ++j;
         const uint32_t mj = g_split_pre[w][j] - (j ? g_split_pre[w][j - 1] : 0u);
         const uint32_t k = u - (g_split_pre[w][j] - mj);  // piece index within buffer j
         const uint32_t slot = pb + u;
@@ -2599,8 +2599,8 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
                            0, s, P, c.image[2], ws);
     // joins split long buffers (exits at once when the sort split none)
     if (longs)
-        hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(64), dim3(256), 0, s, ws, longs, part, c.base_mats, out,
-                           flags);
+        hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(256), 0, s, ws, longs,
+                           part, c.base_mats, out, flags);
     return 0;
 }
 
