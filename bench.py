@@ -204,7 +204,8 @@ def measure_traffic(args):
     out = tempfile.mkdtemp(prefix="lvgpu_pmc_", dir="/tmp")
     cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
            sys.executable, os.path.abspath(__file__), "--steps", "10", "--warmup", "60", "--cpu-seconds", "0",
-           "--traffic", "off", "--workload", args.workload, "--api", args.api, "--scaling", args.scaling]
+           "--traffic", "off", "--no-settle", "--workload", args.workload, "--api", args.api,
+           "--scaling", args.scaling]  # bytes per launch do not depend on the clock state: no settle
     if args.group:
         cmd += ["--group", str(args.group)]
     if args.blocks:

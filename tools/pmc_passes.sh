@@ -13,7 +13,7 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
            "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --pmc $set --output-format csv -d "$out/p$i" -o pmc -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --traffic off "$@" > "$out/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$out/p$i.log"; }
+  timeout -k 10 180 rocprofv3 --pmc $set --output-format csv -d "$out/p$i" -o pmc -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --traffic off --no-settle "$@" > "$out/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$out/p$i.log"; }
 done
 python3 - "$out" <<'PY'
 import csv, glob, os, sys, collections
