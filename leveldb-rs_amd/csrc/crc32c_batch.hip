@@ -1053,11 +1053,13 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
     pb = __shfl(pb, 0);
     lb = __shfl(lb, 0);
     const uint32_t base = pb + incl - m;
-    const bool fits = m > 0 && static_cast<uint64_t>(base) + m <= kPieceBudget;
-    if (m > 0) {  // long record (m = 0 if over budget: combine_long_kernel skips it)
-        const uint32_t li = lb + static_cast<uint32_t>(__popcll(want & ((1ull << lane) - 1ull)));
+    // (both limits hold by construction -- sum of m <= 16,384 + 8,192 and at
+    // most 8,192 buffers longer than 2P >= batch bytes / 8,192 -- and are
+    // checked anyway: a claim past them leaves its buffer whole)
+    const uint32_t li = lb + static_cast<uint32_t>(__popcll(want & ((1ull << lane) - 1ull)));
+    const bool fits = m > 0 && static_cast<uint64_t>(base) + m <= kPieceBudget && li < kPieceBudget / 2;
+    if (m > 0 && li < kPieceBudget / 2)  // long record (m = 0 when not split: combine_long_kernel skips it)
         longs[li] = make_uint4(i, base, fits ? m : 0u, p);
-    }
     // the wave writes every claimed buffer's piece entries (or blanks for
     // claims past the budget, so every slot below min(counter, budget) is
     // set), lane-parallel over the wave's pieces: the claiming lanes park
@@ -1069,7 +1071,7 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
     const uint32_t w = threadIdx.x >> 6;
     g_split[w][lane] = make_uint4(static_cast<uint32_t>(o), static_cast<uint32_t>(o >> 32), L, s);
     g_split_pre[w][lane] = incl;
-    g_split_p[w][lane] = p;
+    g_split_p[w][lane] = p | (fits ? 0x100u : 0u);
     __builtin_amdgcn_wave_barrier();
     uint32_t j = 0;  // first lane with incl > u (u grows, so j only moves forward)
     for (uint32_t u = lane; u < tot; u += 64) {
@@ -1077,10 +1079,10 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
         const uint32_t mj = g_split_pre[w][j] - (j ? g_split_pre[w][j - 1] : 0u);
         const uint32_t k = u - (g_split_pre[w][j] - mj);  // piece index within buffer j
         const uint32_t slot = pb + u;
-        const bool fj = static_cast<uint64_t>(pb) + g_split_pre[w][j] <= kPieceBudget;
-        if (fj) {
+        const uint32_t pj = g_split_p[w][j];
+        if (pj & 0x100u) {  // buffer j was split
             const uint4 gj = g_split[w][j];
-            const uint64_t P = 1ull << g_split_p[w][j];
+            const uint64_t P = 1ull << (pj & 0xffu);
             const uint64_t first = gj.z - (static_cast<uint64_t>(mj) - 1) * P;  // piece 0: [0, first)
             // every piece is walked like a seed-0 buffer except piece 0,
             // which takes the buffer's seed: piece k > 0 yields R(~0, piece)
