@@ -86,3 +86,41 @@ def test_scalar_combine():
     assert lvgpu.combine(0x1234, lvgpu.value(b""), 0) == 0x1234
     big = bytes(range(256)) * 4096  # 1 MiB: a long shift
     assert lvgpu.combine(lvgpu.value(b"head"), lvgpu.value(big), len(big)) == lvgpu.value(b"head" + big)
+
+
+def test_argument_checks_before_any_device_call():
+    """Argument validation of the batch entry points happens before they touch
+    the GPU, with an error code and a message (no CPU fallback, no crash)."""
+    import lvgpu.wal as LW
+    L = lvgpu.lib()
+    W = LW._bind()
+    vp = ctypes.c_void_p
+    fake = vp(0x1000)  # never dereferenced: every call below fails its checks first
+    # strided: more than 2^32-1 blocks (ADVICE r01: output slots are 32-bit)
+    rc = L.lv_crc32c_batch_strided(fake, 16, 16, 1 << 32, None, fake, 0, None)
+    assert rc == -1 and b"2^32" in L.lv_last_error()
+    # device WAL scan: null count, misaligned log, workspace too small
+    assert W.lv_wal_scan_device(fake, 64, fake, fake, fake, 8, None, fake, 1 << 20, None) == -1
+    assert W.lv_wal_scan_device(vp(0x1004), 64, fake, fake, fake, 8, fake, fake, 1 << 20, None) == -1
+    assert b"aligned" in L.lv_last_error()
+    need = W.lv_wal_scan_workspace_bytes(64, 8)
+    assert need > 0
+    assert W.lv_wal_scan_device(fake, 64, fake, fake, fake, 8, fake, fake, need - 1, None) == -1
+    assert b"workspace" in L.lv_last_error()
+    # the workspace grows with the capacity, 16 B per entry
+    assert W.lv_wal_scan_workspace_bytes(64, 1008) - need == 1000 * 16
+    # kernel-choice query: empty on a thread that has launched nothing
+    import threading
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(L.lv_crc32c_last_kernel()))
+    t.start()
+    t.join()
+    assert seen == [b""]
+
+
+def test_workspace_bytes_cover_pieces():
+    """The offsets-API workspace holds n sorted entries plus the long-buffer
+    split's piece budget, whatever n."""
+    small, big = lvgpu.workspace_bytes(1), lvgpu.workspace_bytes(1 << 20)
+    assert small >= 65536 * 16  # the piece entries alone
+    assert big - small >= ((1 << 20) - 1) * 20  # 16-B entry + 4-B seed per buffer
