@@ -196,7 +196,20 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 // The LVK_EXP_* switches compute WRONG CRCs: a build that sets one must say
 // so explicitly (tools/build_variant.sh passes LVK_EXPERIMENT_BUILD=1 and
 // names the library a variant), so they can never reach the product library.
-#if (LVK_EXP_NOSHIFT || LVK_EXP_NOFOLD || LVK_EXP_NOSTAGE) && !defined(LVK_EXPERIMENT_BUILD)
+// Sorted-walk studies: LVK_EXP_NOTAIL skips the tail granule's fold,
+// LVK_EXP_NOFIX the head/end fix-ups of a round's rows, LVK_EXP_NOMERGE the
+// merge lookups (rows XORed) and the lane rotation.
+#ifndef LVK_EXP_NOTAIL
+#define LVK_EXP_NOTAIL 0
+#endif
+#ifndef LVK_EXP_NOFIX
+#define LVK_EXP_NOFIX 0
+#endif
+#ifndef LVK_EXP_NOMERGE
+#define LVK_EXP_NOMERGE 0
+#endif
+#if (LVK_EXP_NOSHIFT || LVK_EXP_NOFOLD || LVK_EXP_NOSTAGE || LVK_EXP_NOTAIL || LVK_EXP_NOFIX || LVK_EXP_NOMERGE) && \
+    !defined(LVK_EXPERIMENT_BUILD)
 #error "LVK_EXP_* timing switches compute wrong CRCs; define LVK_EXPERIMENT_BUILD for an experiment variant"
 #endif
 // NU rows per batch; W4OFF = LDS offset of the Latin row-shift table (the
@@ -1602,6 +1615,16 @@ __device__ __forceinline__ uint32_t round_jfix_al(const RGeo &q, uint32_t nbw) {
     return wave_max_u32(static_cast<uint32_t>(jh), 16);
 }
 
+// Granules outside the buffer's whole granules (d < 0: before its first
+// 256-B row's start, or padding rows; d > dmax: past its end) load from a
+// zero block instead of being zeroed after the load, so only the head batches
+// need a fix-up pass (fix_rbatch_al); the load address costs the same selects
+// a clamp would.
+#ifndef LVK_ZERO_PAGE
+#define LVK_ZERO_PAGE 1
+#endif
+__device__ __attribute__((aligned(256))) uint4 g_zero_granules[16];  // zero-initialised
+
 template <uint32_t NU>
 __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
                                                uint4 (&v)[NU]) {
@@ -1611,14 +1634,20 @@ __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) {
         int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
+#if LVK_ZERO_PAGE
+        const uint64_t ad = (d < 0 || d > dmax) ? reinterpret_cast<uint64_t>(&g_zero_granules[gl])
+                                                : ab + (static_cast<uint32_t>(d) << 4);
+#else
         d = d > dmax ? dmax : d;  // upper clamp first: a buffer with no whole granule has dmax = -1
         d = d < 0 ? 0 : d;
         const uint64_t ad = ab + (static_cast<uint32_t>(d) << 4);
+#endif
         v[i] = (LVK_AL_RT_LAST && i == NU - 1) ? load16_rt(ad) : load16(ad);
     }
 }
 
-// Head fix-up (as fix_rbatch) plus the zero granules past u_e.
+// Head fix-up (as fix_rbatch) plus, without the zero block, the zero
+// granules outside the buffer.
 template <uint32_t NU>
 __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
                                               uint4 (&v)[NU]) {
@@ -1629,9 +1658,13 @@ __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint3
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) {
         const int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
+#if LVK_ZERO_PAGE  // granules outside [0, dmax] were loaded from the zero block
+        if ((d == 0 || (d == 1 && alow > 12)) && d <= dmax) {
+#else
         if (d < 0 || d > dmax) {
             v[i] = make_uint4(0, 0, 0, 0);
         } else if (d == 0 || (d == 1 && alow > 12)) {
+#endif
             const int32_t rel = d * 16 - alow;
             v[i].x = fix_word(v[i].x, rel, s0);
             v[i].y = fix_word(v[i].y, rel + 4, s0);
@@ -1656,12 +1689,20 @@ __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a
     const AGeo g = al_geo(q);
     const bool early = static_cast<int32_t>(gl) > g.e;
     uint32_t X;
-    if constexpr (NU == 4) {
+    if constexpr (LVK_EXP_NOMERGE) {
+        X = early ? a3p : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < NU; ++i) X ^= A[i];
+        return X;
+    } else if constexpr (NU == 4) {
         const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
         const uint32_t x23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
         X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
+    } else if constexpr (NU == 3) {  // W1(W1(h0) ^ h1) ^ h2
+        const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
+        X = lookup4<kRegionB>(x01, L) ^ (early ? A[1] : A[2]);
     } else {  // NU = 2: W1(h0) ^ h1
-        static_assert(NU == 2, "aligned rows: 2 or 4 rows per batch");
+        static_assert(NU == 2, "aligned rows: 2, 3 or 4 rows per batch");
         X = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
     }
     if (rot) X = __shfl(X, static_cast<int32_t>((lane & ~15u) | ((gl + static_cast<uint32_t>(g.e) + 1u) & 15u)));
@@ -1695,10 +1736,12 @@ __device__ __forceinline__ uint32_t round_pad(const RGeo &q, uint32_t nbw) {
 template <int W4K, uint32_t NU, uint32_t W4OFF>
 __device__ __forceinline__ void fold_first(const uint4 (&v)[NU], uint32_t (&A)[NU], const Lut &L, uint32_t pad) {
 #if LVK_SKIP_PAD
-    if constexpr (NU == 4) {
-        if (pad == 3) {
-            fold_batch<true, W4K, NU, W4OFF, 3>(v, A, L);
-            return;
+    if constexpr (NU >= 3) {
+        if constexpr (NU == 4) {
+            if (pad == 3) {
+                fold_batch<true, W4K, NU, W4OFF, 3>(v, A, L);
+                return;
+            }
         }
         if (pad == 2) {
             fold_batch<true, W4K, NU, W4OFF, 2>(v, A, L);
@@ -1717,7 +1760,7 @@ __device__ __forceinline__ void fold_first(const uint4 (&v)[NU], uint32_t (&A)[N
 // xor and mask: the tail bytes, then the short-buffer seed.
 __device__ __forceinline__ uint32_t finish_raw(const RGeo &q, uint32_t X, const uint4 &tail, uint32_t gl,
                                                const Lut &L) {
-    X = fold_tail(X, tail, q, L);
+    if (!LVK_EXP_NOTAIL) X = fold_tail(X, tail, q, L);
     if (gl == 0 && q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for short buffers
         uint32_t s = ~q.seed;
         for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u);
@@ -1766,13 +1809,15 @@ struct SortedList {
 // loads and spills cost more than the conservative wait counts they remove.)
 // The image is always the G = 16 one: groups of G = 1 and 4 take their
 // row-shift and merge tables from the plain combine tables.
-template <int G, class Src, class Next>
+template <int G, class Src, class Next, uint32_t ALR = kAlRows>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {
     constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
-    constexpr uint32_t NU = AL ? kAlRows : U;          // rows per batch
-    // Latin row shift Shift_{16 G NU}: the image's W4 (NU = 4) or W2 (NU = 2)
-    constexpr uint32_t W4OFF = NU == 4 ? kRegionA + kHalf : kRegionB + kHalf;
+    constexpr uint32_t NU = AL ? ALR : U;              // rows per batch
+    // Latin row shift Shift_{16 G NU}: region A's second half (the image's W4
+    // for NU = 4; Shift_768 in the table image for NU = 3) or region B's W2
+    // (NU = 2)
+    constexpr uint32_t W4OFF = NU >= 3 ? kRegionA + kHalf : kRegionB + kHalf;
     constexpr uint32_t K = 64 / G;
     constexpr int W4K = G == 16 ? -1 : (G == 4 ? 4 : 2);  // Shift_{64G}
     constexpr int W1K = G == 16 ? -1 : (G == 4 ? 2 : 0);  // Shift_{16G}
@@ -1827,7 +1872,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             }
         }
         if constexpr (AL) {
-            if (j <= jfix || (lastj && rot)) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
+            if (!LVK_EXP_NOFIX && (j <= jfix || (!LVK_ZERO_PAGE && lastj && rot))) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
         } else if (j <= jfix) {
             fix_rbatch<G>(q, nbw, j, gl, cur);
         }
@@ -2062,6 +2107,16 @@ struct TableUnits {
     }
 };
 
+// Rows per batch of the table walk.  A 4,097-4,352-B unit at a byte-packed
+// start spans 17-19 rows of the 256-B grid: 5 four-row batches (20 rows) or
+// 6 three-row batches (18 rows, with Shift_768 as the batch shift: the table
+// image, host_image(kTableImage)).
+#ifndef LVK_SST_ROWS
+#define LVK_SST_ROWS 3
+#endif
+constexpr uint32_t kSstRows = LVK_SST_ROWS;
+static_assert(kSstRows == 3 || kSstRows == 4, "table walk: 3 or 4 rows per batch");
+
 template <bool SEAL>
 __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
                                                               TableUnits<SEAL> src) {
@@ -2076,7 +2131,7 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
         if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
         return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
     };
-    sorted_stream<16>(P, src, lane, L, pool(), pool);
+    sorted_stream<16, TableUnits<SEAL>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
 }
 
 // Joins the raw piece registers of the long-block split: block b's pieces
@@ -2226,10 +2281,15 @@ int set_err(int code, const std::string &msg) {
     } while (0)
 
 constexpr int kGs[4] = {1, 4, 16, 64};
+// The table walk's image: the G = 16 one with region A's row shift
+// Shift_{256 kSstRows} (Shift_768 for three-row batches).
+constexpr int kTableImage = 4;
+constexpr int kImages = 5;
 
-// Host copy of the LDS image for each G (index into kGs); layout in lvk.
+// Host copy of the LDS image for each G (index into kGs), and the table
+// image; layout in lvk.
 const std::vector<uint32_t> &host_image(int gi) {
-    static std::vector<uint32_t> images[4];
+    static std::vector<uint32_t> images[kImages];
     static std::once_flag once;
     std::call_once(once, [] {
         uint32_t T[4][256], C[6][4][256];
@@ -2259,6 +2319,13 @@ const std::vector<uint32_t> &host_image(int gi) {
                 for (int j = 0; j < 4; ++j)
                     for (int e = 0; e < 256; ++e) rc[(k * 4 + j) * 256 + e] = C[k][j][e];
         }
+        uint32_t WT[4][256];
+        lvgpu::shift_tables(256ull * lvk::kSstRows, WT);
+        images[kTableImage] = images[2];
+        uint32_t *ra = &images[kTableImage][lvk::kRegionA / 4];
+        for (int e = 0; e < 256; ++e)
+            for (int c = 0; c < 8; ++c)
+                for (int k = 0; k < 4; ++k) ra[e * 64 + 32 + 4 * c + k] = WT[3 - k][e];
     });
     return images[gi];
 }
@@ -2279,7 +2346,7 @@ struct DevCtx {
     std::mutex m;  // one-time init
     bool ready = false;
     int cus = 0;
-    uint4 *image[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint4 *image[kImages] = {};  // per G (kGs), then the table image
     uint32_t *base_mats = nullptr;  // Shift_{2^i}, i < lvk::kBaseMats (combine_long_kernel)
     std::mutex ws_m;  // guards the map (entries are never erased)
     std::map<hipStream_t, std::unique_ptr<StreamWs>> ws;
@@ -2368,7 +2435,7 @@ int current_ctx(DevCtx **out) {
         hipDeviceProp_t prop;
         LV_HIP(hipGetDeviceProperties(&prop, dev));
         c.cus = prop.multiProcessorCount;
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kImages; ++i) {
             const auto &im = host_image(i);
             LV_HIP(hipMalloc(&c.image[i], im.size() * 4));
             LV_HIP(hipMemcpy(c.image[i], im.data(), im.size() * 4, hipMemcpyHostToDevice));
@@ -2936,11 +3003,11 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     if (seal) {
         lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
         g_kernel = "sst_blocks_kernel<seal>";
-        hipLaunchKernelGGL(lvk::sst_blocks_kernel<true>, grid, block, 0, s, P, c->image[2], u);
+        hipLaunchKernelGGL(lvk::sst_blocks_kernel<true>, grid, block, 0, s, P, c->image[kTableImage], u);
     } else {
         lvk::TableUnits<false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
         g_kernel = "sst_blocks_kernel<verify>";
-        hipLaunchKernelGGL(lvk::sst_blocks_kernel<false>, grid, block, 0, s, P, c->image[2], u);
+        hipLaunchKernelGGL(lvk::sst_blocks_kernel<false>, grid, block, 0, s, P, c->image[kTableImage], u);
     }
     return check_launch();
 }

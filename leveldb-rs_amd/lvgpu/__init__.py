@@ -36,6 +36,12 @@ def _lib_path() -> str:
 
 
 LIB_PATH = _lib_path()
+
+
+def experiment_variant() -> bool:
+    """True when an experiment variant (tools/build_variant.sh) is loaded
+    instead of the product library: timing studies only, CRCs may be wrong."""
+    return LIB_PATH != PRODUCT_LIB
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "lvgpu", "crc32c.h")
 
 MASK = 0x1  # LV_CRC_MASK
