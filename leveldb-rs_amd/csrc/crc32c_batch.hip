@@ -208,7 +208,11 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 #ifndef LVK_EXP_NOMERGE
 #define LVK_EXP_NOMERGE 0
 #endif
-#if (LVK_EXP_NOSHIFT || LVK_EXP_NOFOLD || LVK_EXP_NOSTAGE || LVK_EXP_NOTAIL || LVK_EXP_NOFIX || LVK_EXP_NOMERGE) && \
+#ifndef LVK_EXP_NOSEALWRITE  // the seal computes its trailers but stores none
+#define LVK_EXP_NOSEALWRITE 0
+#endif
+#if (LVK_EXP_NOSHIFT || LVK_EXP_NOFOLD || LVK_EXP_NOSTAGE || LVK_EXP_NOTAIL || LVK_EXP_NOFIX || LVK_EXP_NOMERGE || \
+     LVK_EXP_NOSEALWRITE) && \
     !defined(LVK_EXPERIMENT_BUILD)
 #error "LVK_EXP_* timing switches compute wrong CRCs; define LVK_EXPERIMENT_BUILD for an experiment variant"
 #endif
@@ -2031,7 +2035,10 @@ struct TableUnits {
     uint32_t *status;      // verify: LV_SST_BLOCK_* per block
     uint32_t *crc_out;     // verify: optional crc32c(contents || type)
     uint64_t file_bytes;
-    static constexpr uint32_t kFlush = 8;  // 32 slots of four words (g_oidx, g_ocrc halves)
+    // seal: 64 slots of {block, masked crc} (16 rounds of 4 blocks per flush;
+    // the trailer stores are partial-line writes, and fewer, larger bursts of
+    // them measured faster); verify: 32 slots of four words
+    static constexpr uint32_t kFlush = SEAL ? 16 : 8;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
@@ -2064,11 +2071,8 @@ struct TableUnits {
         if constexpr (SEAL) {
             const uint32_t t = (q.aux >> 8) & 0xffu;
             const uint32_t crc = ~byte_step(X, t);
-            const uint64_t at = q.a + q.len;  // type byte, then LE32(mask(crc))
-            g_oidx[wave][slot] = static_cast<uint32_t>(at);
-            g_oidx[wave][32 + slot] = static_cast<uint32_t>(at >> 32);
+            g_oidx[wave][slot] = ok ? q.bid : 0xffffffffu;  // the flush re-reads the handle and type
             g_ocrc[wave][slot] = mask_crc(crc);
-            g_ocrc[wave][32 + slot] = t | (ok && q.bid != 0xffffffffu ? 0x100u : 0u);
         } else {
             const uint32_t crc = ~X;
             const uint32_t k = static_cast<uint32_t>(q.a + q.len) & 3u;
@@ -2081,22 +2085,24 @@ struct TableUnits {
             g_ocrc[wave][32 + slot] = ok ? crc : 0u;
         }
     }
-    __device__ __forceinline__ void flush(const Params &, uint32_t wave, uint32_t lane, uint32_t nslots) const {
-        const uint32_t sl = lane & 31u;
-        if (sl >= nslots) return;
+    __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
         if constexpr (SEAL) {
-            if (lane >= 32) return;
-            const uint32_t f = g_ocrc[wave][32 + sl];
-            if (!(f & 0x100u)) return;
-            uint8_t *p = reinterpret_cast<uint8_t *>((static_cast<uint64_t>(g_oidx[wave][32 + sl]) << 32) |
-                                                      g_oidx[wave][sl]);
-            const uint32_t m = g_ocrc[wave][sl];
+            if (lane >= nslots) return;
+            const uint32_t bi = g_oidx[wave][lane];
+            if (bi == 0xffffffffu || LVK_EXP_NOSEALWRITE) return;
+            const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
+            const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
+            uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
+            const uint32_t f = types ? types[bi] : 0u;
+            const uint32_t m = g_ocrc[wave][lane];
             p[0] = static_cast<uint8_t>(f);
             p[1] = static_cast<uint8_t>(m);
             p[2] = static_cast<uint8_t>(m >> 8);
             p[3] = static_cast<uint8_t>(m >> 16);
             p[4] = static_cast<uint8_t>(m >> 24);
         } else {
+            const uint32_t sl = lane & 31u;
+            if (sl >= nslots) return;
             const uint32_t bi = g_oidx[wave][sl];
             if (bi == 0xffffffffu) return;
             if (lane < 32)
