@@ -365,6 +365,7 @@ struct Params {
     const uint32_t *sseed;  // optional: seeds in sorted-entry order
     uint64_t nplain;        // sorted walk: entries [nplain, n) are long-buffer pieces
     uint32_t *part;         // piece registers (long-buffer split of the offsets API)
+    const uint32_t *mats;   // blocks kernel, FUSE: Shift_{j plen}, j < 2^pshift (32 column words each)
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of
@@ -696,9 +697,40 @@ __device__ __forceinline__ uint32_t final_crc(const Params &P, uint32_t X) {
 // v & (2^pshift - 1) of block v >> pshift (plen bytes each); piece 0 takes
 // the block's seed, the others start from a zero register, and the output is
 // the raw register R (no final xor, no mask) for combine_pieces_kernel.
-template <int G, bool SEEDED, bool PIECES = false>
+// FUSE (PIECES, <= kFuseMax pieces per block, one round: n <= 64 x grid):
+// a workgroup's 64 virtual blocks are whole blocks, so it joins their pieces
+// itself after one barrier -- the matrices Shift_{j plen} wait in g_oidx
+// (unused by this kernel), staged with the tables -- and there is no second
+// launch.
+constexpr uint32_t kFuseMax = 16;  // pieces per block; kFuseMax x 33 words fit g_oidx
+
+// R = sum of the columns of m selected by the bits of v (a GF(2) matrix-vector product).
+__device__ __forceinline__ uint32_t gf2_apply(const uint32_t *m, uint32_t v) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) r ^= (v >> j & 1u) ? m[j] : 0u;
+    return r;
+}
+
+// The fused combine (FUSE): wave 0 lane l holds WG-local piece l (wave l/4,
+// group l%4) -- piece k = l mod s of its block -- shifts it by Shift_{(s-1-k)
+// plen} and the s lanes of a block xor; the block's first lane stores.
+__device__ __forceinline__ void fuse_pieces(const Params &P, const uint32_t *fm, uint32_t (&res)[kWaves][64],
+                                            uint32_t lane, uint32_t wave) {
+    __syncthreads();  // every wave's piece registers are in res[w][0..3] (one round)
+    if (wave != 0) return;
+    const uint32_t s = 1u << P.pshift;
+    const uint64_t v = static_cast<uint64_t>(blockIdx.x) * 64u + lane;
+    const uint32_t k = lane & (s - 1u);
+    uint32_t acc = v < P.n ? gf2_apply(fm + (s - 1u - k) * 33u, res[lane >> 2][lane & 3u]) : 0u;
+    for (uint32_t d = s >> 1; d >= 1; d >>= 1) acc ^= __shfl_xor(acc, d);
+    if (v < P.n && k == 0) P.out[v >> P.pshift] = final_crc(P, acc);
+}
+static_assert(kFuseMax * 33 <= kWaves * 64, "fused combine matrices fit g_oidx");
+template <int G, bool SEEDED, bool PIECES = false, bool FUSE = false>
 __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint32_t nb,
                                                                  const uint4 *__restrict__ image) {
+    static_assert(!FUSE || (PIECES && G == 16), "fused combine: pieces of the G = 16 kernel");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     constexpr uint32_t kGroups = 64 / G;
@@ -737,10 +769,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     uint4 slot0[U], slot1[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) slot0[i] = load16(ptr + kRow * i);
+    uint32_t *const fm = &g_oidx[0][0];  // FUSE: matrix j at word 33 j (distinct banks per lane)
+    if constexpr (FUSE) {
+        const uint32_t nw = (1u << P.pshift) * 32u;
+        for (uint32_t i = threadIdx.x; i < nw; i += kThreads) fm[(i >> 5) * 33 + (i & 31u)] = P.mats[i];
+    }
 #if !LVK_EXP_NOSTAGE
     stage_tables(image);
 #endif
-    if (wblk0 >= P.n) return;
+    if (wblk0 >= P.n) {
+        if constexpr (FUSE) fuse_pieces(P, fm, g_ocrc, lane, wave);  // the barrier is workgroup-wide
+        return;
+    }
     // Blocks of >= 8 KiB: the waves of a CU start ~0.85 us apart.  Waves that
     // start together walk their blocks in lockstep, so all 16 K concurrent
     // streams sit at the same offset within their blocks, and at 8-64 KiB
@@ -785,7 +825,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
             // the wave's 64 slots every G rounds (and after the last round)
             const uint32_t X = merge_group<G, -1, -1, true>(A, L);
             if (gl == 0) g_ocrc[wave][(r % G) * kGroups + lane / G] = PIECES ? X : final_crc(P, X);
-            if ((r + 1) % G == 0 || r + 1 == rounds) {
+            if (!FUSE && ((r + 1) % G == 0 || r + 1 == rounds)) {
                 __builtin_amdgcn_wave_barrier();
                 const uint64_t r0 = r - r % G;
                 const uint64_t k = wblk0 + (r0 + lane / kGroups) * gstride + lane % kGroups;
@@ -813,6 +853,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         if (++j == nb) { j = 0; ++r; }
     }
     asm volatile("" ::"v"(st_val), "v"(st_ptr));
+    if constexpr (FUSE) fuse_pieces(P, fm, g_ocrc, lane, wave);
 }
 
 // Length classes of the offsets API.  Buffers are counting-sorted by key =
@@ -2148,13 +2189,6 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
 // by (min(s, 64) - 1 - l) plen; an xor over the wave, then ~ and the mask.
 // mats: 65 GF(2) matrices of 32 column images, Shift_{j plen} for j < 64 and
 // Shift_{64 plen} (built on the host, crc32c_gf2.h).
-__device__ __forceinline__ uint32_t gf2_apply(const uint32_t *m, uint32_t v) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) r ^= (v >> j & 1u) ? m[j] : 0u;
-    return r;
-}
-
 // Matrices sit in LDS at a stride of 33 words: lanes applying different
 // matrices (j = w - 1 - lane) then read 32 distinct banks.
 __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__restrict__ raw, uint64_t n, uint32_t s,
@@ -2896,6 +2930,30 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
         const uint64_t nv = static_cast<uint64_t>(n) << ps, plen = block_len >> ps;
         const uint32_t *mats = nullptr;
         if (int rc = piece_mats(*c, plen, &mats)) return rc;
+        const uint32_t nb = static_cast<uint32_t>(plen / (16ull * 16 * lvk::U));
+        if ((1u << ps) <= lvk::kFuseMax && nv <= 64ull * static_cast<uint64_t>(c->cus)) {
+            // one round of the grid: each workgroup joins its own blocks' pieces
+            lvk::Params P{};
+            P.base = reinterpret_cast<uint64_t>(d_base);
+            P.seed = d_seed;
+            P.out = d_out;
+            P.n = nv;
+            P.stride = stride;
+            P.blen = static_cast<uint32_t>(plen);
+            P.flags = flags;
+            P.plen = plen;
+            P.pshift = ps;
+            P.mats = mats;
+            const dim3 grid(static_cast<uint32_t>((nv + 63) / 64));
+            if (d_seed)
+                hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, true, true, true>), grid, dim3(lvk::kThreads), 0, hs,
+                                   P, nb, c->image[2]);
+            else
+                hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true, true>), grid, dim3(lvk::kThreads), 0,
+                                   hs, P, nb, c->image[2]);
+            g_kernel = "crc32c_blocks_kernel<16,pieces,fused>";
+            return check_launch();
+        }
         uint8_t *scr = nullptr;
         std::unique_lock<std::mutex> ws_lk;  // held through both launches
         if (int rc = stream_ws_bytes(*c, hs, nv * 4, &scr, &ws_lk)) return rc;
@@ -2909,7 +2967,6 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
         P.plen = plen;
         P.pshift = ps;
         const uint64_t grid = std::min<uint64_t>(c->cus, (nv + 63) / 64);
-        const uint32_t nb = static_cast<uint32_t>(plen / (16ull * 16 * lvk::U));
         if (d_seed)
             hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, true, true>), dim3(static_cast<uint32_t>(grid)),
                                dim3(lvk::kThreads), 0, hs, P, nb, c->image[2]);

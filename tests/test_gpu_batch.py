@@ -494,16 +494,37 @@ def test_kernel_choice_query(torch_dev):
     torch.cuda.synchronize()
 
 
+def _split_kernel(n, blen, cus):
+    """The strided API's long-block split as lv_crc32c_batch_strided picks it
+    (pick_split): 2^ps pieces of >= 4 KiB (whole KiB) until n 2^ps fills one
+    pass of the grid; <= 16 pieces per block in one pass join in the same
+    launch (FUSE), otherwise combine_pieces_kernel follows."""
+    want, ps = 4 * cus * 16, 0
+    while (n << ps) < want and ps < 10:
+        s2 = 2 << ps
+        if blen % s2 or (blen // s2) % 1024 or blen // s2 < 4096:
+            break
+        ps += 1
+    if (1 << ps) <= 16 and (n << ps) <= 64 * cus:
+        return "crc32c_blocks_kernel<16,pieces,fused>"
+    return "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel"
+
+
 @pytest.mark.parametrize("n,blen,seeded,masked", [(1, 16 << 20, False, False), (3, 1 << 20, True, True),
                                                   (64, 16 << 20, True, False), (1024, 65536, False, True),
+                                                  (1024, 65536, True, False), (1001, 65536, True, True),
+                                                  (2048, 32768, True, True), (4096, 16384, False, False),
+                                                  (300, 65536, False, False), (1500, 65536, True, False),
                                                   (5, 8192, True, False), (200, 12288, False, False),
                                                   (7, 3 << 20, True, True)])
 def test_strided_long_block_split(torch_dev, n, blen, seeded, masked):
     """Few long blocks through lv_crc32c_batch_strided: each block is cut into
     2^k pieces that fill the grid and the piece registers are joined on the
-    device (combine_pieces_kernel) -- the reference bench's 1 MiB and 16 MiB
+    device (in the same launch for <= 16 pieces per block in one grid pass,
+    else combine_pieces_kernel) -- the reference bench's 1 MiB and 16 MiB
     buffers (benches/crc32c.rs:59-60) and 1,024 x 64 KiB, bit-exact."""
     torch, dev = torch_dev
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
     stride = blen + (0 if n % 2 else 4096)
     base = torch.empty(stride * n + 64, dtype=torch.uint8, device=dev)
     lvgpu.fill_splitmix(base, 0, 0x51D + n)
@@ -511,7 +532,7 @@ def test_strided_long_block_split(torch_dev, n, blen, seeded, masked):
     seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if seeded else None
     sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
     out = lvgpu.batch_strided(base, stride, blen, n, seed=sd, masked=masked)
-    assert lvgpu.last_kernel() == "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel"
+    assert lvgpu.last_kernel() == _split_kernel(n, blen, cus)
     got = out.cpu().numpy().view(np.uint32)
     host = base.cpu().numpy().tobytes()
     want = oracle_batch(host, np.arange(n, dtype=np.uint64) * stride, np.full(n, blen, np.uint32), seeds, masked)
