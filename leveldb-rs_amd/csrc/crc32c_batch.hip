@@ -1131,15 +1131,26 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
     g_split_pre[w][lane] = incl;
     g_split_p[w][lane] = p | (fits ? 0x100u : 0u);
     __builtin_amdgcn_wave_barrier();
-    uint32_t j = 0;  // first lane with incl > u (u grows, so j only moves forward)
+    // Buffer j's prefix pair and geometry stay in registers and are re-read
+    // only when the cursor moves (every m / 64 slots), so a slot costs no
+    // dependent LDS read (with one per slot: 62 us for 64 x 256 pieces).
+    uint32_t j = 0;                        // first lane with incl > u (u grows, so j only moves forward)
+    uint32_t pre = g_split_pre[w][0], prv = 0;  // incl of lanes j and j - 1
+    uint4 gj = g_split[w][0];
+    uint32_t pj = g_split_p[w][0];
     for (uint32_t u = lane; u < tot; u += 64) {
-        while (g_split_pre[w][j] <= u) ++j;
-        const uint32_t mj = g_split_pre[w][j] - (j ? g_split_pre[w][j - 1] : 0u);
-        const uint32_t k = u - (g_split_pre[w][j] - mj);  // piece index within buffer j
+        if (pre <= u) {
+            do {
+                prv = pre;
+                pre = g_split_pre[w][++j];
+            } while (pre <= u);
+            gj = g_split[w][j];
+            pj = g_split_p[w][j];
+        }
+        const uint32_t mj = pre - prv;
+        const uint32_t k = u - prv;  // piece index within buffer j
         const uint32_t slot = pb + u;
-        const uint32_t pj = g_split_p[w][j];
         if (pj & 0x100u) {  // buffer j was split
-            const uint4 gj = g_split[w][j];
             const uint64_t P = 1ull << (pj & 0xffu);
             const uint64_t first = gj.z - (static_cast<uint64_t>(mj) - 1) * P;  // piece 0: [0, first)
             // every piece is walked like a seed-0 buffer except piece 0,
@@ -2561,8 +2572,10 @@ uint64_t sort_wgs(uint64_t n, uint64_t *chunk) {
     constexpr uint64_t kSortMinWgs = LVK_SORT_MIN_WGS;
     // small batches: >= 1 workgroup per 64 buffers (one wave each), so the
     // long-buffer split's piece writes spread over the grid (1,024 x 64 KiB:
-    // one sorting workgroup wrote all 16,384 pieces, 33 us)
-    const uint64_t kSortMinChunk = n < 65536 ? 64 : 1024;
+    // one sorting workgroup wrote all 16,384 pieces, 33 us); the fewest
+    // buffers go one (<= 256) or 16 (<= 4,096) per workgroup (64 x 16 MiB:
+    // one wave wrote 64 x 256 pieces, 42 us)
+    const uint64_t kSortMinChunk = n <= 256 ? 1 : n <= 4096 ? 16 : n < 65536 ? 64 : 1024;
     uint64_t wgs = (n + lvk::kSortChunk - 1) / lvk::kSortChunk;
     const uint64_t small = std::min(kSortMinWgs, (n + kSortMinChunk - 1) / kSortMinChunk);
     if (wgs < small) wgs = small;
