@@ -2021,6 +2021,9 @@ constexpr uint32_t kPoolWord = (kComb + 5 * 4096) / 4;
 // every workgroup walking every class in turn, with the image restaged per
 // G -- the small classes ran alone, latency- and VALU-bound, for ~100 us of
 // C2's 1.2 ms.)
+#ifndef LVK_CLASS_STAGGER
+#define LVK_CLASS_STAGGER 1
+#endif
 template <bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, const uint4 *__restrict__ image,
                                                                   const uint32_t *ws) {
@@ -2053,6 +2056,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         if (cls[5]) sorted_stream<4>(sub_list(P, cls[1], cls[5]), SortedList<SEEDED>(), lane, L, sw, stride);
     }
     if (n23) {
+#if LVK_CLASS_STAGGER
+        // A list of mostly long-buffer pieces (>= 3/4 of the entries), with
+        // >= 64 KiB per wave, is the blocks kernel's long-block regime: waves
+        // that start together stream their pieces in lockstep, which reads
+        // slower; stagger them as crc32c_blocks_kernel does (64 x 16 MiB:
+        // 223 -> 201 us per call).
+        const uint64_t bytes = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];
+        if (4ull * np >= 3ull * (n23 + np) && bytes >= (64ull << 10) * grid * kWaves)
+            for (uint32_t k = 0; k < wave * LVK_STAGGER; ++k) __builtin_amdgcn_s_sleep(32);
+#endif
         auto pool = [&]() -> uint64_t {
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
@@ -2719,7 +2732,11 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     else
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<false>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads),
                            0, s, P, c.image[2], ws);
-    // joins split long buffers (exits at once when the sort split none)
+    // joins split long buffers (exits at once when the sort split none).  (A
+    // last-finisher join inside the class kernel -- agent-scope release and
+    // acquire around a per-buffer counter -- measured 64 x 16 MiB 200 -> 345
+    // us and 1,024 x 64 KiB 41 -> 177 us: every fence writes back or
+    // invalidates the XCD's whole L2; and C3 via offsets -2 % from spills.)
     if (longs)
         hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(256), 0, s, ws, longs,
                            part, c.base_mats, out, flags);
