@@ -2093,7 +2093,7 @@ __device__ __forceinline__ bool sst_in_range(uint64_t o, uint64_t sz, uint64_t f
     return sz < 0xffffffffull && o <= file_bytes && sz <= file_bytes - o && file_bytes - o - sz >= 5u;
 }
 
-template <bool SEAL>
+template <bool SEAL, bool CRCOUT = false>
 struct TableUnits {
     const uint2 *handles;  // {offset, size} u64 pairs per block
     const uint8_t *types;  // seal: per-block type byte (NULL: 0 = no compression)
@@ -2102,8 +2102,9 @@ struct TableUnits {
     uint64_t file_bytes;
     // seal: 64 slots of {block, masked crc} (16 rounds of 4 blocks per flush;
     // the trailer stores are partial-line writes, and fewer, larger bursts of
-    // them measured faster); verify: 32 slots of four words
-    static constexpr uint32_t kFlush = SEAL ? 16 : 8;
+    // them measured faster); verify: 64 slots of {block, status}, or with
+    // crc_out 32 slots of four words
+    static constexpr uint32_t kFlush = SEAL || !CRCOUT ? 16 : 8;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
@@ -2147,7 +2148,7 @@ struct TableUnits {
                                     : (((r >> 17) | (r << 15)) == crc ? LV_SST_BLOCK_OK : LV_SST_BLOCK_CHECKSUM_MISMATCH);
             g_oidx[wave][slot] = q.bid;
             g_ocrc[wave][slot] = st;
-            g_ocrc[wave][32 + slot] = ok ? crc : 0u;
+            if (CRCOUT) g_ocrc[wave][32 + slot] = ok ? crc : 0u;
         }
     }
     __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
@@ -2165,6 +2166,10 @@ struct TableUnits {
             p[2] = static_cast<uint8_t>(m >> 8);
             p[3] = static_cast<uint8_t>(m >> 16);
             p[4] = static_cast<uint8_t>(m >> 24);
+        } else if constexpr (!CRCOUT) {
+            if (lane >= nslots) return;
+            const uint32_t bi = g_oidx[wave][lane];
+            if (bi != 0xffffffffu) status[bi] = g_ocrc[wave][lane];
         } else {
             const uint32_t sl = lane & 31u;
             if (sl >= nslots) return;
@@ -2188,9 +2193,9 @@ struct TableUnits {
 constexpr uint32_t kSstRows = LVK_SST_ROWS;
 static_assert(kSstRows == 3 || kSstRows == 4, "table walk: 3 or 4 rows per batch");
 
-template <bool SEAL>
+template <bool SEAL, bool CRCOUT>
 __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
-                                                              TableUnits<SEAL> src) {
+                                                              TableUnits<SEAL, CRCOUT> src) {
     stage_tables(image);
     if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
     __syncthreads();
@@ -2202,7 +2207,7 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
         if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
         return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
     };
-    sorted_stream<16, TableUnits<SEAL>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
+    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
 }
 
 // Joins the raw piece registers of the long-block split: block b's pieces
@@ -3083,6 +3088,9 @@ int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath
 }
 
 // SSTable trailers (csrc/sst.hip): one sst_blocks_kernel launch.
+#ifndef LVK_VERIFY_WIDE  // experiment: the four-word verify staging even without crc_out
+#define LVK_VERIFY_WIDE 0
+#endif
 int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, const uint64_t *d_handles,
                       const uint8_t *d_types, size_t n, uint32_t *d_status, uint32_t *d_crc, void *stream) {
     DevCtx *c = nullptr;
@@ -3096,11 +3104,16 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     if (seal) {
         lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
         g_kernel = "sst_blocks_kernel<seal>";
-        hipLaunchKernelGGL(lvk::sst_blocks_kernel<true>, grid, block, 0, s, P, c->image[kTableImage], u);
+        hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P, c->image[kTableImage], u);
+    } else if (d_crc || LVK_VERIFY_WIDE) {
+        lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
+        g_kernel = "sst_blocks_kernel<verify,crc>";
+        hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, true>), grid, block, 0, s, P, c->image[kTableImage], u);
     } else {
-        lvk::TableUnits<false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
+        lvk::TableUnits<false, false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, nullptr,
+                                        file_bytes};
         g_kernel = "sst_blocks_kernel<verify>";
-        hipLaunchKernelGGL(lvk::sst_blocks_kernel<false>, grid, block, 0, s, P, c->image[kTableImage], u);
+        hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, false>), grid, block, 0, s, P, c->image[kTableImage], u);
     }
     return check_launch();
 }

@@ -193,7 +193,10 @@ def test_gpu_table_one_launch_any_order(gpu):
     want = _oracle_seal(file, handles, types.tolist())
     assert d.cpu().numpy().tobytes() == want
     st, crc = LT.verify_blocks(d, h, out_crc=True)
-    assert lvgpu.last_kernel() == "sst_blocks_kernel<verify>"
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<verify,crc>"
     assert st.cpu().numpy().tolist() == [0] * len(handles)
     got = crc.cpu().numpy().view(np.uint32).tolist()
     assert got == [W.value(want[o:o + sz + 1]) for o, sz in handles]
+    st = LT.verify_blocks(d, h)  # status only: the two-word staging
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<verify>"
+    assert st.cpu().numpy().tolist() == [0] * len(handles)
