@@ -1228,16 +1228,15 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
 // block (one thread per block) and counts the records' CRC units
 // [type || payload] (log_reader.rs:336) into the length-sort histogram, plus
 // the records per block, and keeps each block's first kHdrCache headers; sort_scan
-// is shared; wal_scatter takes those headers from the cache (one independent
-// load each instead of a dependent chain step), walks on only for blocks
-// with more records, and writes every record straight into its sorted slot,
-// plus its log-order header offset and info word.  The class kernel then checksums the
+// is shared; wal_scatter takes those headers from the cache, one thread per
+// record (no dependent chain step), walks on only for blocks with more
+// records, and writes every record straight into its sorted slot, plus its
+// log-order header offset and info word.  The class kernel then checksums the
 // units.  Four launches, no host synchronisation (round 1: count pass, hipCUB
 // scan, host readback of the total, emit pass, then the whole offsets API).
 constexpr uint32_t kWalBlock = 32768;  // log_format.rs:63
 constexpr uint32_t kWalHeader = 7;     // log_format.rs:66
 constexpr uint32_t kHdrCache = 64;     // headers per block wal_hist keeps for wal_scatter
-constexpr uint32_t kHdrChunk = 8;      // cached headers wal_scatter requests at once
 
 // A cached header: position in its block | length << 16 | type << 32.
 __device__ __forceinline__ uint64_t hdr_pack(uint32_t pos, uint32_t len, uint32_t type) {
@@ -1248,8 +1247,10 @@ __device__ __forceinline__ uint64_t hdr_pack(uint32_t pos, uint32_t len, uint32_
 // 8-B words, each read only if it holds a byte of the log (an aligned word
 // never crosses a page), and a funnel shift.  (A per-thread 64-B LDS window
 // of the log, which would keep several short records' headers per load,
-// measured slower: wal_hist 36.6 -> 41.6 us.  The chains that bound the
-// walk are hops over longer records, one HBM round trip each.)
+// measured slower: wal_hist 36.6 -> 41.6 us; so did a 64-B register window
+// parsed divergently, one load per record that leaves it: 38.9 -> 49.6 us.
+// The chains that bound the walk are hops over longer records, one HBM
+// round trip each.)
 __device__ __forceinline__ uint64_t wal_load8(const uint8_t *log, uint64_t size, uint64_t pos) {
     const uint64_t a = pos & ~7ull;
     const uint64_t *w = reinterpret_cast<const uint64_t *>(log + a);
@@ -1266,9 +1267,7 @@ struct WalRec {
     uint32_t len, type, status, ulen;
 };
 
-__device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, uint64_t start, uint32_t blen,
-                                             uint32_t pos) {
-    const uint64_t h = wal_load8(log, size, start + pos);  // crc(4) | length(2) | type(1)
+__device__ __forceinline__ WalRec wal_decode(uint64_t h, uint32_t blen, uint32_t pos) {  // crc(4) | length(2) | type(1)
     WalRec r;
     r.len = static_cast<uint32_t>(h >> 32) & 0xffffu;
     r.type = static_cast<uint32_t>(h >> 48) & 0xffu;
@@ -1279,6 +1278,11 @@ __device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, 
         r.status = LV_WAL_REC_ZERO;        // log_reader.rs:326-331
     r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
     return r;
+}
+
+__device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, uint64_t start, uint32_t blen,
+                                             uint32_t pos) {
+    return wal_decode(wal_load8(log, size, start + pos), blen, pos);
 }
 
 __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
@@ -1368,7 +1372,7 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
         const uint64_t b = b0 + t;
         const uint32_t c = b < hi ? blkcnt[b] : 0u;
-        red[t] = c;  // exclusive scan of the block counts (Hillis-Steele in LDS)
+        red[t] = c;  // inclusive scan of the block counts (Hillis-Steele in LDS)
         __syncthreads();
         for (uint32_t d = 1; d < kSortThreads; d <<= 1) {
             const uint64_t x = t >= d ? red[t - d] : 0u;
@@ -1376,72 +1380,77 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
             red[t] += x;
             __syncthreads();
         }
-        uint64_t rid = run + red[t] - c;  // log-order index of this block's first record
-        run += red[kSortThreads - 1];
-        __syncthreads();
-        const uint64_t start = b * kWalBlock;
-        const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
-        uint32_t pos = 0;
-        bool active = c > 0;
-        // the first kHdrCache records of every block, from the cache, in
-        // chunks of kHdrChunk requested one chunk ahead (k is wave-uniform:
-        // every lane of the wave is at its block's k-th record)
-        uint64_t hc[kHdrChunk], hn[kHdrChunk];
-#pragma unroll
-        for (uint32_t q = 0; q < kHdrChunk; ++q) hc[q] = q < c ? hcache[b * kHdrCache + q] : 0u;
-        for (uint32_t k0 = 0; k0 < kHdrCache; k0 += kHdrChunk) {
-            if (!__any(active)) break;  // wave-uniform
-#pragma unroll
-            for (uint32_t q = 0; q < kHdrChunk; ++q) {
-                const uint32_t k = k0 + kHdrChunk + q;
-                hn[q] = k < c && k < kHdrCache ? hcache[b * kHdrCache + k] : 0u;
-            }
-#pragma unroll
-        for (uint32_t q = 0; q < kHdrChunk; ++q) {
-            const uint32_t k = k0 + q;
-            if (!__any(active)) break;  // wave-uniform
+        const uint32_t tot = static_cast<uint32_t>(red[kSortThreads - 1]);  // records of these blocks
+        // The chunk's cached records, thread-parallel in log order: record q
+        // belongs to the block j whose inclusive prefix first exceeds q (a
+        // binary search over red), as its record k = q - excl(j).  (Round 2
+        // first ran one thread per block over its records: a wave then took
+        // as many claim-and-store steps as its longest block has records,
+        // ~30 us for the bench log.)
+        for (uint32_t q0 = 0; q0 < tot; q0 += kSortThreads) {  // block-uniform
+            const uint32_t q = q0 + t;
+            uint32_t j = 0;
+            for (uint32_t step = kSortThreads / 2; step >= 1; step >>= 1)
+                if (red[j + step - 1] <= q) j += step;
+            const uint32_t ex = j ? static_cast<uint32_t>(red[j - 1]) : 0u;
+            const uint32_t k = q - ex;
+            const bool rec = q < tot && k < kHdrCache;
+            const uint64_t bj = b0 + j;
+            const uint64_t start = bj * kWalBlock;
             WalRec r{};
-            const bool rec = active;
-            if (active) {
-                pos = static_cast<uint32_t>(hc[q]) & 0xffffu;
-                r.len = static_cast<uint32_t>(hc[q] >> 16) & 0xffffu;
-                r.type = static_cast<uint32_t>(hc[q] >> 32) & 0xffu;
+            uint32_t pos = 0;
+            if (rec) {
+                const uint64_t h = hcache[bj * kHdrCache + k];
+                const uint32_t blen = static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock);
+                pos = static_cast<uint32_t>(h) & 0xffffu;
+                r.len = static_cast<uint32_t>(h >> 16) & 0xffffu;
+                r.type = static_cast<uint32_t>(h >> 32) & 0xffu;
                 r.status = kWalHeader + r.len > blen - pos ? LV_WAL_REC_BAD_LENGTH
                                                            : (r.type == 0 && r.len == 0 ? LV_WAL_REC_ZERO : LV_WAL_REC_OK);
                 r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
             }
             const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
             if (rec) {
+                const uint64_t rid = run + q;  // log order: blocks in order, records in chain order
                 const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
                 ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
                                        static_cast<uint32_t>(rid));
                 o.hdr_off[rid] = start + pos;
                 o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
-                ++rid;
-                pos += kWalHeader + r.len;
-                active = k + 1 < c;
             }
         }
-#pragma unroll
-            for (uint32_t q = 0; q < kHdrChunk; ++q) hc[q] = hn[q];
-        }
-        // blocks with more records walk on from there
-        while (__any(active)) {
-            WalRec r{};
-            const bool rec = active;
-            if (active) r = wal_record(log, size, start, blen, pos);
-            const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
-            if (rec) {
-                const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
-                ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
-                                       static_cast<uint32_t>(rid));
-                o.hdr_off[rid] = start + pos;
-                o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
-                ++rid;
-                pos += kWalHeader + r.len;
-                active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
+        // blocks with more records than the cache holds walk on from there
+        // (one thread per block; rare: a 32 KiB block holds > 64 records only
+        // when most of them are a few bytes long)
+        {
+            const uint64_t start = b * kWalBlock;
+            const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
+            bool active = c > kHdrCache;
+            uint32_t pos = 0;
+            uint64_t rid = run + static_cast<uint64_t>(red[t]) - c + kHdrCache;
+            if (active) {
+                const uint64_t h = hcache[b * kHdrCache + kHdrCache - 1];
+                pos = (static_cast<uint32_t>(h) & 0xffffu) + kWalHeader + (static_cast<uint32_t>(h >> 16) & 0xffffu);
+            }
+            while (__any(active)) {
+                WalRec r{};
+                const bool rec = active;
+                if (active) r = wal_record(log, size, start, blen, pos);
+                const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
+                if (rec) {
+                    const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
+                    ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
+                                           static_cast<uint32_t>(rid));
+                    o.hdr_off[rid] = start + pos;
+                    o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
+                    ++rid;
+                    pos += kWalHeader + r.len;
+                    active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
+                }
             }
         }
+        run += tot;
+        __syncthreads();  // red is rewritten by the next chunk
     }
 }
 
