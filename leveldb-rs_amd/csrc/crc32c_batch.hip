@@ -2102,6 +2102,9 @@ __device__ __forceinline__ bool sst_in_range(uint64_t o, uint64_t sz, uint64_t f
     return sz < 0xffffffffull && o <= file_bytes && sz <= file_bytes - o && file_bytes - o - sz >= 5u;
 }
 
+#ifndef LVK_SEAL_FLUSH  // rounds per seal flush (<= 16: 64 two-word slots)
+#define LVK_SEAL_FLUSH 16
+#endif
 template <bool SEAL, bool CRCOUT = false>
 struct TableUnits {
     const uint2 *handles;  // {offset, size} u64 pairs per block
@@ -2113,7 +2116,7 @@ struct TableUnits {
     // the trailer stores are partial-line writes, and fewer, larger bursts of
     // them measured faster); verify: 64 slots of {block, status}, or with
     // crc_out 32 slots of four words
-    static constexpr uint32_t kFlush = SEAL || !CRCOUT ? 16 : 8;
+    static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
