@@ -897,6 +897,10 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
 constexpr uint32_t kWsPieces = 0;
 constexpr uint32_t kWsLongs = 1;
 constexpr uint32_t kWsBytes = 2;
+#ifndef LVK_IDENT
+#define LVK_IDENT 1
+#endif
+constexpr uint32_t kWsIdent = 4;  // 1: the sorted list is the identity (one key, no split): see sort_scatter
 constexpr uint32_t kPieceBudget = 65536;  // piece entries per call (each split buffer takes <= kMaxPieces)
 constexpr uint32_t kMaxPieces = 1024;
 constexpr uint32_t kPieceFlag = 0x80000000u;  // output slot flag of a piece entry (slot < kPieceBudget)
@@ -1181,11 +1185,23 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
     const uint32_t mrow = M[static_cast<uint64_t>(blockIdx.x) * kKeys + t];
     const uint32_t ks = key_starts(ws, sc);
     cur[t] = ks + mrow;
+    // A batch whose buffers all share one key (uniform lengths: the C3-like
+    // case) is already "sorted" in index order; if none of them can be split
+    // (classes 0-1 never are; class 2 only above 16 KiB and only in batches
+    // of < 16,384 buffers, since a split needs L > 2P >= batch bytes / 8,192)
+    // the class kernel reads off/len/seed directly and the scatter is skipped.
+    const uint32_t tk = ws[kWsTot + t];
+    const bool ident_key = tk == static_cast<uint32_t>(n);  // this thread's key holds every buffer
+    const uint32_t kc = t / kBuckets, knb = kBuckets - 1 - t % kBuckets;
+    const bool ident_ok = ident_key && (kc <= 1 || (kc == 2 && (knb <= 16 || n >= 16384)));
+    const bool ident = __syncthreads_or(LVK_IDENT && ident_ok);
     if (blockIdx.x == 0 && t % kBuckets == 0) {  // per-class [start, count) for the CRC kernel
         const uint32_t c = t / kBuckets;
         ws[kWsCls + c] = ks;
         ws[kWsCls + 4 + c] = sc[t + kBuckets - 1] - ks;
     }
+    if (blockIdx.x == 0 && t == 0) ws[kWsIdent] = ident ? 1u : 0u;
+    if (ident) return;  // block-uniform
     __syncthreads();
     const uint64_t total = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
@@ -1355,7 +1371,10 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
         ws[kWsCls + c] = over ? 0u : ks;
         ws[kWsCls + 4 + c] = over ? 0u : sc[t + kBuckets - 1] - ks;
     }
-    if (blockIdx.x == 0 && t == 0) *o.count = total;
+    if (blockIdx.x == 0 && t == 0) {
+        *o.count = total;
+        ws[kWsIdent] = 0u;  // the class kernel reads the sorted entries
+    }
     // this workgroup's first record in log order: the records of the ones before
     uint64_t pre = 0;
     for (uint32_t v = t; v < blockIdx.x; v += kSortThreads) pre += wgrec[v];
@@ -1842,7 +1861,19 @@ __device__ __forceinline__ uint32_t finish_raw(const RGeo &q, uint32_t X, const 
 template <bool SEEDED>
 struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
-    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const { return load_rgeo<SEEDED>(P, e); }
+    bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
+    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
+        if (!ident) return load_rgeo<SEEDED>(P, e);
+        const bool valid = e < P.n;
+        const uint64_t ec = valid ? e : P.n - 1;
+        RGeo q;
+        q.len = P.len[ec];
+        q.a = q.len ? P.base + P.off[ec] : P.base;  // an empty buffer reads nothing of its own
+        q.seed = SEEDED ? P.seed[ec] : 0u;
+        q.bid = valid ? static_cast<uint32_t>(ec) : 0xffffffffu;
+        q.aux = 0;
+        return q;
+    }
     __device__ __forceinline__ uint2 trailer(const RGeo &, uint32_t) const { return make_uint2(0, 0); }
     // A piece parks its raw register for combine_long_kernel; its output slot
     // is its piece slot with the top bit set (piece slots are < kPieceBudget,
@@ -2037,6 +2068,7 @@ template <bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, const uint4 *__restrict__ image,
                                                                   const uint32_t *ws) {
     const uint32_t *cls = ws + kWsCls;
+    const bool ident = ws[kWsIdent] != 0u;  // sort_scatter skipped a one-key batch
     stage_tables(image);
     if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
     __syncthreads();
@@ -2059,10 +2091,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         uint64_t k = 0;
         auto stride = [&]() { return sw + (++k) * nsw; };
         if (cls[4]) {
-            sorted_stream<1>(sub_list(P, cls[0], cls[4]), SortedList<SEEDED>(), lane, L, sw, stride);
+            sorted_stream<1>(sub_list(P, cls[0], cls[4]), SortedList<SEEDED>{ident}, lane, L, sw, stride);
             k = 0;
         }
-        if (cls[5]) sorted_stream<4>(sub_list(P, cls[1], cls[5]), SortedList<SEEDED>(), lane, L, sw, stride);
+        if (cls[5]) sorted_stream<4>(sub_list(P, cls[1], cls[5]), SortedList<SEEDED>{ident}, lane, L, sw, stride);
     }
     if (n23) {
 #if LVK_CLASS_STAGGER
@@ -2080,7 +2112,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
             if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
             return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
         };
-        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), SortedList<SEEDED>(), lane, L, pool(),
+        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), SortedList<SEEDED>{ident}, lane, L, pool(),
                           pool);
     }
 }

@@ -576,3 +576,29 @@ def test_offsets_api_long_buffers(torch_dev, case, seeded):
     want = oracle_batch(arena.cpu().numpy().tobytes(), offs, sizes, seeds, True)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(i), sizes[i]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("n,size,seeded", [(20000, 3000, True), (5000, 200, False), (1, 100, True),
+                                           (16384, 20000, True), (300, 20000, False), (70000, 4096, False),
+                                           (40000, 2048, True)])
+def test_offsets_api_one_key_batches(torch_dev, n, size, seeded):
+    """Uniform lengths through the offsets API: when every buffer falls in one
+    sort key and none can be split, sort_scatter is skipped and the class
+    kernel reads off/len/seed in index order (kWsIdent); 300 x 20,000 B stays
+    on the sorted path (class 2 above 16 KiB in a small batch: split into
+    pieces).  Byte-packed offsets with gaps, seeded or not, masked."""
+    torch, dev = torch_dev
+    offs = 7 + np.arange(n, dtype=np.int64) * (size + 3)
+    total = int(offs[-1]) + size + 64
+    arena = torch.empty(total, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, 0x1DE + n)
+    rng = np.random.default_rng(n)
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    o = torch.from_numpy(offs).to(dev)
+    ln = torch.full((n,), size, dtype=torch.int32, device=dev)
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out = lvgpu.batch(arena, o, ln, sd, masked=True)
+    got = out.cpu().numpy().view(np.uint32)
+    want = oracle_batch(arena.cpu().numpy().tobytes(), offs, np.full(n, size), seeds, True)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, bad[:10]
