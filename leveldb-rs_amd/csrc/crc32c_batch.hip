@@ -2295,6 +2295,55 @@ __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__r
     }
 }
 
+// Blocks of many pieces (s >= 2,048, up to 4,096): one workgroup per block.
+// The s pieces are padded at the FRONT to 256 c (c = s / 256, at least 1;
+// leading zero pieces add nothing); thread t runs Horner with Shift_plen
+// over its c consecutive pieces, a 6-level tree joins the lanes of each wave
+// with Shift_{c 2^u plen}, and wave 0 joins the four wave partials by Horner
+// with Shift_{64 c plen}.  Every matrix is uniform (Shift_{2^i plen} at
+// index 65 + i of mats; LDS broadcasts).  (One wave per block ran Horner
+// over s / 64 rows: 16 serial matrix products at s = 1,024.)
+constexpr uint32_t kPow2Mats = 13;  // Shift_{2^i plen}, i <= 12 (s <= 4,096)
+constexpr uint32_t kPieceMats = 65 + kPow2Mats;
+__global__ __launch_bounds__(256) void combine_pieces_wg_kernel(const uint32_t *__restrict__ raw, uint32_t s,
+                                                                const uint32_t *__restrict__ mats,
+                                                                uint32_t *__restrict__ out, uint32_t flags) {
+    __shared__ uint32_t M[kPow2Mats * 32];  // Shift_{2^i plen}
+    __shared__ uint32_t part[4];
+    uint32_t c = 1, lc = 0;
+    while (256u * c < s) {
+        c <<= 1;
+        ++lc;
+    }
+    for (uint32_t i = threadIdx.x; i < (lc + 7u) * 32u; i += blockDim.x) M[i] = mats[65u * 32u + i];
+    __syncthreads();
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t b = blockIdx.x;
+    const int32_t pad = static_cast<int32_t>(256u * c - s);
+    const uint32_t *P1 = M;  // Shift_plen
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < c; ++i) {  // uniform trip count
+        const int32_t k = static_cast<int32_t>(t * c + i) - pad;
+        const uint32_t rk = k >= 0 ? raw[b * s + static_cast<uint32_t>(k)] : 0u;
+        acc = (i ? gf2_apply(P1, acc) : 0u) ^ rk;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 6; ++u) {  // lane l joins lane l + 2^u
+        const uint32_t right = __shfl_down(acc, 1u << u);
+        const uint32_t sh = gf2_apply(M + (lc + u) * 32u, acc);
+        if ((lane & ((2u << u) - 1u)) == 0) acc = sh ^ right;
+    }
+    if (lane == 0) part[w] = acc;
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t *S = M + (lc + 6u) * 32u;  // Shift_{64 c plen}
+        uint32_t x = part[0];
+        for (uint32_t v = 1; v < 4; ++v) x = gf2_apply(S, x) ^ part[v];
+        const uint32_t crc = ~x;
+        out[b] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+    }
+}
+
 // Joins the pieces of the offsets API's split long buffers (sort_scatter,
 // split_wave): long record {buffer, first piece slot, m, p}, pieces of
 // P = 2^p bytes aligned to the buffer end; piece 0's register is
@@ -2703,17 +2752,23 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_l
 }
 
 // Shift_{j plen} (j < 64) and Shift_{64 plen} as 65 GF(2) matrices of 32
-// column images, on the device (combine_pieces_kernel); built once per plen.
+// column images, then Shift_{2^i plen} (i < kPow2Mats), on the device
+// (combine_pieces_kernel, combine_pieces_wg_kernel); built once per plen.
 int piece_mats(DevCtx &c, uint64_t plen, const uint32_t **out) {
     std::lock_guard<std::mutex> lk(c.mats_m);
     uint32_t *&d = c.piece_mats[plen];
     if (!d) {
-        std::vector<uint32_t> h(65 * 32);
+        std::vector<uint32_t> h(lvk::kPieceMats * 32);
         const lvgpu::Gf2Mat step = lvgpu::shift_matrix(plen);
         lvgpu::Gf2Mat m = lvgpu::shift_matrix(0);
         for (int j = 0; j <= 64; ++j) {
             for (int b = 0; b < 32; ++b) h[j * 32 + b] = m.col[b];
             m = m.then(step);
+        }
+        m = step;  // then Shift_{2^i plen}, i < kPow2Mats (combine_pieces_wg_kernel)
+        for (uint32_t i = 0; i < lvk::kPow2Mats; ++i) {
+            for (int b = 0; b < 32; ++b) h[(65 + i) * 32 + b] = m.col[b];
+            m = m.then(m);
         }
         uint32_t *p = nullptr;
         LV_HIP(hipMalloc(&p, h.size() * 4));
@@ -2733,7 +2788,7 @@ uint32_t pick_split(uint64_t base, uint64_t stride, uint64_t blen, uint64_t n, i
     if (forced >= 0 || base % 16 || stride % 16) return 0;
     const uint64_t want = 4ull * static_cast<uint64_t>(cus) * lvk::kWaves;
     uint32_t ps = 0;
-    while ((n << ps) < want && ps < 10) {
+    while ((n << ps) < want && ps < 12) {
         const uint64_t s2 = 2ull << ps;
         if (blen % s2 || (blen / s2) % 1024 || blen / s2 < 4096) break;
         ++ps;
@@ -3054,9 +3109,16 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
         else
             hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true>), dim3(static_cast<uint32_t>(grid)),
                                dim3(lvk::kThreads), 0, hs, P, nb, c->image[2]);
-        hipLaunchKernelGGL(lvk::combine_pieces_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(1024, (n + 3) / 4))),
-                           dim3(256), 0, hs, P.out, static_cast<uint64_t>(n), 1u << ps, mats, d_out, flags);
-        g_kernel = "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel";
+        if (ps >= 11) {  // > 1,024 pieces per block: a workgroup per block
+            hipLaunchKernelGGL(lvk::combine_pieces_wg_kernel, dim3(static_cast<uint32_t>(n)), dim3(256), 0, hs, P.out,
+                               1u << ps, mats, d_out, flags);
+            g_kernel = "crc32c_blocks_kernel<16,pieces>+combine_pieces_wg_kernel";
+        } else {
+            hipLaunchKernelGGL(lvk::combine_pieces_kernel,
+                               dim3(static_cast<uint32_t>(std::min<uint64_t>(1024, (n + 3) / 4))), dim3(256), 0, hs,
+                               P.out, static_cast<uint64_t>(n), 1u << ps, mats, d_out, flags);
+            g_kernel = "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel";
+        }
         return check_launch();
     }
     // Aligned whole-batch blocks take the uniform-block kernel.

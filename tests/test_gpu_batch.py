@@ -500,13 +500,15 @@ def _split_kernel(n, blen, cus):
     pass of the grid; <= 16 pieces per block in one pass join in the same
     launch (FUSE), otherwise combine_pieces_kernel follows."""
     want, ps = 4 * cus * 16, 0
-    while (n << ps) < want and ps < 10:
+    while (n << ps) < want and ps < 12:
         s2 = 2 << ps
         if blen % s2 or (blen // s2) % 1024 or blen // s2 < 4096:
             break
         ps += 1
     if (1 << ps) <= 16 and (n << ps) <= 64 * cus:
         return "crc32c_blocks_kernel<16,pieces,fused>"
+    if ps >= 11:
+        return "crc32c_blocks_kernel<16,pieces>+combine_pieces_wg_kernel"
     return "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel"
 
 
@@ -516,7 +518,8 @@ def _split_kernel(n, blen, cus):
                                                   (2048, 32768, True, True), (4096, 16384, False, False),
                                                   (300, 65536, False, False), (1500, 65536, True, False),
                                                   (5, 8192, True, False), (200, 12288, False, False),
-                                                  (7, 3 << 20, True, True)])
+                                                  (7, 3 << 20, True, True), (2, 16 << 20, True, True),
+                                                  (1, 8 << 20, False, True), (3, 12 << 20, True, False)])
 def test_strided_long_block_split(torch_dev, n, blen, seeded, masked):
     """Few long blocks through lv_crc32c_batch_strided: each block is cut into
     2^k pieces that fill the grid and the piece registers are joined on the
