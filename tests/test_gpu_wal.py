@@ -109,16 +109,23 @@ def test_encode_then_scan_then_read(gpu):
     assert rep.dropped_bytes == 0 and rep.message == ""
 
 
-def _check_scan_device(log, cap=None):
+FUSED = "wal_fused_kernel+wal_fused_scan+wal_fused_emit"
+SORTED = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel"
+
+
+def _check_scan_device(log, cap=None, shift=0):
+    """shift = 0: the log starts 16-B aligned (the fused one-pass scan);
+    shift = 8: 8-B aligned only (the framing + length-sort scan)."""
     import lvgpu
     import lvgpu.wal as LW
     import torch
     o, c, i = W.scan_log(log)
     cap = len(o) if cap is None else cap
-    t = torch.frombuffer(bytearray(log) or bytearray(1), dtype=torch.uint8)[:len(log)].to("cuda:0")
+    t = torch.frombuffer(bytes(shift) + bytes(log) + b"\0", dtype=torch.uint8).to("cuda:0")[shift:shift + len(log)]
+    assert len(log) == 0 or t.data_ptr() % 16 == shift
     hdr, crc, info, count = LW.scan_device(t, cap)
     torch.cuda.synchronize()
-    assert lvgpu.last_kernel() == "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel" or len(log) == 0
+    assert lvgpu.last_kernel() == (FUSED if shift == 0 else SORTED) or len(log) == 0
     n = int(count.item())
     assert n == len(o)
     if n <= cap:
@@ -127,15 +134,16 @@ def _check_scan_device(log, cap=None):
         assert crc[:n].cpu().numpy().view(np.uint32).tolist() == c
 
 
-def test_scan_device_matches_oracle(gpu):
-    """lv_wal_scan_device (log already in HBM, framing fused into the length
-    sort, no host sync) == oracle.scan_log on intact, corrupted, truncated,
-    zero-padded, garbage and odd-length logs."""
+@pytest.mark.parametrize("shift", [0, 8])
+def test_scan_device_matches_oracle(gpu, shift):
+    """lv_wal_scan_device (log already in HBM, no host sync) ==
+    oracle.scan_log on intact, corrupted, truncated, zero-padded, garbage and
+    odd-length logs, through both scans (fused one-pass, framing + sort)."""
     rng = np.random.default_rng(29)
-    _check_scan_device(b"")
+    _check_scan_device(b"", shift=shift)
     for n in (1, 5, 6, 7, 8, 13):
-        _check_scan_device(_oracle_encode([b"ab" * n])[: n + 3])
-    _check_scan_device(_oracle_encode([b"foo", b"", b"bar" * 11000, b"x"]))
+        _check_scan_device(_oracle_encode([b"ab" * n])[: n + 3], shift=shift)
+    _check_scan_device(_oracle_encode([b"foo", b"", b"bar" * 11000, b"x"]), shift=shift)
     for trial in range(4):
         log = bytearray(_oracle_encode(_random_records(rng, 400), int(rng.integers(0, 2 * B))))
         if trial >= 1:
@@ -143,11 +151,35 @@ def test_scan_device_matches_oracle(gpu):
                 log[int(pos)] ^= int(rng.integers(1, 256))
         if trial >= 2:
             del log[len(log) - int(rng.integers(1, 5000)):]
-        _check_scan_device(bytes(log))
-    _check_scan_device(_oracle_encode(_random_records(rng, 50)) + bytes(3 * B + 123))
-    _check_scan_device(rng.integers(0, 256, size=5 * B + 77, dtype=np.uint8).tobytes())
-    # many tiny records: long header chains within a block
-    _check_scan_device(_oracle_encode([bytes([k % 251]) * (k % 9) for k in range(20000)]))
+        _check_scan_device(bytes(log), shift=shift)
+    _check_scan_device(_oracle_encode(_random_records(rng, 50)) + bytes(3 * B + 123), shift=shift)
+    _check_scan_device(rng.integers(0, 256, size=5 * B + 77, dtype=np.uint8).tobytes(), shift=shift)
+    # many tiny records: long header chains within a block (the fused scan's
+    # overflow chunks: > 64 records per block)
+    _check_scan_device(_oracle_encode([bytes([k % 251]) * (k % 9) for k in range(20000)]), shift=shift)
+
+
+def test_scan_device_fused_edges(gpu):
+    """The fused scan's record-boundary cases: units of every length 0..70
+    around every batch (4 KiB) and row (1 KiB) edge, headers straddling a
+    batch, units ending exactly on a granule / row / batch, blocks of exactly
+    64 / 65 / 128 records (the inline slots and the first overflow chunks),
+    ZERO and BAD_LENGTH headers mid-block, a log ending inside a header."""
+    rng = np.random.default_rng(37)
+    for fill in (1000, 1017, 4090, 4096 - 7, 4096 - 6, 4096 + 3, 8181):
+        recs = [bytes(fill)] + [rng.integers(0, 256, size=k, dtype=np.uint8).tobytes() for k in range(71)]
+        _check_scan_device(_oracle_encode(recs))
+    for per in (64, 65, 128, 200):  # records per block
+        ln = (B // per) - H
+        _check_scan_device(_oracle_encode([bytes([7]) * ln for _ in range(3 * per)]))
+    log = bytearray(_oracle_encode(_random_records(rng, 200, maxlog=12)))
+    log[5000:5007] = bytes(7)                      # a ZERO header mid-block (or inside a payload)
+    log[B + 300 + 4:B + 300 + 6] = (60000).to_bytes(2, "little")  # a length past the block
+    _check_scan_device(bytes(log))
+    for cut in (1, 3, 6, 7, 100):
+        _check_scan_device(bytes(log[:len(log) - cut]))
+    big = _oracle_encode(_random_records(rng, 3000, maxlog=16))
+    _check_scan_device(big)
 
 
 def test_scan_device_capacity(gpu):
@@ -157,3 +189,9 @@ def test_scan_device_capacity(gpu):
     n = len(W.scan_log(log)[0])
     _check_scan_device(log, cap=n - 1)
     _check_scan_device(log, cap=n + 100)
+    _check_scan_device(log, cap=n - 1, shift=8)
+    # > 64 records per block: the fused scan's overflow pool is sized from cap
+    tiny = _oracle_encode([bytes([k % 7]) * (k % 5) for k in range(30000)])
+    n = len(W.scan_log(tiny)[0])
+    for cap in (n - 1, n, n + 1, 2 * n):
+        _check_scan_device(tiny, cap=cap)
