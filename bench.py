@@ -83,8 +83,6 @@ def parse():
     p.add_argument("--long", action="store_true",
                    help="few long buffers through both device APIs (1,024 x 64 KiB, 64 x 16 MiB, 16 x 1 MiB, "
                         "1 x 16 MiB); one JSON line")
-    p.add_argument("--wal-sorted", action="store_true",
-                   help="with --wal-device: scan an 8-B aligned view (framing + length-sort path, not the fused scan)")
     p.add_argument("--wal-device", action="store_true",
                    help="SURVEY 8f row 1 in HBM: lv_wal_scan_device (framing + CRC) of a ~1 GiB log already on "
                         "the GPU; one JSON line with a roofline")
@@ -518,11 +516,11 @@ def long_bench(args):
 
 def wal_device_bench(args):
     """SURVEY 8f row 1 in HBM (verdict r01 "missing" 3): lv_wal_scan_device
-    over a ~1 GiB log of Random(301).skewed(17) records already on the GPU.
-    Default: the fused scan (one wave per 32 KiB block parses the headers from
-    the bytes it checksums; a count scan and a compaction put the records in
-    log order).  --wal-sorted: the framing + length-sort scan (wal_hist,
-    sort_scan, wal_scatter, class kernel).  No host sync either way.
+    over a ~1 GiB log of Random(301).skewed(17) records already on the GPU:
+    each 32 KiB block's header chain is walked inside the length sort's passes
+    (wal_hist, wal_scatter), every [type || payload] unit is checksummed by the
+    class kernel, records land in log order -- four launches, no host sync.
+    (A fused one-pass scan measured slower: profiles/r02/walfused/.)
     Algorithmic bytes: the log (every byte read once by the CRC; the framing
     reads the 7-B headers again).  HIP-event mean per call; the whole scan is
     checked against the oracle's framing (first 2000 records' CRCs vs value())."""
@@ -557,11 +555,6 @@ def wal_device_bench(args):
         raise SystemExit("encode failed: " + lvgpu.lib().lv_last_error().decode())
     del payload
     d_log = torch.from_numpy(log).to(dev)
-    if args.wal_sorted:  # an 8-B (not 16-B) aligned view: the framing + length-sort scan
-        buf = torch.empty(log.size + 16, dtype=torch.uint8, device=dev)
-        buf[8:8 + log.size].copy_(d_log)
-        d_log = buf[8:8 + log.size]
-        del buf
     # capacity from a first scan (a caller learns its log's record count once)
     _, _, _, count = LW.scan_device(d_log, 0)
     torch.cuda.synchronize()

@@ -2256,497 +2256,6 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
     sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
 }
 
-// ---------------------------------------------------------------------------
-// Fused WAL scan (lv_wal_scan_device on a 16-B aligned log; SURVEY 8f row 1,
-// log_reader.rs:271-364).  The four-launch scan above walks every block's
-// header chain first -- one dependent HBM round trip per record, ~39 us for
-// the 54-record chain of the bench log while HBM idles -- then length-sorts
-// the units for the class kernel.  Here ONE wave owns a 32 KiB block and
-// streams it once, in batches of 4 rows x 1 KiB (G = 64 image: W4 =
-// Shift_4096, W1/W2 = Shift_1024/2048): every header is parsed from the
-// registers the block's bytes already sit in (v_readlane), so the chain costs
-// no memory round trip, and the row accumulators are split at record
-// boundaries:
-//  * p_i = R(0, granule) of every granule of the batch, once;
-//  * the open unit [ra, rb) (= [type || payload], log_reader.rs:336) takes
-//    its whole granules (granules holding bytes < ra + 4 refolded with the
-//    pre-unit bytes zeroed and ~0 xored into its first 4 bytes: value() =
-//    extend(0, .)), A_i = Shift_4096(A_i) ^ q_i, or A_i = q_i in the batch it
-//    starts in;
-//  * a unit whose last whole granule u_e (row ie of the batch, lane e) falls
-//    in this batch finishes: rows after ie are not stepped, lanes past e
-//    count row ie - 1 as their last, a per-lane row rotation and one lane
-//    rotation by e + 1 turn the ordinary merge tree into R over its whole
-//    granules (merge_al's argument with a wave-uniform row), and the < 16
-//    bytes after u_e fold in as one shifted granule (finish_raw);
-//  * headers straddling two batches keep the last 8 bytes of a batch.
-// Records go to a per-wave LDS stage and leave 16 at a time into the block's
-// scratch slots (kWalInline inline, then chunks from a pool); a one-workgroup
-// scan of the per-block counts and a compaction kernel put them in log order.
-// Timing studies of the fused scan (wrong CRCs; experiment builds only):
-// bit 0 skips the record loop, bit 1 the unit finish (merge, tail), bit 2 the
-// head refold, bit 3 the Shift_4096 row steps.
-#ifndef LVK_WF_EXP
-#define LVK_WF_EXP 0
-#endif
-#if LVK_WF_EXP && !defined(LVK_EXPERIMENT_BUILD)
-#error "LVK_WF_EXP computes wrong CRCs; define LVK_EXPERIMENT_BUILD for an experiment variant"
-#endif
-// Matrices of the WAL image (in place of the combine tables, word offsets,
-// 33 words apart so that lanes reading different matrices hit distinct
-// banks): Shift_{16 j}, j < 64, and Shift_k, k < 16.
-constexpr uint32_t kWalLaneMat = kComb / 4;
-constexpr uint32_t kWalTailMat = kWalLaneMat + 64 * 33;
-static_assert((kWalTailMat + 16 * 33) * 4 <= kComb + 6 * 4 * 1024, "WAL matrices fit the combine-table area");
-constexpr uint32_t kWalInline = 64;  // records per block kept inline in the scratch
-constexpr uint32_t kWalChunk = 64;   // records per overflow chunk
-constexpr uint32_t kWalStage = 16;   // records a wave parks in LDS (g_oidx) between stores
-constexpr uint32_t kWalCtab = (kWalBlock / kWalHeader + 1 + kWalChunk - 1) / kWalChunk;  // chunk ids per block
-constexpr uint32_t kWalGroup = 256;  // blocks per compaction workgroup
-constexpr uint32_t kWalBatch = 4096; // bytes per batch: 4 rows x 64 granules
-static_assert(kWalChunk % kWalStage == 0 && kWalInline % kWalStage == 0, "a stage never spans two chunks");
-static_assert(kWalStage * 4 <= 64, "one staged word per lane");
-static_assert(kWalBlock % kWalBatch == 0, "whole batches per full block");
-
-struct WalFused {
-    uint64_t log;         // 16-B aligned
-    uint64_t size;
-    uint64_t nblocks;
-    uint32_t *cnt;        // records per block
-    uint4 *inl;           // nblocks x kWalInline records {header pos in block, info, crc, 0}
-    uint32_t *ctab;       // nblocks x kWalCtab overflow chunk ids
-    uint4 *pool;          // overflow chunks of kWalChunk records
-    uint32_t *pool_next;  // chunk allocator, zeroed before the launch
-    uint32_t pool_chunks;
-};
-
-// Selects by a run-time index over register arrays.  The values pass through
-// an empty asm first: a select of array elements is otherwise folded into a
-// load from a run-time address, which puts the whole register array (the
-// batch's 16 granule registers) in scratch memory.
-__device__ __forceinline__ uint32_t opq(uint32_t x) {
-    asm("" : "+v"(x));
-    return x;
-}
-
-__device__ __forceinline__ uint32_t sel4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-    a = opq(a);
-    b = opq(b);
-    c = opq(c);
-    d = opq(d);
-    return k == 0 ? a : k == 1 ? b : k == 2 ? c : d;
-}
-
-__device__ __forceinline__ uint32_t u4_get(const uint4 &v, uint32_t c) { return sel4(v.x, v.y, v.z, v.w, c); }
-
-// Row r (wave-uniform) of a batch.
-__device__ __forceinline__ uint4 row_sel(const uint4 (&v)[U], uint32_t r) {
-    return make_uint4(sel4(v[0].x, v[1].x, v[2].x, v[3].x, r), sel4(v[0].y, v[1].y, v[2].y, v[3].y, r),
-                      sel4(v[0].z, v[1].z, v[2].z, v[3].z, r), sel4(v[0].w, v[1].w, v[2].w, v[3].w, r));
-}
-
-// The dword at block offset o (a multiple of 4, wave-uniform, >= bs - 8):
-// from the batch's registers, or from the carried last 8 bytes of the batch
-// before.
-__device__ __forceinline__ uint32_t wal_dword(const uint4 (&v)[U], uint32_t bs, uint32_t o, uint32_t c0, uint32_t c1) {
-    if (o < bs) return o + 4u == bs ? c1 : c0;
-    const uint32_t r = o - bs;
-    const uint32_t k = r >> 10, c = (r >> 2) & 3u;
-    const uint32_t x = sel4(u4_get(v[0], c), u4_get(v[1], c), u4_get(v[2], c), u4_get(v[3], c), k);
-    return __builtin_amdgcn_readlane(x, (r >> 4) & 63u);
-}
-
-// XOR over the wave (every lane gets it): DPP within rows of 16, then
-// gfx950's permlane16/32 swaps.
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-    v ^= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-    v ^= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-    v ^= __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, false);  // row_ror:4
-    v ^= __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, false);  // row_ror:8
-    const auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    v = r16[0] ^ r16[1];
-    const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return r32[0] ^ r32[1];
-}
-
-// R over a finishing unit's whole granules (every lane): last whole granule
-// in row ie (-1: the batch before) and lane e.  Each lane merges its rows
-// (Horner with Shift_1024 / Shift_2048, rows rotated so its last row is B3),
-// shifts by its distance to u_e with ONE matrix, Shift_{16 ((e - l) mod 64)}
-// -- lanes past e ended a row earlier, which the rotation of their rows
-// already counts -- and the wave xors.  (A lane-rotation and a six-level
-// shift tree cost six dependent LDS round trips per unit: 130 us of the
-// 1 GiB scan.)
-__device__ __forceinline__ uint32_t wal_merge(const uint32_t (&A)[U], int32_t ie, uint32_t e, uint32_t lane,
-                                              const Lut &L) {
-    const int32_t iel = static_cast<int32_t>(lane) > static_cast<int32_t>(e) ? ie - 1 : ie;
-    const uint32_t sh = static_cast<uint32_t>(iel + 1) & 3u;  // B_k = A[(k + sh) & 3]: B3 is the last row
-    uint32_t B[U];
-#pragma unroll
-    for (uint32_t k = 0; k < U; ++k) B[k] = sel4(A[0], A[1], A[2], A[3], (k + sh) & 3u);
-    const uint32_t x01 = lookup4<kRegionB>(B[0], L) ^ B[1];
-    const uint32_t x23 = lookup4<kRegionB>(B[2], L) ^ B[3];
-    const uint32_t X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
-    return wave_xor(gf2_apply(g_lds + kWalLaneMat + 33u * ((e - lane) & 63u), X));
-}
-
-// R(0, D) for the unit's bytes D = [max(ra, rbw), rb) of the granule V at
-// rbw (pre-unit bytes zeroed, ~0 xored into unit bytes 0..3): one granule
-// fold of D moved to the granule's end (leading zeros leave R(0, .)
-// unchanged).  rel = rbw - ra, k = rb - rbw in [1, 16).
-__device__ __forceinline__ uint32_t wal_tail(uint4 V, int32_t rel, uint32_t k, uint32_t s0, const Lut &L) {
-    uint32_t w[4] = {fix_word(V.x, rel, s0), fix_word(V.y, rel + 4, s0), fix_word(V.z, rel + 8, s0),
-                     fix_word(V.w, rel + 12, s0)};
-#pragma unroll
-    for (uint32_t m = 0; m < 4; ++m) {  // zero bytes >= k
-        const int32_t nb = static_cast<int32_t>(k) - static_cast<int32_t>(4 * m);
-        w[m] &= nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : (0xffffffffu >> (32 - 8 * nb)));
-    }
-    const uint64_t lo = (static_cast<uint64_t>(w[1]) << 32) | w[0];
-    const uint64_t hi = (static_cast<uint64_t>(w[3]) << 32) | w[2];
-    const uint32_t b = 8u * (16u - k);  // 8 .. 120
-    uint64_t h2, l2;
-    if (b >= 64) {
-        h2 = lo << (b - 64);
-        l2 = 0;
-    } else {
-        h2 = (hi << b) | (lo >> (64 - b));
-        l2 = lo << b;
-    }
-    return r0_granule(make_uint4(static_cast<uint32_t>(l2), static_cast<uint32_t>(l2 >> 32),
-                                 static_cast<uint32_t>(h2), static_cast<uint32_t>(h2 >> 32)),
-                      L);
-}
-
-__global__ __launch_bounds__(kThreads) void wal_fused_kernel(WalFused W, const uint4 *__restrict__ image) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * kWaves;
-    uint64_t b = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;  // this wave's block
-    const uint64_t zero = reinterpret_cast<uint64_t>(&g_zero_granules[0]);
-    auto row_addr = [&](uint64_t blk, uint32_t bs, uint32_t i) __attribute__((always_inline)) -> uint64_t {
-        const uint64_t o = blk * kWalBlock + bs + 1024u * i + 16u * lane;
-        return o < W.size ? W.log + o : zero;
-    };
-    auto block_len = [&](uint64_t blk) __attribute__((always_inline)) -> uint32_t {
-        const uint64_t sb = blk * kWalBlock;
-        return static_cast<uint32_t>(W.size - sb < kWalBlock ? W.size - sb : kWalBlock);
-    };
-    uint4 slot0[U], slot1[U];
-    {
-        const uint64_t bb = b < W.nblocks ? b : 0;
-#pragma unroll
-        for (uint32_t i = 0; i < U; ++i) slot0[i] = load16(row_addr(bb, 0, i));
-    }
-    stage_tables(image);
-    if (b >= W.nblocks) return;
-    const Lut L = make_lut(lane);
-
-    // wave-uniform block state
-    uint32_t blen = block_len(b), nbat = (blen + kWalBatch - 1) / kWalBatch, j = 0;
-    uint32_t pos = 0, cnt = 0, ra = 0, rb = 0, rlen = 0, rtype = 0, chunk = 0xffffffffu;
-    uint32_t c0 = 0, c1 = 0;  // last 8 bytes of the previous batch
-    // flags in ONE word (bit 0: a unit is open, bit 1: the block's walk is
-    // done): two flag variables set on different paths were merged into a
-    // store through a selected address, which keeps them in scratch memory
-    uint32_t fl = 0;
-    constexpr uint32_t kOpen = 1u, kDone = 2u;
-    uint32_t A[U] = {0u, 0u, 0u, 0u};
-    // Records are parked in an LDS stage of kWalStage records (g_oidx, 4
-    // words each).  A full stage -- or a block's last records and its count --
-    // is stored in ONE instruction at the top of the next batch, BEFORE its
-    // prefetch: a later reuse of the store's registers then waits only for
-    // the store (vmcnt counts in order), not for the prefetch behind it.  Only
-    // a stage still pending when more records arrive (> kWalStage records in
-    // one batch) is stored at once.  (One descriptor of plain scalars: two
-    // stages chosen by a branch were merged into accesses through a selected
-    // address, which put the descriptors in scratch memory.)
-    uint32_t *const sw = &g_oidx[wave][0];
-    uint64_t pd_dst = 0, pd_cw = 0;  // first record's slot (0: none), count address (0: none)
-    uint32_t pd_n = 0, pd_cv = 0, pd_pend = 0;
-    // The store's operands live in registers of their own for the whole loop
-    // (opaque, and kept past the loop): no temporary reuses them, so no
-    // register write waits for the store.
-    uint32_t st_val = 0;
-    uint64_t st_ptr = 0;
-    auto store_stage = [&]() __attribute__((always_inline)) {
-        __builtin_amdgcn_wave_barrier();
-        const bool cw = pd_cw != 0 && lane == 63u;
-        const bool on = cw || (pd_dst != 0 && lane < 4u * pd_n);
-        st_val = cw ? pd_cv : sw[lane];
-        st_ptr = cw ? pd_cw : pd_dst + 4u * lane;
-        asm volatile("" : "+v"(st_ptr), "+v"(st_val));
-        if (on) *reinterpret_cast<__attribute__((address_space(1))) uint32_t *>(st_ptr) = st_val;
-        __builtin_amdgcn_wave_barrier();
-        pd_pend = 0;
-    };
-    // the stage holds records [cnt - n, cnt) of block b (one chunk); `last`: also the count
-    auto mark = [&](uint32_t n, bool last) __attribute__((always_inline)) {
-        if (pd_pend) store_stage();
-        const uint32_t cf = cnt - n;
-        uint64_t dst = 0;
-        if (n == 0)
-            dst = 0;
-        else if (cf < kWalInline)
-            dst = reinterpret_cast<uint64_t>(W.inl + b * kWalInline + cf);
-        else if (chunk < W.pool_chunks)
-            dst = reinterpret_cast<uint64_t>(W.pool + static_cast<uint64_t>(chunk) * kWalChunk + (cf % kWalChunk));
-        pd_dst = dst;
-        pd_n = n;
-        pd_cw = last ? reinterpret_cast<uint64_t>(W.cnt + b) : 0ull;
-        pd_cv = cnt;
-        pd_pend = 1;
-    };
-    auto emit = [&](uint32_t hpos, uint32_t info, uint32_t crc) __attribute__((always_inline)) {
-        if (cnt >= kWalInline && cnt % kWalChunk == 0) {  // a new overflow chunk (rare: > 64 records)
-            uint32_t id = 0;
-            if (lane == 0) id = atomicAdd(W.pool_next, 1u);
-            chunk = __builtin_amdgcn_readfirstlane(id);
-            if (lane == 0 && chunk < W.pool_chunks) W.ctab[b * kWalCtab + cnt / kWalChunk - 1] = chunk;
-        }
-        const uint32_t s = cnt % kWalStage;
-        if (pd_pend) store_stage();  // the stage filled earlier in this batch
-        if (lane == 0) {
-            sw[4 * s] = hpos;
-            sw[4 * s + 1] = info;
-            sw[4 * s + 2] = crc;
-            sw[4 * s + 3] = 0u;
-        }
-        ++cnt;
-        if (cnt % kWalStage == 0) mark(kWalStage, false);
-    };
-
-    // one batch: prefetch the next one into nxt, walk cur; true when the wave has
-    // no block left.  Two register slots in ping-pong (a copy of the prefetched
-    // batch would wait for it at the end of every batch).
-    auto step = [&](uint4(&cur)[U], uint4(&nxt)[U]) __attribute__((always_inline)) -> bool {
-        const bool lastb = (fl & kDone) || j + 1 == nbat;  // cur is the block's last batch worth walking
-        const uint64_t nb = lastb ? b + wstride : b;
-        const uint32_t nbs = lastb ? 0u : (j + 1) * kWalBatch;
-        const bool more = nb < W.nblocks;
-        if (pd_pend) store_stage();  // before the prefetch (see the stage above)
-#pragma unroll
-        for (uint32_t i = 0; i < U; ++i) nxt[i] = load16(row_addr(more ? nb : 0, more ? nbs : 0, i));
-        if (!(fl & kDone)) {
-            const uint32_t bs = j * kWalBatch;
-            const uint32_t be = bs + kWalBatch < blen ? bs + kWalBatch : blen;
-            uint32_t p[U];
-#pragma unroll
-            for (uint32_t i = 0; i < U; ++i) p[i] = r0_granule(cur[i], L);
-            uint32_t fresh = 0;
-            for (;;) {  // the units this batch holds bytes of (wave-uniform)
-                if (LVK_WF_EXP & 1) {
-                    asm volatile("" ::"v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]));
-                    break;
-                }
-                if (!(fl & kOpen)) {
-                    if (blen - pos < kWalHeader) {  // log_reader.rs:285-300: block trailer
-                        fl = kDone;
-                        break;
-                    }
-                    if (pos + kWalHeader > be) break;  // the header ends in the next batch
-                    const uint32_t pa = pos & ~3u, sh = (pos & 3u) * 8u;
-                    const uint64_t lo = wal_dword(cur, bs, pa, c0, c1) |
-                                        (static_cast<uint64_t>(wal_dword(cur, bs, pa + 4u, c0, c1)) << 32);
-                    const uint64_t h = sh ? (lo >> sh) | (static_cast<uint64_t>(wal_dword(cur, bs, pa + 8u, c0, c1))
-                                                          << (64u - sh))
-                                          : lo;
-                    const WalRec r = wal_decode(h, blen, pos);
-                    if (r.status != LV_WAL_REC_OK) {  // BAD_LENGTH / ZERO end the block's walk
-                        emit(pos, r.type | (r.status << 8) | (r.len << 16), 0u);
-                        fl = kDone;
-                        break;
-                    }
-                    ra = pos + 6u;  // [type || payload]
-                    rb = pos + kWalHeader + r.len;
-                    rlen = r.len;
-                    rtype = r.type;
-                    pos = rb;
-                    fl = kOpen;
-                    fresh = 1;
-                }
-                const uint32_t rag = ra & ~15u, rbw = rb & ~15u;
-                const uint32_t s0 = rb - ra >= 4u ? 0xffffffffu : 0u;
-                const bool fin = rb <= be;
-                int32_t ie = 3;
-                uint32_t e = 63u;
-                if (fin) {
-                    const int32_t rel = static_cast<int32_t>(rbw >> 4) - 1 - static_cast<int32_t>(bs >> 4);  // >= -1
-                    ie = rel >> 6;
-                    e = static_cast<uint32_t>(rel) & 63u;
-                }
-                const int32_t iel = static_cast<int32_t>(lane) > static_cast<int32_t>(e) ? ie - 1 : ie;
-#pragma unroll
-                for (uint32_t i = 0; i < U; ++i) {
-                    const uint32_t gs = bs + 1024u * i + 16u * lane;
-                    const bool inr = gs >= rag && gs + 16u <= rbw;
-                    uint32_t q = inr ? p[i] : 0u;
-                    const bool hd = inr && gs < ra + 4u;  // holds pre-unit bytes or seed bytes
-                    if (!(LVK_WF_EXP & 4) && __any(hd)) {
-                        const int32_t rel = static_cast<int32_t>(gs) - static_cast<int32_t>(ra);
-                        const uint4 f = make_uint4(fix_word(cur[i].x, rel, s0), fix_word(cur[i].y, rel + 4, s0),
-                                                   fix_word(cur[i].z, rel + 8, s0), fix_word(cur[i].w, rel + 12, s0));
-                        const uint32_t qf = r0_granule(f, L);
-                        q = hd ? qf : q;
-                    }
-                    if (fresh || (LVK_WF_EXP & 8)) {
-                        A[i] = q;
-                    } else {
-                        const uint32_t w = lookup4<kRegionA + kHalf>(A[i], L);  // Shift_4096
-                        A[i] = static_cast<int32_t>(i) <= iel ? w ^ q : A[i];
-                    }
-                }
-                fresh = 0;
-                if (!fin) break;  // the unit goes on in the next batch
-                uint32_t X = 0u;
-                if (LVK_WF_EXP & 2) {
-                    X = A[0] ^ A[1] ^ A[2] ^ A[3];
-                    emit(ra - 6u, rtype | (LV_WAL_REC_OK << 8) | (rlen << 16), X);
-                    fl = 0;
-                    continue;
-                }
-                // R(0, unit) = Shift_k(R over the whole granules) ^ R(0, tail bytes), k = rb & 15
-                const uint32_t k = rb & 15u;
-                uint32_t T = 0u;
-                if (k) {  // the granule after u_e, in this batch
-                    const uint32_t t = rbw - bs;
-                    const uint4 rw = row_sel(cur, t >> 10);
-                    const uint32_t tl = (t >> 4) & 63u;
-                    const uint4 tail = make_uint4(__builtin_amdgcn_readlane(rw.x, tl), __builtin_amdgcn_readlane(rw.y, tl),
-                                                  __builtin_amdgcn_readlane(rw.z, tl), __builtin_amdgcn_readlane(rw.w, tl));
-                    T = wal_tail(tail, static_cast<int32_t>(rbw) - static_cast<int32_t>(ra), k, s0, L);
-                }
-                if (rbw > rag) {
-                    X = wal_merge(A, ie, e, lane, L);
-                    if (k) X = gf2_apply(g_lds + kWalTailMat + 33u * k, X);
-                }
-                X ^= T;
-                if (rb - ra < 4u) {  // no seed in the bytes: R(~0, D) = R(0, D) ^ Shift_|D|(~0)
-                    uint32_t sd = 0xffffffffu;
-                    for (uint32_t i = 0; i < rb - ra; ++i) sd = byte_step(sd, 0u);
-                    X ^= sd;
-                }
-                emit(ra - 6u, rtype | (LV_WAL_REC_OK << 8) | (rlen << 16), ~X);  // lane 0's value is stored
-                fl = 0;
-            }
-            c0 = __builtin_amdgcn_readlane(cur[3].z, 63);
-            c1 = __builtin_amdgcn_readlane(cur[3].w, 63);
-        } else {
-            // a batch past the block's walk: consume its loads here, or their
-            // pending writes would make the next prefetch into these
-            // registers wait for everything in flight
-            asm volatile("" ::"v"(cur[0].x), "v"(cur[1].x), "v"(cur[2].x), "v"(cur[3].x));
-        }
-        if (!lastb) {
-            ++j;
-            return false;
-        }
-        // block done: its last staged records and its count
-        mark(cnt % kWalStage, true);
-        if (!more) return true;
-        b = nb;
-        blen = block_len(b);
-        nbat = (blen + kWalBatch - 1) / kWalBatch;
-        j = 0;
-        pos = 0;
-        cnt = 0;
-        chunk = 0xffffffffu;
-        fl = 0;
-        return false;
-    };
-    for (;;) {
-        if (step(slot0, slot1)) break;
-        if (step(slot1, slot0)) break;
-    }
-    if (pd_pend) store_stage();
-    asm volatile("" ::"v"(st_val), "v"(st_ptr));
-}
-
-// Exclusive prefix of the per-block record counts over groups of kWalGroup
-// blocks (one workgroup; a wave sums a group, then a scan of the group sums),
-// and the total: *count and ws_total.
-constexpr uint32_t kWalMaxGroups = 4096;  // > (7 * 2^32 / 32 KiB) / 256
-__global__ __launch_bounds__(1024) void wal_fused_scan(const uint32_t *__restrict__ cnt, uint64_t nblocks,
-                                                       uint64_t *__restrict__ gpre, uint64_t *__restrict__ count,
-                                                       uint64_t *__restrict__ ws_total) {
-    __shared__ uint64_t gs[kWalMaxGroups];
-    __shared__ uint64_t part[1024];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    const uint64_t ng = (nblocks + kWalGroup - 1) / kWalGroup;
-    for (uint64_t g = wave; g < ng; g += 16) {
-        uint64_t s = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kWalGroup / 64; ++k) {
-            const uint64_t bb = g * kWalGroup + k * 64u + lane;
-            s += bb < nblocks ? cnt[bb] : 0u;
-        }
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-        if (lane == 0) gs[g] = s;
-    }
-    __syncthreads();
-    // thread t scans groups [t*per, (t+1)*per)
-    const uint64_t per = (ng + 1023) / 1024;
-    uint64_t run = 0;
-    for (uint64_t g = t * per; g < ng && g < (t + 1) * per; ++g) run += gs[g];
-    part[t] = run;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint64_t x = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
-    }
-    uint64_t ex = part[t] - run;
-    for (uint64_t g = t * per; g < ng && g < (t + 1) * per; ++g) {
-        gpre[g] = ex;
-        ex += gs[g];
-    }
-    if (t == 1023) {
-        *count = part[1023];
-        *ws_total = part[1023];
-    }
-}
-
-// Records in log order: workgroup g takes blocks [256 g, 256 g + 256), one
-// thread per record (its block by a binary search over the inclusive prefix
-// of the counts in LDS, as wal_scatter).  Over capacity: nothing is written.
-__global__ __launch_bounds__(kWalGroup) void wal_fused_emit(WalFused W, const uint64_t *__restrict__ gpre,
-                                                            const uint64_t *__restrict__ ws_total, WalOut o,
-                                                            uint32_t *__restrict__ crc) {
-    __shared__ uint32_t red[kWalGroup];
-    if (*ws_total > o.cap) return;
-    const uint32_t t = threadIdx.x;
-    const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * kWalGroup;
-    red[t] = b0 + t < W.nblocks ? W.cnt[b0 + t] : 0u;
-    __syncthreads();
-    for (uint32_t d = 1; d < kWalGroup; d <<= 1) {
-        const uint32_t x = t >= d ? red[t - d] : 0u;
-        __syncthreads();
-        red[t] += x;
-        __syncthreads();
-    }
-    const uint32_t tot = red[kWalGroup - 1];
-    const uint64_t base = gpre[blockIdx.x];
-    for (uint32_t q0 = 0; q0 < tot; q0 += kWalGroup) {
-        const uint32_t q = q0 + t;
-        if (q >= tot) break;
-        uint32_t jb = 0;
-        for (uint32_t step = kWalGroup / 2; step >= 1; step >>= 1)
-            if (red[jb + step - 1] <= q) jb += step;
-        const uint32_t k = q - (jb ? red[jb - 1] : 0u);
-        const uint64_t bj = b0 + jb;
-        const uint4 r = k < kWalInline
-                            ? W.inl[bj * kWalInline + k]
-                            : W.pool[static_cast<uint64_t>(W.ctab[bj * kWalCtab + k / kWalChunk - 1]) * kWalChunk +
-                                     k % kWalChunk];
-        const uint64_t rid = base + q;
-        o.hdr_off[rid] = bj * kWalBlock + r.x;
-        o.info[rid] = r.y;
-        crc[rid] = r.z;
-    }
-}
-
 // Joins the raw piece registers of the long-block split: block b's pieces
 // R_k = raw[b*s + k], k < s (s a power of two <= 1024), give
 //   R(~seed, block) = XOR_k Shift_{(s-1-k) plen}(R_k)
@@ -2939,10 +2448,7 @@ constexpr int kGs[4] = {1, 4, 16, 64};
 // The table walk's image: the G = 16 one with region A's row shift
 // Shift_{256 kSstRows} (Shift_768 for three-row batches).
 constexpr int kTableImage = 4;
-// The fused WAL scan's image: the G = 64 one with the plain combine tables
-// replaced by GF(2) matrices (lvk::kWalLaneMat / kWalTailMat).
-constexpr int kWalImage = 5;
-constexpr int kImages = 6;
+constexpr int kImages = 5;
 
 // Host copy of the LDS image for each G (index into kGs), and the table
 // image; layout in lvk.
@@ -2979,19 +2485,6 @@ const std::vector<uint32_t> &host_image(int gi) {
         }
         uint32_t WT[4][256];
         lvgpu::shift_tables(256ull * lvk::kSstRows, WT);
-        images[kWalImage] = images[3];
-        {
-            uint32_t *m = &images[kWalImage][lvk::kComb / 4];
-            std::fill(m, m + 6 * 4 * 256, 0u);
-            for (uint32_t j = 0; j < 64; ++j) {
-                const lvgpu::Gf2Mat g = lvgpu::shift_matrix(16ull * j);
-                for (int b = 0; b < 32; ++b) m[lvk::kWalLaneMat - lvk::kComb / 4 + 33 * j + b] = g.col[b];
-            }
-            for (uint32_t k = 0; k < 16; ++k) {
-                const lvgpu::Gf2Mat g = lvgpu::shift_matrix(k);
-                for (int b = 0; b < 32; ++b) m[lvk::kWalTailMat - lvk::kComb / 4 + 33 * k + b] = g.col[b];
-            }
-        }
         images[kTableImage] = images[2];
         uint32_t *ra = &images[kTableImage][lvk::kRegionA / 4];
         for (int e = 0; e < 256; ++e)
@@ -3507,33 +3000,7 @@ static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
     return w;
 }
 
-// Workspace of the fused scan (16-B aligned logs): header {pool counter,
-// total}, per-block counts, per-group prefixes, kWalInline inline records per
-// block, the per-block chunk tables and a pool of ceil(cap / 64) + 1 chunks.
-// Chunks used <= sum over blocks of (ceil(cnt/64) - 1) <= total / 64, so a
-// scan whose total fits cap never runs out of pool.
-struct WalFusedWs {
-    size_t cnt, gpre, inl, ctab, pool, total;
-    uint32_t pool_chunks;
-};
-
-static WalFusedWs wal_fused_layout(uint64_t bytes, uint64_t cap) {
-    const uint64_t nblocks = (bytes + lvk::kWalBlock - 1) / lvk::kWalBlock;
-    const uint64_t ng = (nblocks + lvk::kWalGroup - 1) / lvk::kWalGroup;
-    WalFusedWs w;
-    w.pool_chunks = static_cast<uint32_t>((cap + lvk::kWalChunk - 1) / lvk::kWalChunk + 1);
-    w.cnt = 64;
-    w.gpre = w.cnt + al16(nblocks * sizeof(uint32_t));
-    w.inl = w.gpre + al16(ng * sizeof(uint64_t));
-    w.ctab = w.inl + nblocks * lvk::kWalInline * sizeof(uint4);
-    w.pool = w.ctab + al16(nblocks * lvk::kWalCtab * sizeof(uint32_t));
-    w.total = w.pool + static_cast<size_t>(w.pool_chunks) * lvk::kWalChunk * sizeof(uint4);
-    return w;
-}
-
-size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) {
-    return std::max(wal_ws_layout(bytes, cap).total, wal_fused_layout(bytes, cap).total);
-}
+size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) { return wal_ws_layout(bytes, cap).total; }
 
 int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
                        size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream) {
@@ -3546,8 +3013,7 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     if (bytes / lvk::kWalHeader >= 0xffffffffull || cap > 0xffffffffull)
         return set_err(LV_ERR_INVALID, "log too large for one scan");
     const WalWs lay = wal_ws_layout(bytes, cap);
-    if (workspace_bytes < lv_wal_scan_workspace_bytes(bytes, cap))
-        return set_err(LV_ERR_INVALID, "workspace too small");
+    if (workspace_bytes < lay.total) return set_err(LV_ERR_INVALID, "workspace too small");
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -3557,33 +3023,6 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
         return LV_OK;
     }
     uint8_t *wb = static_cast<uint8_t *>(d_workspace);
-    if (reinterpret_cast<uintptr_t>(d_log) % 16 == 0) {  // fused: one pass over the log
-        const WalFusedWs fl = wal_fused_layout(bytes, cap);
-        lvk::WalFused W{};
-        W.log = reinterpret_cast<uint64_t>(d_log);
-        W.size = bytes;
-        W.nblocks = nblocks;
-        W.cnt = reinterpret_cast<uint32_t *>(wb + fl.cnt);
-        W.inl = reinterpret_cast<uint4 *>(wb + fl.inl);
-        W.ctab = reinterpret_cast<uint32_t *>(wb + fl.ctab);
-        W.pool = reinterpret_cast<uint4 *>(wb + fl.pool);
-        W.pool_next = reinterpret_cast<uint32_t *>(wb);
-        W.pool_chunks = fl.pool_chunks;
-        uint64_t *gpre = reinterpret_cast<uint64_t *>(wb + fl.gpre);
-        uint64_t *total = reinterpret_cast<uint64_t *>(wb + 16);
-        const uint64_t ng = (nblocks + lvk::kWalGroup - 1) / lvk::kWalGroup;
-        uint64_t grid = (nblocks + lvk::kWaves - 1) / lvk::kWaves;
-        grid = std::min<uint64_t>(grid, static_cast<uint64_t>(c->cus));
-        LV_HIP(hipMemsetAsync(W.pool_next, 0, sizeof(uint32_t), s));
-        hipLaunchKernelGGL(lvk::wal_fused_kernel, dim3(static_cast<uint32_t>(grid)), dim3(lvk::kThreads), 0, s, W,
-                           c->image[kWalImage]);
-        hipLaunchKernelGGL(lvk::wal_fused_scan, dim3(1), dim3(1024), 0, s, W.cnt, nblocks, gpre, d_count, total);
-        lvk::WalOut o{d_hdr_off, d_info, d_count, cap};
-        hipLaunchKernelGGL(lvk::wal_fused_emit, dim3(static_cast<uint32_t>(ng)), dim3(lvk::kWalGroup), 0, s, W, gpre,
-                           total, o, d_crc);
-        g_kernel = "wal_fused_kernel+wal_fused_scan+wal_fused_emit";
-        return check_launch();
-    }
     uint32_t *ws = reinterpret_cast<uint32_t *>(wb);
     uint32_t *M = reinterpret_cast<uint32_t *>(wb + lay.m);
     uint64_t *wgrec = reinterpret_cast<uint64_t *>(wb + lay.wgrec);

@@ -109,13 +109,12 @@ def test_encode_then_scan_then_read(gpu):
     assert rep.dropped_bytes == 0 and rep.message == ""
 
 
-FUSED = "wal_fused_kernel+wal_fused_scan+wal_fused_emit"
 SORTED = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel"
 
 
 def _check_scan_device(log, cap=None, shift=0):
-    """shift = 0: the log starts 16-B aligned (the fused one-pass scan);
-    shift = 8: 8-B aligned only (the framing + length-sort scan)."""
+    """shift: the log's offset from a 16-B boundary (the scan needs 8-B
+    alignment)."""
     import lvgpu
     import lvgpu.wal as LW
     import torch
@@ -125,7 +124,7 @@ def _check_scan_device(log, cap=None, shift=0):
     assert len(log) == 0 or t.data_ptr() % 16 == shift
     hdr, crc, info, count = LW.scan_device(t, cap)
     torch.cuda.synchronize()
-    assert lvgpu.last_kernel() == (FUSED if shift == 0 else SORTED) or len(log) == 0
+    assert lvgpu.last_kernel() == SORTED or len(log) == 0
     n = int(count.item())
     assert n == len(o)
     if n <= cap:
@@ -136,9 +135,9 @@ def _check_scan_device(log, cap=None, shift=0):
 
 @pytest.mark.parametrize("shift", [0, 8])
 def test_scan_device_matches_oracle(gpu, shift):
-    """lv_wal_scan_device (log already in HBM, no host sync) ==
-    oracle.scan_log on intact, corrupted, truncated, zero-padded, garbage and
-    odd-length logs, through both scans (fused one-pass, framing + sort)."""
+    """lv_wal_scan_device (log already in HBM, framing fused into the length
+    sort, no host sync) == oracle.scan_log on intact, corrupted, truncated,
+    zero-padded, garbage and odd-length logs, 16-B and 8-B aligned."""
     rng = np.random.default_rng(29)
     _check_scan_device(b"", shift=shift)
     for n in (1, 5, 6, 7, 8, 13):
@@ -154,16 +153,15 @@ def test_scan_device_matches_oracle(gpu, shift):
         _check_scan_device(bytes(log), shift=shift)
     _check_scan_device(_oracle_encode(_random_records(rng, 50)) + bytes(3 * B + 123), shift=shift)
     _check_scan_device(rng.integers(0, 256, size=5 * B + 77, dtype=np.uint8).tobytes(), shift=shift)
-    # many tiny records: long header chains within a block (the fused scan's
-    # overflow chunks: > 64 records per block)
+    # many tiny records: long header chains within a block (> 64 records per
+    # block: past wal_hist's header cache)
     _check_scan_device(_oracle_encode([bytes([k % 251]) * (k % 9) for k in range(20000)]), shift=shift)
 
 
-def test_scan_device_fused_edges(gpu):
-    """The fused scan's record-boundary cases: units of every length 0..70
-    around every batch (4 KiB) and row (1 KiB) edge, headers straddling a
-    batch, units ending exactly on a granule / row / batch, blocks of exactly
-    64 / 65 / 128 records (the inline slots and the first overflow chunks),
+def test_scan_device_record_edges(gpu):
+    """Record-boundary cases: units of every length 0..70 around 1 KiB and 4
+    KiB edges, units ending exactly on a granule / row, blocks of exactly 64 /
+    65 / 128 / 200 records (wal_hist's 64-header cache and the walk past it),
     ZERO and BAD_LENGTH headers mid-block, a log ending inside a header."""
     rng = np.random.default_rng(37)
     for fill in (1000, 1017, 4090, 4096 - 7, 4096 - 6, 4096 + 3, 8181):
@@ -190,7 +188,7 @@ def test_scan_device_capacity(gpu):
     _check_scan_device(log, cap=n - 1)
     _check_scan_device(log, cap=n + 100)
     _check_scan_device(log, cap=n - 1, shift=8)
-    # > 64 records per block: the fused scan's overflow pool is sized from cap
+    # > 64 records per block, at and around the exact capacity
     tiny = _oracle_encode([bytes([k % 7]) * (k % 5) for k in range(30000)])
     n = len(W.scan_log(tiny)[0])
     for cap in (n - 1, n, n + 1, 2 * n):

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Fused WAL scan timing variants (wrong CRCs): builds them on the box, runs
+# WAL device-scan timing variants (experiment builds, -D flags; wrong CRCs allowed): builds them on the box, runs
 # bench.py --wal-device under each.   tools/exp_wal.sh OUT "name:flags ..."
 set -o pipefail
 out=$1; shift
