@@ -2257,15 +2257,28 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
 }
 
 // Joins the raw piece registers of the long-block split: block b's pieces
-// R_k = raw[b*s + k], k < s (s a power of two <= 1024), give
+// R_k = raw[b*s + k], k < s (s a power of two <= 4,096), give
 //   R(~seed, block) = XOR_k Shift_{(s-1-k) plen}(R_k)
-// (linearity, DESIGN "CRC algebra").  One wave per block: lane l < min(s, 64)
-// runs Horner over its pieces k = l + 64 m with Shift_{64 plen}, then shifts
-// by (min(s, 64) - 1 - l) plen; an xor over the wave, then ~ and the mask.
-// mats: 65 GF(2) matrices of 32 column images, Shift_{j plen} for j < 64 and
-// Shift_{64 plen} (built on the host, crc32c_gf2.h).
-// Matrices sit in LDS at a stride of 33 words: lanes applying different
-// matrices (j = w - 1 - lane) then read 32 distinct banks.
+// (linearity, DESIGN "CRC algebra").
+constexpr uint32_t kPow2Tabs = 13;  // Shift_{2^v plen}, v <= 12 (s <= 4,096)
+
+__device__ __forceinline__ uint32_t tab_shift(const uint32_t *t, uint32_t a) {
+    return t[a & 0xffu] ^ t[256 + ((a >> 8) & 0xffu)] ^ t[512 + ((a >> 16) & 0xffu)] ^ t[768 + (a >> 24)];
+}
+
+// Stage n4 uint4 of `src` into LDS `dst` (16-B loads, all issued first).
+__device__ __forceinline__ void stage_words(uint32_t *dst, const uint32_t *src, uint32_t n4) {
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
+}
+
+// s <= 1,024: one wave per block (GF(2) matrices Shift_{j plen}, j <= 64, at a
+// stride of 33 words so that lanes applying different matrices read distinct
+// banks): lane l < min(s, 64) runs Horner over its pieces k = l + 64 m with
+// Shift_{64 plen}, then shifts by (min(s, 64) - 1 - l) plen; an xor over the
+// wave.  (Byte tables here -- a tree of Shift_{2^u plen} lookups -- staged
+// 28 KiB per workgroup against 8 KiB of matrices: 16 x 1 MiB 16.9 -> 19.5 us.)
 __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__restrict__ raw, uint64_t n, uint32_t s,
                                                              const uint32_t *__restrict__ mats,
                                                              uint32_t *__restrict__ out, uint32_t flags) {
@@ -2295,52 +2308,50 @@ __global__ __launch_bounds__(256) void combine_pieces_kernel(const uint32_t *__r
     }
 }
 
-// Blocks of many pieces (s >= 2,048, up to 4,096): one workgroup per block.
-// The s pieces are padded at the FRONT to 256 c (c = s / 256, at least 1;
-// leading zero pieces add nothing); thread t runs Horner with Shift_plen
-// over its c consecutive pieces, a 6-level tree joins the lanes of each wave
-// with Shift_{c 2^u plen}, and wave 0 joins the four wave partials by Horner
-// with Shift_{64 c plen}.  Every matrix is uniform (Shift_{2^i plen} at
-// index 65 + i of mats; LDS broadcasts).  (One wave per block ran Horner
-// over s / 64 rows: 16 serial matrix products at s = 1,024.)
-constexpr uint32_t kPow2Mats = 13;  // Shift_{2^i plen}, i <= 12 (s <= 4,096)
-constexpr uint32_t kPieceMats = 65 + kPow2Mats;
-__global__ __launch_bounds__(256) void combine_pieces_wg_kernel(const uint32_t *__restrict__ raw, uint32_t s,
-                                                                const uint32_t *__restrict__ mats,
-                                                                uint32_t *__restrict__ out, uint32_t flags) {
-    __shared__ uint32_t M[kPow2Mats * 32];  // Shift_{2^i plen}
-    __shared__ uint32_t part[4];
-    uint32_t c = 1, lc = 0;
-    while (256u * c < s) {
-        c <<= 1;
-        ++lc;
-    }
-    for (uint32_t i = threadIdx.x; i < (lc + 7u) * 32u; i += blockDim.x) M[i] = mats[65u * 32u + i];
+// Blocks of many pieces (s = 2,048 or 4,096): one 1024-thread workgroup per
+// block.  Thread t runs Horner with Shift_plen over its c = s / 1024
+// consecutive pieces; a 6-level tree joins the lanes of each wave with
+// Shift_{c 2^u plen}, and a 4-level tree over the 16 wave partials (lanes of
+// wave 0) with Shift_{64 c 2^u plen}.  Every shift is a byte-table lookup
+// (Shift_n(v) = S0[v.b0] ^ S1[v.b1] ^ S2[v.b2] ^ S3[v.b3], 4 KiB per n, from
+// the per-plen set Shift_{2^v plen}, piece_tabs): four LDS reads where a
+// GF(2) matrix product took ~100 VALU instructions, so the 14 dependent steps
+// cost what 25 matrix products on 256 threads did not (1 x 16 MiB: join 12.7
+// -> ~4 us, call 25.7 -> 16.8 us).
+__global__ __launch_bounds__(1024) void combine_pieces_wg_kernel(const uint32_t *__restrict__ raw, uint32_t s,
+                                                                 const uint32_t *__restrict__ tabs,
+                                                                 uint32_t *__restrict__ out, uint32_t flags) {
+    __shared__ __attribute__((aligned(16))) uint32_t T[11 * 1024];  // slot 0: Shift_plen; 1 + u: Shift_{c 2^u plen}
+    __shared__ uint32_t part[16];
+    const uint32_t c = s / 1024u;
+    const uint32_t lc = c >= 4u ? 2u : 1u;  // log2 c (s >= 2,048)
+    stage_words(T, tabs, 256u);
+    stage_words(T + 1024, tabs + lc * 1024u, 10u * 256u);
     __syncthreads();
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint64_t b = blockIdx.x;
-    const int32_t pad = static_cast<int32_t>(256u * c - s);
-    const uint32_t *P1 = M;  // Shift_plen
     uint32_t acc = 0;
-    for (uint32_t i = 0; i < c; ++i) {  // uniform trip count
-        const int32_t k = static_cast<int32_t>(t * c + i) - pad;
-        const uint32_t rk = k >= 0 ? raw[b * s + static_cast<uint32_t>(k)] : 0u;
-        acc = (i ? gf2_apply(P1, acc) : 0u) ^ rk;
-    }
+    for (uint32_t i = 0; i < c; ++i) acc = (i ? tab_shift(T, acc) : 0u) ^ raw[b * s + t * c + i];
 #pragma unroll
     for (uint32_t u = 0; u < 6; ++u) {  // lane l joins lane l + 2^u
         const uint32_t right = __shfl_down(acc, 1u << u);
-        const uint32_t sh = gf2_apply(M + (lc + u) * 32u, acc);
+        const uint32_t sh = tab_shift(T + (1u + u) * 1024u, acc);
         if ((lane & ((2u << u) - 1u)) == 0) acc = sh ^ right;
     }
     if (lane == 0) part[w] = acc;
     __syncthreads();
-    if (t == 0) {
-        const uint32_t *S = M + (lc + 6u) * 32u;  // Shift_{64 c plen}
-        uint32_t x = part[0];
-        for (uint32_t v = 1; v < 4; ++v) x = gf2_apply(S, x) ^ part[v];
-        const uint32_t crc = ~x;
-        out[b] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+    if (w == 0) {
+        acc = lane < 16u ? part[lane] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t right = __shfl_down(acc, 1u << u);
+            const uint32_t sh = tab_shift(T + (7u + u) * 1024u, acc);
+            if ((lane & ((2u << u) - 1u)) == 0) acc = sh ^ right;
+        }
+        if (lane == 0) {
+            const uint32_t crc = ~acc;
+            out[b] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+        }
     }
 }
 
@@ -2517,6 +2528,7 @@ struct DevCtx {
     // long-block split: Shift matrices per piece length (immutable once built)
     std::mutex mats_m;
     std::map<uint64_t, uint32_t *> piece_mats;
+    std::map<uint64_t, uint32_t *> piece_tabs;
     // host-path staging (grown on demand), serialised by host_m
     std::mutex host_m;
     uint8_t *d_arena = nullptr;
@@ -2752,23 +2764,40 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_l
 }
 
 // Shift_{j plen} (j < 64) and Shift_{64 plen} as 65 GF(2) matrices of 32
-// column images, then Shift_{2^i plen} (i < kPow2Mats), on the device
-// (combine_pieces_kernel, combine_pieces_wg_kernel); built once per plen.
+// column images on the device (combine_pieces_kernel, and the fused join of
+// crc32c_blocks_kernel<16, ..., FUSE>); built once per plen.
 int piece_mats(DevCtx &c, uint64_t plen, const uint32_t **out) {
     std::lock_guard<std::mutex> lk(c.mats_m);
     uint32_t *&d = c.piece_mats[plen];
     if (!d) {
-        std::vector<uint32_t> h(lvk::kPieceMats * 32);
+        std::vector<uint32_t> h(65 * 32);
         const lvgpu::Gf2Mat step = lvgpu::shift_matrix(plen);
         lvgpu::Gf2Mat m = lvgpu::shift_matrix(0);
-        for (int j = 0; j <= 64; ++j) {
+        for (uint32_t j = 0; j <= 64; ++j) {
             for (int b = 0; b < 32; ++b) h[j * 32 + b] = m.col[b];
             m = m.then(step);
         }
-        m = step;  // then Shift_{2^i plen}, i < kPow2Mats (combine_pieces_wg_kernel)
-        for (uint32_t i = 0; i < lvk::kPow2Mats; ++i) {
-            for (int b = 0; b < 32; ++b) h[(65 + i) * 32 + b] = m.col[b];
-            m = m.then(m);
+        uint32_t *p = nullptr;
+        LV_HIP(hipMalloc(&p, h.size() * 4));
+        LV_HIP(hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        d = p;
+    }
+    *out = d;
+    return 0;
+}
+
+// Byte tables of Shift_{2^v plen}, v < kPow2Tabs (4 x 256 words each), on the
+// device (combine_pieces_wg_kernel); built once per plen.
+int piece_tabs(DevCtx &c, uint64_t plen, const uint32_t **out) {
+    std::lock_guard<std::mutex> lk(c.mats_m);
+    uint32_t *&d = c.piece_tabs[plen];
+    if (!d) {
+        std::vector<uint32_t> h(lvk::kPow2Tabs * 1024);
+        for (uint32_t v = 0; v < lvk::kPow2Tabs; ++v) {
+            uint32_t S[4][256];
+            lvgpu::shift_tables(plen << v, S);
+            for (int j = 0; j < 4; ++j)
+                for (int e = 0; e < 256; ++e) h[v * 1024 + j * 256 + e] = S[j][e];
         }
         uint32_t *p = nullptr;
         LV_HIP(hipMalloc(&p, h.size() * 4));
@@ -3109,9 +3138,11 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
         else
             hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true>), dim3(static_cast<uint32_t>(grid)),
                                dim3(lvk::kThreads), 0, hs, P, nb, c->image[2]);
+        const uint32_t *tabs = nullptr;
+        if (int rc = piece_tabs(*c, plen, &tabs)) return rc;
         if (ps >= 11) {  // > 1,024 pieces per block: a workgroup per block
-            hipLaunchKernelGGL(lvk::combine_pieces_wg_kernel, dim3(static_cast<uint32_t>(n)), dim3(256), 0, hs, P.out,
-                               1u << ps, mats, d_out, flags);
+            hipLaunchKernelGGL(lvk::combine_pieces_wg_kernel, dim3(static_cast<uint32_t>(n)), dim3(1024), 0, hs, P.out,
+                               1u << ps, tabs, d_out, flags);
             g_kernel = "crc32c_blocks_kernel<16,pieces>+combine_pieces_wg_kernel";
         } else {
             hipLaunchKernelGGL(lvk::combine_pieces_kernel,
