@@ -1234,6 +1234,159 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
     }
 }
 
+// Small batches (n <= kSmallSort): the three passes in ONE launch.  Every
+// workgroup reads all n lengths (<= 4 KiB), so it knows the whole key
+// histogram, the histogram of the buffers before its chunk, the batch's
+// payload bytes and every buffer's split (pieces m_i, log2 piece length p_i);
+// piece slots and long-record indices are index-order prefix sums instead of
+// device-atomic claims, so no pass waits for another and no counter needs
+// zeroing.  (By construction every split fits: sum m <= 16,384 + n pieces
+// and <= n long records, below the budgets.)  Each workgroup then claims its
+// chunk's sorted slots and writes its pieces, a contiguous slot range, one
+// slot per thread.  Same grid and chunks as the three-pass sort.
+#ifndef LVK_SMALL_SORT
+#define LVK_SMALL_SORT 1
+#endif
+constexpr uint32_t kSmallSort = 4 * kSortThreads;  // buffers
+__global__ __launch_bounds__(kSortThreads) void sort_small(const uint64_t *__restrict__ off,
+                                                           const uint32_t *__restrict__ len, uint64_t n,
+                                                           uint64_t chunk, uint32_t *__restrict__ ws,
+                                                           uint4 *__restrict__ ent, const uint32_t *__restrict__ seed,
+                                                           uint32_t *__restrict__ sseed, uint4 *__restrict__ longs) {
+    __shared__ uint32_t hall[kKeys], hpre[kKeys], sc[kKeys];
+    __shared__ uint32_t mpre[kSmallSort + 1];  // exclusive prefix of m over buffer index (+ total)
+    __shared__ uint32_t lpre[kSmallSort + 1];  // exclusive prefix of split buffers
+    __shared__ uint32_t pp[kSmallSort];        // log2 piece length of a split buffer
+    __shared__ uint64_t red[kSortThreads / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    hall[t] = 0;
+    hpre[t] = 0;
+    uint32_t l[4];
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 4; ++e) {
+        const uint64_t i = e * kSortThreads + t;
+        l[e] = i < n ? len[i] : 0u;
+        mine += l[e];
+    }
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) mine += __shfl_xor(mine, k);
+    if (lane == 0) red[w] = mine;
+    __syncthreads();
+    const uint64_t total = red[0] + red[1] + red[2] + red[3];
+    // histograms, splits and their index-order prefixes
+    uint32_t run_m = 0, run_l = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 4; ++e) {
+        const uint64_t i = e * kSortThreads + t;
+        const bool valid = i < n;
+        const uint32_t k = sort_key(l[e]);
+        wave_count(hall, k, valid, lane);
+        wave_count(hpre, k, valid && i < lo, lane);
+        uint32_t m = 0, p = 0;
+        if (longs && valid && l[e] > 16384u) {  // split_wave's rule
+            p = ceil_log2(total / 16384u);
+            const uint32_t pl = ceil_log2((static_cast<uint64_t>(l[e]) + kMaxPieces - 1) / kMaxPieces);
+            p = p > pl ? p : pl;
+            p = p > 12u ? p : 12u;
+            p = p < 22u ? p : 22u;
+            if (l[e] > (2ull << p)) m = static_cast<uint32_t>((l[e] + (1ull << p) - 1) >> p);
+        }
+        // exclusive scans over t of m and (m > 0), plus the running totals of rows e' < e
+        uint32_t im = m, il = m > 0 ? 1u : 0u;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t xm = __shfl_up(im, d), xl = __shfl_up(il, d);
+            if (lane >= d) {
+                im += xm;
+                il += xl;
+            }
+        }
+        __syncthreads();  // red / sc reuse
+        if (lane == 63) {
+            sc[w] = im;
+            sc[4 + w] = il;
+        }
+        __syncthreads();
+        uint32_t bm = run_m, bl = run_l;
+        for (uint32_t v = 0; v < w; ++v) {
+            bm += sc[v];
+            bl += sc[4 + v];
+        }
+        pp[i] = p;  // i < kSmallSort: e < 4, t < kSortThreads
+        mpre[i] = bm + im - m;
+        lpre[i] = bl + il - (m > 0 ? 1u : 0u);
+        run_m += sc[0] + sc[1] + sc[2] + sc[3];
+        run_l += sc[4] + sc[5] + sc[6] + sc[7];
+    }
+    __syncthreads();
+    if (t == 0) {
+        mpre[kSmallSort] = run_m;
+        lpre[kSmallSort] = run_l;
+    }
+    // key starts (exclusive scan of the whole histogram) and this chunk's slots
+    const uint32_t mineh = hall[t];
+    sc[t] = mineh;
+    __syncthreads();
+    for (uint32_t d = 1; d < kKeys; d <<= 1) {
+        const uint32_t x = t >= d ? sc[t - d] : 0u;
+        __syncthreads();
+        sc[t] += x;
+        __syncthreads();
+    }
+    const uint32_t ks = sc[t] - mineh;
+    const uint32_t kc = t / kBuckets, knb = kBuckets - 1 - t % kBuckets;
+    const bool ident_ok = mineh == static_cast<uint32_t>(n) && (kc <= 1 || (kc == 2 && (knb <= 16 || n >= 16384)));
+    const bool ident = __syncthreads_or(LVK_IDENT && ident_ok && run_l == 0);
+    if (blockIdx.x == 0) {
+        ws[kWsTot + t] = mineh;
+        if (t % kBuckets == 0) {  // per-class [start, count) for the CRC kernel
+            ws[kWsCls + kc] = ks;
+            ws[kWsCls + 4 + kc] = sc[t + kBuckets - 1] - ks;
+        }
+        if (t == 0) {
+            ws[kWsIdent] = ident ? 1u : 0u;
+            ws[kWsBytes] = static_cast<uint32_t>(total);
+            ws[kWsBytes + 1] = static_cast<uint32_t>(total >> 32);
+            ws[kWsPieces] = run_m;
+            ws[kWsLongs] = run_l;
+        }
+    }
+    if (ident) return;  // block-uniform
+    __syncthreads();  // sc (inclusive) is read above; hpre becomes the claim cursor
+    hpre[t] += ks;
+    __syncthreads();
+    // this chunk's buffers: sorted slots, entries, long records
+    const uint64_t i = lo + t;
+    const bool valid = i < hi;  // chunk <= 16 <= kSortThreads for n <= kSmallSort
+    const uint32_t L = valid ? len[i] : 0u;
+    const uint64_t o = valid ? off[i] : 0u;
+    const uint32_t sd = (seed && valid) ? seed[i] : 0u;
+    const uint32_t pos = wave_claim(hpre, sort_key(L), valid, lane);
+    const uint32_t m = valid ? mpre[i + 1] - mpre[i] : 0u;
+    if (valid) {
+        ent[pos] = make_uint4(static_cast<uint32_t>(o), static_cast<uint32_t>(o >> 32), m ? 0u : L,
+                              m ? 0xffffffffu : static_cast<uint32_t>(i));
+        if (seed) sseed[pos] = sd;
+        if (m) longs[lpre[i]] = make_uint4(static_cast<uint32_t>(i), mpre[i], m, pp[i]);
+    }
+    // pieces of the chunk: slots [mpre[lo], mpre[hi]), one per thread
+    const uint32_t s0 = mpre[lo], s1 = mpre[hi];
+    for (uint32_t u = s0 + t; u < s1; u += kSortThreads) {
+        uint32_t j = static_cast<uint32_t>(lo);  // the chunk's buffer holding slot u (<= 16 buffers)
+        while (mpre[j + 1] <= u) ++j;
+        const uint32_t mj = mpre[j + 1] - mpre[j], k = u - mpre[j];
+        const uint32_t Lj = len[j];
+        const uint64_t P = 1ull << pp[j];
+        const uint64_t first = Lj - (static_cast<uint64_t>(mj) - 1) * P;  // piece 0: [0, first)
+        const uint64_t a = off[j] + (k ? first + (k - 1) * P : 0);
+        ent[n + u] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                                static_cast<uint32_t>(k ? P : first), u | kPieceFlag);
+        if (seed) sseed[n + u] = k ? 0u : seed[j];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // WAL scan with the framing fused into the sort passes (the
 // reader side, log_reader.rs:271-364).  Records never straddle a 32 KiB block
@@ -2842,10 +2995,14 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     // whose buffer indices reach the piece flag bit
     uint4 *longs = n < lvk::kPieceFlag ? reinterpret_cast<uint4 *>(ws_bytes + lay.longs) : nullptr;
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
-    hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M, ws, wgb);
-    hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
-                       static_cast<uint32_t>(wgs), ws, wgb);
-    hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed, longs);
+    if (n <= lvk::kSmallSort && LVK_SMALL_SORT) {  // one launch (sort_small)
+        hipLaunchKernelGGL(lvk::sort_small, g, b, 0, s, off, len, n, chunk, ws, ent, seed, sseed, longs);
+    } else {
+        hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M, ws, wgb);
+        hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
+                           static_cast<uint32_t>(wgs), ws, wgb);
+        hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed, longs);
+    }
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(arena);
     P.off = off;
