@@ -1456,6 +1456,41 @@ __device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, 
     return wal_decode(wal_load8(log, size, start + pos), blen, pos);
 }
 
+// Long chains: after LVK_WAL_TOUCH_HOPS hops, the wave loads one dword of
+// every 128-B line of the rest of each block still being walked (a block with
+// that many records has short ones: its remaining headers are close
+// together), four blocks at a time (16 loads per lane in flight, one HBM round
+// trip per four blocks), so the remaining hops hit L2 (~200 cycles) instead
+// of HBM (~900).  In the bench log 5 % of the blocks hold > 16 records and the
+// longest chain is 54.
+#ifndef LVK_WAL_TOUCH_HOPS
+#define LVK_WAL_TOUCH_HOPS 16
+#endif
+__device__ __forceinline__ uint32_t wal_touch(const uint8_t *log, uint64_t b0, uint32_t pos, uint32_t blen,
+                                              bool active, uint32_t lane) {
+    uint64_t dm = __ballot(active);
+    uint32_t x = 0;
+    while (dm) {  // wave-uniform
+        uint32_t v[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int l0 = dm ? __ffsll(static_cast<long long>(dm)) - 1 : 0;
+            const bool on = dm != 0;
+            dm &= dm - 1;
+            const uint32_t p0 = __shfl(pos, l0), bl = on ? __shfl(blen, l0) : 0u;
+            const uint8_t *blk = log + (b0 + static_cast<uint64_t>(l0)) * kWalBlock;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t o = (p0 & ~127u) + 128u * (lane + 64u * k);
+                v[g][k] = o < bl ? *reinterpret_cast<const uint32_t *>(blk + o) : 0u;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) x ^= xor3(v[g][0], v[g][1], v[g][2]) ^ v[g][3];
+    }
+    return x;
+}
+
 __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
                                                          uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ M,
                                                          uint64_t *__restrict__ wgrec, uint32_t *__restrict__ blkcnt,
@@ -1467,13 +1502,16 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
     uint64_t mine = 0;
+    uint32_t touched = 0;
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
         const uint64_t b = b0 + t;
         const uint64_t start = b * kWalBlock;
         const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
-        uint32_t pos = 0, cnt = 0;
+        uint32_t pos = 0, cnt = 0, hops = 0;
         bool active = blen >= kWalHeader;
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
+            if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
+                touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
             uint32_t key = 0;
             const bool rec = active;
             if (active) {
@@ -1492,6 +1530,7 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
 #pragma unroll
     for (int k = 32; k >= 1; k >>= 1) mine += __shfl_xor(mine, k);
     if (lane == 0) wsum[t >> 6] = mine;
+    asm volatile("" ::"v"(touched));  // the touches are kept
     __syncthreads();
     M[static_cast<uint64_t>(blockIdx.x) * kKeys + t] = h[t];
     if (t == 0) wgrec[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // sort_scan sums these
