@@ -1497,6 +1497,7 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
                                                          uint64_t *__restrict__ hcache) {
     __shared__ uint32_t h[kKeys];
     __shared__ uint64_t wsum[kSortThreads / 64];
+    __shared__ uint64_t hcl[kSortThreads * (kHdrCache + 1)];  // per-thread header cache (130 KiB)
     const uint32_t t = threadIdx.x, lane = t & 63u;
     h[t] = 0;
     __syncthreads();
@@ -1509,6 +1510,11 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
         const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
         uint32_t pos = 0, cnt = 0, hops = 0;
         bool active = blen >= kWalHeader;
+        // The header cache is filled in LDS and stored after the walk: a
+        // global store in the hop (vmcnt counts stores too, in order) made
+        // every hop's wait for its header load also wait for the previous
+        // hop's store.
+        uint64_t *const hl = hcl + t * (kHdrCache + 1);  // stride 65 words: lanes spread over the banks
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
                 touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
@@ -1517,13 +1523,14 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
             if (active) {
                 const WalRec r = wal_record(log, size, start, blen, pos);
                 key = sort_key(r.ulen);
-                if (cnt < kHdrCache) hcache[b * kHdrCache + cnt] = hdr_pack(pos, r.len, r.type);
+                if (cnt < kHdrCache) hl[cnt] = hdr_pack(pos, r.len, r.type);
                 ++cnt;
                 pos += kWalHeader + r.len;
                 active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
             }
             wave_count(h, key, rec, lane);
         }
+        for (uint32_t c = 0; c < cnt && c < kHdrCache; ++c) hcache[b * kHdrCache + c] = hl[c];
         if (b < hi) blkcnt[b] = cnt;
         mine += cnt;
     }
