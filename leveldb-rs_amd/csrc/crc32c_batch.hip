@@ -2565,16 +2565,27 @@ __global__ __launch_bounds__(1024) void combine_pieces_wg_kernel(const uint32_t 
 // of m - 1 - k, 9.9 us for 64 x 16 MiB).
 // base: Shift_{2^i} bytes, i < kBaseMats, as GF(2) matrices (32 columns).
 constexpr uint32_t kBaseMats = 48;
+#ifndef LVK_LONG_TABS
+#define LVK_LONG_TABS 1
+#endif
 __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__restrict__ ws,
                                                            const uint4 *__restrict__ longs,
                                                            const uint32_t *__restrict__ part,
                                                            const uint32_t *__restrict__ base,
+                                                           const uint32_t *__restrict__ tabs,
                                                            uint32_t *__restrict__ out, uint32_t flags) {
-    __shared__ uint32_t M[kBaseMats * 32];
     const uint32_t nl = ws[kWsLongs];
     if (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64) >= nl) return;  // block-uniform
+#if !LVK_LONG_TABS
+    __shared__ uint32_t M[kBaseMats * 32];
     for (uint32_t i = threadIdx.x; i < kBaseMats * 32; i += blockDim.x) M[i] = base[i];
     __syncthreads();
+    auto shift = [&](uint32_t i, uint32_t v) { return gf2_apply(M + i * 32, v); };
+#else
+    // Shift_{2^i}(v) by four byte-table lookups (tables in HBM, L2-resident:
+    // 192 KiB for every i) instead of a staged 32-column matrix product
+    auto shift = [&](uint32_t i, uint32_t v) { return tab_shift(tabs + i * 1024u, v); };
+#endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
     for (uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < nl; w += nw) {
@@ -2590,18 +2601,18 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
             c <<= 1;
             ++lc;
         }
-        const uint32_t corr = gf2_apply(M + p * 32, 0xffffffffu);  // Shift_P(~0)
+        const uint32_t corr = shift(p, 0xffffffffu);  // Shift_P(~0)
         const int32_t pad = static_cast<int32_t>(64u * c - m);
         uint32_t acc = 0;
         for (uint32_t i = 0; i < c; ++i) {  // wave-uniform trip count
             const int32_t k = static_cast<int32_t>(lane * c + i) - pad;
             const uint32_t rk = k >= 0 ? part[r.y + static_cast<uint32_t>(k)] ^ (k ? corr : 0u) : 0u;
-            acc = (i ? gf2_apply(M + p * 32, acc) : 0u) ^ rk;
+            acc = (i ? shift(p, acc) : 0u) ^ rk;
         }
 #pragma unroll
         for (uint32_t t = 0; t < 6; ++t) {  // lane l joins lane l + 2^t: Shift_{c 2^t P}(left) ^ right
             const uint32_t right = __shfl_down(acc, 1u << t);
-            const uint32_t sh = gf2_apply(M + (p + lc + t) * 32, acc);
+            const uint32_t sh = shift(p + lc + t, acc);
             if ((lane & ((2u << t) - 1u)) == 0) acc = sh ^ right;
         }
         if (lane == 0) {
@@ -2722,6 +2733,7 @@ struct DevCtx {
     int cus = 0;
     uint4 *image[kImages] = {};  // per G (kGs), then the table image
     uint32_t *base_mats = nullptr;  // Shift_{2^i}, i < lvk::kBaseMats (combine_long_kernel)
+    uint32_t *base_tabs = nullptr;  // the same shifts as byte tables (4 x 256 words each)
     std::mutex ws_m;  // guards the map (entries are never erased)
     std::map<hipStream_t, std::unique_ptr<StreamWs>> ws;
     // long-block split: Shift matrices per piece length (immutable once built)
@@ -2824,6 +2836,15 @@ int current_ctx(DevCtx **out) {
             }
             LV_HIP(hipMalloc(&c.base_mats, bm.size() * 4));
             LV_HIP(hipMemcpy(c.base_mats, bm.data(), bm.size() * 4, hipMemcpyHostToDevice));
+            std::vector<uint32_t> bt(lvk::kBaseMats * 1024);
+            for (uint32_t i = 0; i < lvk::kBaseMats; ++i) {
+                uint32_t S[4][256];
+                lvgpu::shift_tables(1ull << i, S);
+                for (int j = 0; j < 4; ++j)
+                    for (int e = 0; e < 256; ++e) bt[i * 1024 + j * 256 + e] = S[j][e];
+            }
+            LV_HIP(hipMalloc(&c.base_tabs, bt.size() * 4));
+            LV_HIP(hipMemcpy(c.base_tabs, bt.data(), bt.size() * 4, hipMemcpyHostToDevice));
         }
         c.ready = true;
     }
@@ -3077,7 +3098,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     // invalidates the XCD's whole L2; and C3 via offsets -2 % from spills.)
     if (longs)
         hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(256), 0, s, ws, longs,
-                           part, c.base_mats, out, flags);
+                           part, c.base_mats, c.base_tabs, out, flags);
     return 0;
 }
 
