@@ -609,3 +609,31 @@ def test_offsets_api_one_key_batches(torch_dev, n, size, seeded):
     want = oracle_batch(arena.cpu().numpy().tobytes(), offs, np.full(n, size), seeds, True)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, bad[:10]
+
+
+@pytest.mark.parametrize("trial", range(6))
+def test_offsets_api_small_batches_random(torch_dev, trial):
+    """Random batches of 1-1,024 buffers (the one-launch sort, sort_small):
+    lengths 0 to 3 MiB with a few long ones split into pieces, overlapping
+    and unaligned offsets, seeded or not, masked or not -- every CRC against
+    the oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(1000 + trial)
+    n = int(rng.integers(1, 1025))
+    lens = rng.integers(0, 5000, size=n)
+    longs = rng.random(n) < 0.02
+    lens[longs] = rng.integers(16385, 3 << 20, size=int(longs.sum()))
+    total = int(lens.max()) + 4 * n + 4096
+    arena = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, 0x5A11 + trial)
+    offs = np.array([int(rng.integers(0, total - int(l) + 1)) for l in lens], dtype=np.int64)
+    seeded, masked = trial % 2 == 0, trial % 3 == 0
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    o = torch.from_numpy(offs).to(dev)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out = lvgpu.batch(arena, o, ln, sd, masked=masked)
+    got = out.cpu().numpy().view(np.uint32)
+    want = oracle_batch(arena.cpu().numpy().tobytes(), offs, lens, seeds, masked)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:10]]
