@@ -784,14 +784,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         if constexpr (FUSE) fuse_pieces(P, fm, g_ocrc, lane, wave);  // the barrier is workgroup-wide
         return;
     }
-    if constexpr (FUSE && LVK_FUSE_INFLIGHT) {
+    if constexpr (PIECES && LVK_FUSE_INFLIGHT) {
         // One round of <= 4 batches per group (pieces of <= 4 KiB): every
         // batch's loads in flight at once -- one memory round trip for the
         // whole walk, where the one-ahead prefetch of the loop below pays one
         // per batch (a 64 MiB call is 4 batches per wave).  1,024 x 64 KiB:
         // 17.4 -> 16.8 us.  (Requesting batches 1-3 before the table staging
-        // too spills 68-80 VGPRs.)
-        if (nb <= U) {
+        // too spills 68-80 VGPRs.)  The fused join always has one round; the
+        // two-launch split has one when the pieces fill at most one pass.
+        if (nb <= U && (FUSE || wblk0 + gstride >= P.n)) {
             uint4 v1[U], v2[U], v3[U];
 #pragma unroll
             for (uint32_t i = 0; i < U; ++i) {
@@ -807,8 +808,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
             if (nb > 2) fold_batch<false>(v2, A, L);
             if (nb > 3) fold_batch<false>(v3, A, L);
             const uint32_t X = merge_group<G, -1, -1, true>(A, L);
-            if (gl == 0) g_ocrc[wave][lane / G] = X;
-            fuse_pieces(P, fm, g_ocrc, lane, wave);
+            if constexpr (FUSE) {
+                if (gl == 0) g_ocrc[wave][lane / G] = X;
+                fuse_pieces(P, fm, g_ocrc, lane, wave);
+            } else {
+                if (gl == 0 && blk < P.n) P.out[blk] = X;  // the raw register, for combine_pieces_*
+            }
             return;
         }
     }
