@@ -938,7 +938,10 @@ constexpr uint32_t kWsBytes = 2;
 #endif
 constexpr uint32_t kWsIdent = 4;  // 1: the sorted list is the identity (one key, no split): see sort_scatter
 constexpr uint32_t kPieceBudget = 65536;  // piece entries per call (each split buffer takes <= kMaxPieces)
-constexpr uint32_t kMaxPieces = 1024;
+#ifndef LVK_MAX_PIECES  // pieces per split buffer (a lone 16 MiB buffer: 4,096 of 4 KiB, as the strided API cuts it)
+#define LVK_MAX_PIECES 4096
+#endif
+constexpr uint32_t kMaxPieces = LVK_MAX_PIECES;
 constexpr uint32_t kPieceFlag = 0x80000000u;  // output slot flag of a piece entry (slot < kPieceBudget)
 constexpr uint32_t kWsCls = kKeys;
 constexpr uint32_t kWsTot = kKeys + 8;
@@ -1130,7 +1133,7 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
         const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + kMaxPieces - 1) / kMaxPieces);
         p = p > pl ? p : pl;
         p = p > 12u ? p : 12u;
-        p = p < 22u ? p : 22u;  // L < 2^32: 4 MiB pieces keep m <= 1024 (and base matrices < kBaseMats)
+        p = p < 22u ? p : 22u;  // (L < 2^32: then p <= 20; base matrices stay < kBaseMats)
         if (L > (2ull << p)) m = static_cast<uint32_t>((L + (1ull << p) - 1) >> p);
     }
     const uint64_t want = __ballot(m > 0);
@@ -1278,12 +1281,16 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
 // device-atomic claims, so no pass waits for another and no counter needs
 // zeroing.  (By construction every split fits: sum m <= 16,384 + n pieces
 // and <= n long records, below the budgets.)  Each workgroup then claims its
-// chunk's sorted slots and writes its pieces, a contiguous slot range, one
-// slot per thread.  Same grid and chunks as the three-pass sort.
+// chunk's sorted slots, and writes an equal share of ALL the piece slots (a
+// binary search over the LDS prefix finds a slot's buffer): a lone 16 MiB
+// buffer is 4,096 pieces, 16 dependent rounds for the one workgroup of its
+// chunk.  The chunks are the three-pass sort's; the grid is at least
+// kSmallSortWgs workgroups (the extra ones write pieces only).
 #ifndef LVK_SMALL_SORT
 #define LVK_SMALL_SORT 1
 #endif
 constexpr uint32_t kSmallSort = 4 * kSortThreads;  // buffers
+constexpr uint32_t kSmallSortWgs = 64;
 __global__ __launch_bounds__(kSortThreads) void sort_small(const uint64_t *__restrict__ off,
                                                            const uint32_t *__restrict__ len, uint64_t n,
                                                            uint64_t chunk, uint32_t *__restrict__ ws,
@@ -1407,11 +1414,15 @@ __global__ __launch_bounds__(kSortThreads) void sort_small(const uint64_t *__res
         if (seed) sseed[pos] = sd;
         if (m) longs[lpre[i]] = make_uint4(static_cast<uint32_t>(i), mpre[i], m, pp[i]);
     }
-    // pieces of the chunk: slots [mpre[lo], mpre[hi]), one per thread
-    const uint32_t s0 = mpre[lo], s1 = mpre[hi];
+    // this workgroup's share of the piece slots [0, run_m), one per thread
+    const uint32_t per = (run_m + gridDim.x - 1) / gridDim.x;
+    const uint32_t s0 = min(blockIdx.x * per, run_m), s1 = min(s0 + per, run_m);
     for (uint32_t u = s0 + t; u < s1; u += kSortThreads) {
-        uint32_t j = static_cast<uint32_t>(lo);  // the chunk's buffer holding slot u (<= 16 buffers)
-        while (mpre[j + 1] <= u) ++j;
+        uint32_t j = 0, jh = static_cast<uint32_t>(n);  // the buffer holding slot u: the last j with mpre[j] <= u
+        while (jh - j > 1) {
+            const uint32_t mid = (j + jh) >> 1;
+            if (mpre[mid] <= u) j = mid; else jh = mid;
+        }
         const uint32_t mj = mpre[j + 1] - mpre[j], k = u - mpre[j];
         const uint32_t Lj = len[j];
         const uint64_t P = 1ull << pp[j];
@@ -2598,7 +2609,9 @@ __global__ __launch_bounds__(1024) void combine_pieces_wg_kernel(const uint32_t 
 // R_k = part ^ Shift_P(~0) and R(~seed, buffer) = XOR_k Shift_{(m-1-k) P}(R_k).  One wave
 // per buffer, Horner within lanes and a tree across them, every shift a
 // wave-uniform base matrix (round 2 before: per-lane shifts by the set bits
-// of m - 1 - k, 9.9 us for 64 x 16 MiB).
+// of m - 1 - k, 9.9 us for 64 x 16 MiB).  A lane's run of c pieces is up to
+// 8 independent Horner chains joined by an in-lane tree: each Horner step is
+// a dependent L2 round trip (~0.18 us), and 4,096 pieces are c = 64.
 // base: Shift_{2^i} bytes, i < kBaseMats, as GF(2) matrices (32 columns).
 constexpr uint32_t kBaseMats = 48;
 #ifndef LVK_LONG_TABS
@@ -2639,12 +2652,36 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
         }
         const uint32_t corr = shift(p, 0xffffffffu);  // Shift_P(~0)
         const int32_t pad = static_cast<int32_t>(64u * c - m);
-        uint32_t acc = 0;
-        for (uint32_t i = 0; i < c; ++i) {  // wave-uniform trip count
-            const int32_t k = static_cast<int32_t>(lane * c + i) - pad;
-            const uint32_t rk = k >= 0 ? part[r.y + static_cast<uint32_t>(k)] ^ (k ? corr : 0u) : 0u;
-            acc = (i ? shift(p, acc) : 0u) ^ rk;
+        // chains q < Q of d = c / Q consecutive pieces each (wave-uniform)
+        const uint32_t lq = lc < 3u ? lc : 3u, Q = 1u << lq, ld = lc - lq, d = 1u << ld;
+        // Branch-free body (every chain's loads issued before any wait; a
+        // guarded load per chain serialized them): chains q >= Q and front
+        // padding read slot 0 and add 0.
+        uint32_t ch[8];
+        auto piece = [&](uint32_t q, uint32_t i) {
+            const uint32_t j = lane * c + q * d + i;
+            const bool ok = q < Q && j >= static_cast<uint32_t>(pad);
+            const uint32_t k = ok ? j - static_cast<uint32_t>(pad) : 0u;
+            const uint32_t v = part[r.y + k];
+            return ok ? v ^ (k ? corr : 0u) : 0u;
+        };
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) ch[q] = piece(q, 0);
+        for (uint32_t i = 1; i < d; ++i) {  // wave-uniform trip count
+            uint32_t rk[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) rk[q] = piece(q, i);
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) ch[q] = shift(p, ch[q]) ^ rk[q];
         }
+#pragma unroll
+        for (uint32_t t = 0; t < 3; ++t) {  // chain q joins chain q + 2^t: Shift_{d 2^t P}(left) ^ right
+            if (t < lq) {
+#pragma unroll
+                for (uint32_t q = 0; q < 8; q += 2u << t) ch[q] = shift(p + ld + t, ch[q]) ^ ch[q + (1u << t)];
+            }
+        }
+        uint32_t acc = ch[0];
 #pragma unroll
         for (uint32_t t = 0; t < 6; ++t) {  // lane l joins lane l + 2^t: Shift_{c 2^t P}(left) ^ right
             const uint32_t right = __shfl_down(acc, 1u << t);
@@ -3099,7 +3136,8 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     uint4 *longs = n < lvk::kPieceFlag ? reinterpret_cast<uint4 *>(ws_bytes + lay.longs) : nullptr;
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
     if (n <= lvk::kSmallSort && LVK_SMALL_SORT) {  // one launch (sort_small)
-        hipLaunchKernelGGL(lvk::sort_small, g, b, 0, s, off, len, n, chunk, ws, ent, seed, sseed, longs);
+        const dim3 gs(static_cast<uint32_t>(std::max<uint64_t>(wgs, lvk::kSmallSortWgs)));
+        hipLaunchKernelGGL(lvk::sort_small, gs, b, 0, s, off, len, n, chunk, ws, ent, seed, sseed, longs);
     } else {
         hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M, ws, wgb);
         hipLaunchKernelGGL(lvk::sort_scan, dim3(lvk::kScanWgs), dim3(lvk::kScanThreads), 0, s, M,
