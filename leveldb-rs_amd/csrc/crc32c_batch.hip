@@ -2617,6 +2617,9 @@ constexpr uint32_t kBaseMats = 48;
 #ifndef LVK_LONG_TABS
 #define LVK_LONG_TABS 1
 #endif
+#ifndef LVK_LONG_LDSP  // Shift_P staged per wave for the Horner steps (d >= 2)
+#define LVK_LONG_LDSP 1
+#endif
 __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__restrict__ ws,
                                                            const uint4 *__restrict__ longs,
                                                            const uint32_t *__restrict__ part,
@@ -2637,6 +2640,10 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
 #endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
+#if LVK_LONG_TABS && LVK_LONG_LDSP
+    __shared__ uint32_t TP[4][1024];  // per wave: Shift_P of its record
+    uint32_t *const tp = TP[threadIdx.x >> 6];
+#endif
     for (uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < nl; w += nw) {
         const uint4 r = longs[w];  // {buffer, first, m, p}
         const uint32_t m = r.z, p = r.w;
@@ -2667,6 +2674,28 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
         };
 #pragma unroll
         for (uint32_t q = 0; q < 8; ++q) ch[q] = piece(q, 0);
+#if LVK_LONG_TABS && LVK_LONG_LDSP
+        // d - 1 dependent Shift_P steps: from an LDS copy (one HBM round trip
+        // to stage 4 KiB) instead of an L2 / HBM round trip each
+        if (d > 1) {  // wave-uniform
+            const uint4 *src = reinterpret_cast<const uint4 *>(tabs + p * 1024u);
+            uint4 *dst = reinterpret_cast<uint4 *>(tp);
+            const uint4 v0 = src[lane], v1 = src[64u + lane], v2 = src[128u + lane], v3 = src[192u + lane];
+            __builtin_amdgcn_wave_barrier();  // the previous record's reads of tp are done
+            dst[lane] = v0;
+            dst[64u + lane] = v1;
+            dst[128u + lane] = v2;
+            dst[192u + lane] = v3;
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (uint32_t i = 1; i < d; ++i) {  // wave-uniform trip count
+            uint32_t rk[8];
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) rk[q] = piece(q, i);
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) ch[q] = tab_shift(tp, ch[q]) ^ rk[q];
+        }
+#else
         for (uint32_t i = 1; i < d; ++i) {  // wave-uniform trip count
             uint32_t rk[8];
 #pragma unroll
@@ -2674,6 +2703,7 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
 #pragma unroll
             for (uint32_t q = 0; q < 8; ++q) ch[q] = shift(p, ch[q]) ^ rk[q];
         }
+#endif
 #pragma unroll
         for (uint32_t t = 0; t < 3; ++t) {  // chain q joins chain q + 2^t: Shift_{d 2^t P}(left) ^ right
             if (t < lq) {
