@@ -1368,17 +1368,24 @@ __global__ __launch_bounds__(kSortThreads) void sort_small(const uint64_t *__res
         mpre[kSmallSort] = run_m;
         lpre[kSmallSort] = run_l;
     }
-    // key starts (exclusive scan of the whole histogram) and this chunk's slots
+    // key starts (exclusive scan of the whole histogram) and this chunk's
+    // slots: a wave scan, then the earlier waves' totals (2 barriers, where a
+    // Hillis-Steele scan over LDS took 16)
+    static_assert(kKeys == kSortThreads, "one key per thread");
+    __shared__ uint32_t wtot[kSortThreads / 64];
     const uint32_t mineh = hall[t];
-    sc[t] = mineh;
-    __syncthreads();
-    for (uint32_t d = 1; d < kKeys; d <<= 1) {
-        const uint32_t x = t >= d ? sc[t - d] : 0u;
-        __syncthreads();
-        sc[t] += x;
-        __syncthreads();
+    uint32_t inc = mineh;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(inc, d);
+        if (lane >= d) inc += x;
     }
-    const uint32_t ks = sc[t] - mineh;
+    if (lane == 63) wtot[w] = inc;
+    __syncthreads();
+    for (uint32_t v = 0; v < w; ++v) inc += wtot[v];
+    sc[t] = inc;  // inclusive (block 0 reads other keys' entries below)
+    __syncthreads();
+    const uint32_t ks = inc - mineh;
     const uint32_t kc = t / kBuckets, knb = kBuckets - 1 - t % kBuckets;
     const bool ident_ok = mineh == static_cast<uint32_t>(n) && (kc <= 1 || (kc == 2 && (knb <= 16 || n >= 16384)));
     const bool ident = __syncthreads_or(LVK_IDENT && ident_ok && run_l == 0);
