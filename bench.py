@@ -8,11 +8,18 @@ One "step" = one batch CRC32C launch over this rank's whole synthetic batch,
 inputs already resident in HBM.  Default workload (N=1 headline, BASELINE.json
 configs[2]): 262,144 SSTable-sized 4 KiB blocks = 1 GiB per GPU, offsets
 i*4096, seed 0, splitmix64 payload generated on the device.  With N>1
-(torchrun) every rank checksums its own batch of the same shape (weak
-scaling, no data-path collective; the only collectives are the timing
-barrier and the max-over-ranks of the elapsed time).  `--scaling strong`
-splits ONE global batch (c5: 16,777,216 x 4 KiB = 64 GiB)
-into contiguous rank ranges instead (lvgpu.shard).
+every rank checksums its own batch of the same shape (weak scaling, no
+data-path collective; the only collectives are the timing barrier, the
+max-over-ranks of the elapsed time and the gather of per-rank records).
+`--scaling strong` splits ONE global batch (c5: 16,777,216 x 4 KiB = 64 GiB,
+SURVEY 8d C5 / 8e) into contiguous rank ranges instead (lvgpu.shard).
+
+N>1 runs either under `python -m torch.distributed.run --nproc-per-node N
+... bench.py --gpus N` or as plain `python bench.py --gpus N`, which starts
+the N ranks itself (lvgpu.shard.launch, torchrun's environment, env://
+rendezvous on 127.0.0.1) before anything touches a GPU.  A WORLD_SIZE that
+differs from --gpus is an error.  Every rank's record in `per_gpu` carries
+its device's PCI bus id, so N distinct devices are visible in the line.
 
 Before the W warmup steps a `settle` phase runs back-to-back launches until
 the chip's idle->busy power transient has passed (reported in the JSON line,
@@ -28,6 +35,7 @@ import argparse
 import ctypes
 import json
 import os
+import socket
 import sys
 import time
 
@@ -86,6 +94,8 @@ def parse():
     p.add_argument("--wal-device", action="store_true",
                    help="SURVEY 8f row 1 in HBM: lv_wal_scan_device (framing + CRC) of a ~1 GiB log already on "
                         "the GPU; one JSON line with a roofline")
+    p.add_argument("--as-rank", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("--as-world", type=int, default=1, help=argparse.SUPPRESS)
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
                    help="auto: measure roofline.traffic in a child rocprofv3 --pmc FETCH_SIZE pass")
     return p.parse_args()
@@ -189,13 +199,17 @@ def read_pmc_traffic(path):
     return 2.0 * 1024.0 * sum(sum(v) / len(v) for v in per.values())
 
 
-def measure_traffic(args):
+def measure_traffic(args, shard_rank=0, shard_world=1):
     """Child process: rocprofv3 --pmc FETCH_SIZE over a short run of the same
-    workload (a separate pass, kernel counters only).  Returns bytes/launch."""
+    workload (a separate pass, kernel counters only).  Returns bytes/launch.
+    In an N-rank job rank 0 runs it after the timed region, as a single
+    process replaying its own shard (--as-rank/--as-world; the torchrun
+    variables are dropped so the child does not join the process group)."""
     import glob
     import shutil
     import subprocess
     import tempfile
+    from lvgpu import shard
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not found"
@@ -205,12 +219,14 @@ def measure_traffic(args):
     cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
            sys.executable, os.path.abspath(__file__), "--steps", "10", "--warmup", "60", "--cpu-seconds", "0",
            "--traffic", "off", "--no-settle", "--workload", args.workload, "--api", args.api,
-           "--scaling", args.scaling]  # bytes per launch do not depend on the clock state: no settle
+           "--scaling", args.scaling,  # bytes per launch do not depend on the clock state: no settle
+           "--as-rank", str(shard_rank), "--as-world", str(shard_world)]
     if args.group:
         cmd += ["--group", str(args.group)]
     if args.blocks:
         cmd += ["--blocks", str(args.blocks)]
-    env = dict(os.environ, TMPDIR="/tmp")
+    env = {k: v for k, v in os.environ.items() if k not in shard.RANK_ENV and k != "LVGPU_LAUNCHER"}
+    env["TMPDIR"] = "/tmp"
     try:
         subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                        timeout=300, check=True)
@@ -882,6 +898,17 @@ def global_lengths(name):
 
 def main():
     args = parse()
+    single = [m for m in ("wal", "c1", "e2e", "sweep", "table", "hash", "long", "wal_device") if getattr(args, m)]
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if single and args.gpus > 1:
+        raise SystemExit(f"--{single[0].replace('_', '-')} is a single-GPU diagnostic; run it with --gpus 1")
+    from lvgpu import shard
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without torchrun: start the N ranks here
+        # (one process per GPU, env:// rendezvous on 127.0.0.1).  This process
+        # never touches a GPU; rank 0's JSON line is the output.
+        sys.exit(shard.self_launch(__file__, sys.argv[1:], args.gpus))
     if args.wal:
         return wal_bench(args)
     if args.c1:
@@ -898,13 +925,15 @@ def main():
         return long_bench(args)
     if args.wal_device:
         return wal_device_bench(args)
+    world, rank, local = shard.world_from_env(args.gpus)
+    # --as-rank/--as-world: a single process rebuilds rank R's shard of a
+    # W-rank job (the PMC child pass of measure_traffic runs this way).
+    shard_rank, shard_world = (args.as_rank, args.as_world) if args.as_world > 1 else (rank, world)
+    if args.as_world > 1 and world > 1:
+        raise SystemExit("--as-rank/--as-world replay one rank's shard in a single process")
     import torch
     import lvgpu
-    from lvgpu import shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     # LVGPU_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs
     # than ranks (ranks share devices round-robin; RCCL refuses two ranks on
@@ -912,19 +941,27 @@ def main():
     backend = os.environ.get("LVGPU_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
+    elif world > 1 and local >= torch.cuda.device_count():
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} visible GPUs "
+                         f"(--gpus {args.gpus} needs one GPU per rank; LVGPU_BENCH_BACKEND=gloo to share)")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group(backend)
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {world}")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     lvgpu.device_init()
 
     if args.scaling == "strong":
-        arena, off, ln, sh, desc = build_shard(torch, lvgpu, args, dev, rank, world)
+        arena, off, ln, sh, desc = build_shard(torch, lvgpu, args, dev, shard_rank, shard_world)
         nbytes, n = sh.payload_bytes, sh.n
     else:
-        arena, off, ln, nbytes, desc = build_workload(torch, lvgpu, args.workload, dev, rank, args.blocks)
+        arena, off, ln, nbytes, desc = build_workload(torch, lvgpu, args.workload, dev, shard_rank, args.blocks)
         n = off.numel()
     out = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
@@ -967,7 +1004,11 @@ def main():
         print("per-launch ms:", " ".join(f"{x:.4f}" for x in kern_seq), file=sys.stderr)
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
     # per-GPU figures: each rank's own timed-pass rate and kernel rate
-    own = {"rank": rank, "device": local, "payload_bytes": nbytes,
+    props = torch.cuda.get_device_properties(dev)
+    own = {"rank": rank, "device": local,
+           "pci_bus_id": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+           "gpu_uuid": str(getattr(props, "uuid", "")), "hostname": socket.gethostname(),
+           "payload_bytes": nbytes,
            "GiB_per_s": round(nbytes * args.steps / 2**30 / el_own, 2),
            "kernel_GB_per_s": round(nbytes / (kern_avg_ms * 1e-3) / 1e9, 1),
            "frac_of_8TBps": round(nbytes / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -980,16 +1021,22 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        if world == 1 and args.cpu_seconds > 0:
+        # after the timed region: on rank 0 at every N (the other ranks wait
+        # at the closing barrier), over rank 0's own shard
+        if args.cpu_seconds > 0:
             cpu, crcs, k = cpu_baseline(torch, arena, off, ln, args.cpu_seconds)
             got = out[:k].cpu().numpy().view("uint32")
             if not (got == crcs).all():
                 raise SystemExit("bench parity check failed: GPU CRCs differ from the oracle on the sample")
         traffic, tsrc = (None, "not collected")
-        if args.traffic == "auto" and world == 1:
-            traffic, tsrc = measure_traffic(args)
+        if args.traffic == "auto":
+            traffic, tsrc = measure_traffic(args, shard_rank, shard_world)
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "world_size": dist.get_world_size() if dist else 1,
+            "launcher": os.environ.get("LVGPU_LAUNCHER", "torch.distributed.run" if world > 1 else "single process"),
+            "backend": backend if world > 1 else None,
+            "distinct_devices": len({(r["hostname"], r["pci_bus_id"]) for r in per_rank}),
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 payload generated in HBM)",

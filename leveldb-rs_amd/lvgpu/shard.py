@@ -7,18 +7,123 @@ Zipf mix of 32 B records and 64 KiB blocks still loads every GPU equally;
 fixed-size blocks (C3/C5) split by count.
 
 The functions below are the whole N > 1 host logic of `bench.py`: the
-rank's range of a global batch (`RankShard`), the timed region between
-barriers with the max over ranks (`timed_steps`), and the gather of per-rank
-figures into the aggregate (`gather_ranks`, `aggregate`).  The world-size-2
-gloo test (tests/test_dist.py) drives the same functions with the CPU oracle
-as the per-rank compute.
+process launcher (`launch`: `bench.py --gpus N` started without torchrun
+starts its N ranks itself), the rank's range of a global batch
+(`RankShard`), the timed region between barriers with the max over ranks
+(`timed_steps`), and the gather of per-rank figures into the aggregate
+(`gather_ranks`, `aggregate`).  The world-size-2 gloo tests
+(tests/test_dist.py) drive the same functions, the launcher included, with
+the CPU oracle as the per-rank compute.
 """
 from __future__ import annotations
 
+import os
+import signal
+import socket
+import subprocess
+import sys
 import time
 from dataclasses import dataclass
 
 import numpy as np
+
+# torchrun's rendezvous variables; `launch` sets them for every child.
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR", "MASTER_PORT")
+
+
+def world_from_env(requested: int, env=None):
+    """(world, rank, local_rank) of this process.
+
+    Without WORLD_SIZE the process is a plain single-rank run (or the parent
+    of a self-launch, see `launch`).  With WORLD_SIZE (torchrun, or a child
+    of `launch`) the world must be the size the caller asked for: a bench
+    told `--gpus 8` that finds itself in a world of 4 would time the wrong
+    job, so that is an error, not a warning."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" not in env:
+        return 1, 0, 0
+    world = int(env["WORLD_SIZE"])
+    if world != requested:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {requested}: launch {requested} ranks "
+                         f"(torchrun --nproc-per-node {requested}) or pass --gpus {world}")
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", str(rank)))
+    if not (0 <= rank < world):
+        raise SystemExit(f"RANK={rank} outside WORLD_SIZE={world}")
+    return world, rank, local
+
+
+def free_port(host: str = "127.0.0.1") -> int:
+    s = socket.socket()
+    s.bind((host, 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(argv, nprocs: int, env=None, master_addr: str = "127.0.0.1", master_port: int = None,
+           timeout: float = None) -> int:
+    """Start `nprocs` ranks of `argv` on this node, torchrun-style, and wait.
+
+    Child r gets RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE =
+    nprocs, GROUP_RANK = 0 and MASTER_ADDR/MASTER_PORT (a free local port
+    unless given), so `torch.distributed.init_process_group()` rendezvouses
+    over env:// exactly as under `python -m torch.distributed.run`.  The
+    children inherit stdout/stderr: rank 0's JSON line is the job's output.
+
+    The parent never initialises a GPU (it imports neither torch nor the
+    library): the children are started as new processes, not forked from a
+    process holding a device context, and not exec'd over it.  If any child
+    fails the others are terminated (by their own pid, never by pattern) and
+    the first non-zero exit status is returned; 0 when all succeed."""
+    if nprocs < 1:
+        raise ValueError("nprocs must be >= 1")
+    base = dict(os.environ if env is None else env)
+    for k in RANK_ENV:
+        base.pop(k, None)
+    port = master_port or free_port(master_addr)
+    procs = []
+    try:
+        for r in range(nprocs):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                     LOCAL_WORLD_SIZE=str(nprocs), GROUP_RANK="0", MASTER_ADDR=master_addr,
+                     MASTER_PORT=str(port), LVGPU_LAUNCHER="lvgpu.shard.launch")
+            procs.append(subprocess.Popen(list(argv), env=e))
+        t0 = time.monotonic()
+        codes = [None] * nprocs
+        while any(c is None for c in codes):
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    codes[i] = p.poll()
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                break
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                bad = [124]
+                break
+            time.sleep(0.05)
+        else:
+            return 0
+        for p in procs:  # one rank failed (or timed out): end the rest
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        return bad[0] if bad[0] > 0 else 128 - bad[0]  # Popen reports a signal as -N
+    except BaseException:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise
+
+
+def self_launch(script: str, args, nprocs: int) -> int:
+    """`python <script> <args>` as `nprocs` ranks (see `launch`)."""
+    return launch([sys.executable, os.path.abspath(script)] + list(args), nprocs)
 
 
 def shard_bounds(lengths, world: int):
