@@ -855,6 +855,21 @@ def settle(torch, step, stream, min_s=0.6, max_s=3.0, chunk=20, window=8, tol=0.
             "why": "idle->busy power transient of the chip (tools/ramp_probe.py); not part of warmup"}
 
 
+class _stdout_to_stderr:
+    """Points file descriptor 1 at stderr for the duration (C/C++ libraries
+    write to the descriptor, not to sys.stdout)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def build_shard(torch, lvgpu, args, dev, rank, world):
     """Strong scaling: ONE global batch, this rank's
     contiguous slice of it.  c5: 16,777,216 x 4 KiB = 64 GiB; c3: 262,144 x
@@ -947,10 +962,12 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group(backend, device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group(backend)
+        with _stdout_to_stderr():  # the backends' C++ chatter must not reach the one JSON line's stdout
+            if backend == "nccl":
+                dist.init_process_group(backend, device_id=torch.device(f"cuda:{local}"))
+            else:
+                dist.init_process_group(backend)
+                dist.barrier()  # gloo prints its peer connections lazily
         if dist.get_world_size() != world:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {world}")
     dev = torch.device(f"cuda:{local}")

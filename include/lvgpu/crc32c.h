@@ -121,6 +121,16 @@ const char *lv_version(void);
  * "" before any).  Lets tests assert which path a geometry takes. */
 const char *lv_crc32c_last_kernel(void);
 
+/* Debug query: what the library's host entry points (lv_crc32c_batch_host,
+ * lv_crc32c_batch_multi*, lv_wal_scan_host, lv_sst_verify_blocks_host) have
+ * moved and allocated on `device` since the process started.  Fills
+ * out[0..min(n, 3)): [0] bytes copied host -> device (payload, metadata and
+ * handles), [1] bytes copied device -> host, [2] device or pinned-host
+ * allocations the library made on the device (hipMalloc / hipHostMalloc).
+ * Lets tests assert that a multi-device batch ships each device only its
+ * buffers and that cached host paths stop allocating.  0 or LV_ERR_INVALID. */
+int lv_device_counters(int device, uint64_t *out, size_t n);
+
 /* ---- synthetic data (bench / tests) ------------------------------------- */
 
 /* d_dst[k] = byte ((begin+k) & 7) of splitmix64(seed ^ ((begin+k) >> 3)) for

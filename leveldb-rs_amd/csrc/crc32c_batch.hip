@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -1133,7 +1134,12 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
         const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + kMaxPieces - 1) / kMaxPieces);
         p = p > pl ? p : pl;
         p = p > 12u ? p : 12u;
-        p = p < 22u ? p : 22u;  // (L < 2^32: then p <= 20; base matrices stay < kBaseMats)
+        // No lower cap than 31: P >= batch bytes / 16,384 must hold for every
+        // batch (it bounds sum m <= 16,384 + 8,192 and the split buffers <= 8,192,
+        // inside kPieceBudget and kPieceBudget / 2).  A split needs L > 2P and
+        // L < 2^32, so split buffers have p <= 30, and the join's shifts
+        // Shift_{2^i}, i <= p + lc + 5 <= 30 + 6 + 5, stay below kBaseMats.
+        p = p < 31u ? p : 31u;
         if (L > (2ull << p)) m = static_cast<uint32_t>((L + (1ull << p) - 1) >> p);
     }
     const uint64_t want = __ballot(m > 0);
@@ -1154,9 +1160,10 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
     pb = __shfl(pb, 0);
     lb = __shfl(lb, 0);
     const uint32_t base = pb + incl - m;
-    // (both limits hold by construction -- sum of m <= 16,384 + 8,192 and at
-    // most 8,192 buffers longer than 2P >= batch bytes / 8,192 -- and are
-    // checked anyway: a claim past them leaves its buffer whole)
+    // (both limits hold by construction, since P >= batch bytes / 16,384 for
+    // every batch: sum of m <= 16,384 + 8,192 and at most 8,192 buffers longer
+    // than 2P >= batch bytes / 8,192 -- and are checked anyway: a claim past
+    // them leaves its buffer whole)
     const uint32_t li = lb + static_cast<uint32_t>(__popcll(want & ((1ull << lane) - 1ull)));
     const bool fits = m > 0 && static_cast<uint64_t>(base) + m <= kPieceBudget && li < kPieceBudget / 2;
     if (m > 0 && li < kPieceBudget / 2)  // long record (m = 0 when not split: combine_long_kernel skips it)
@@ -1279,8 +1286,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
 // payload bytes and every buffer's split (pieces m_i, log2 piece length p_i);
 // piece slots and long-record indices are index-order prefix sums instead of
 // device-atomic claims, so no pass waits for another and no counter needs
-// zeroing.  (By construction every split fits: sum m <= 16,384 + n pieces
-// and <= n long records, below the budgets.)  Each workgroup then claims its
+// zeroing.  (By construction every split fits: P >= batch bytes / 16,384,
+// so sum m <= 16,384 + n pieces and <= n long records, below the budgets.)  Each workgroup then claims its
 // chunk's sorted slots, and writes an equal share of ALL the piece slots (a
 // binary search over the LDS prefix finds a slot's buffer): a lone 16 MiB
 // buffer is 4,096 pieces, 16 dependent rounds for the one workgroup of its
@@ -1333,7 +1340,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_small(const uint64_t *__res
             const uint32_t pl = ceil_log2((static_cast<uint64_t>(l[e]) + kMaxPieces - 1) / kMaxPieces);
             p = p > pl ? p : pl;
             p = p > 12u ? p : 12u;
-            p = p < 22u ? p : 22u;
+            p = p < 31u ? p : 31u;  // split_wave's bound (see there)
             if (l[e] > (2ull << p)) m = static_cast<uint32_t>((l[e] + (1ull << p) - 1) >> p);
         }
         // exclusive scans over t of m and (m > 0), plus the running totals of rows e' < e
@@ -2332,8 +2339,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t grid = gridDim.x;
     const uint32_t n23 = cls[6] + cls[7];
-    // pieces of split long buffers (walked after classes 2+3; every split
-    // buffer is class 3, so n23 > 0 whenever there are pieces)
+    // pieces of split long buffers (walked after classes 2+3; a split buffer
+    // is longer than 16 KiB, so class 2 or 3, and n23 > 0 whenever there are
+    // pieces)
     const uint32_t np = P.part ? min(ws[kWsPieces], kPieceBudget) : 0u;
     // With no large buffers at all, every wave walks the small classes.
 #if LVK_SMALL_ALL
@@ -2633,7 +2641,8 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
                                                            const uint32_t *__restrict__ base,
                                                            const uint32_t *__restrict__ tabs,
                                                            uint32_t *__restrict__ out, uint32_t flags) {
-    const uint32_t nl = ws[kWsLongs];
+    // the counter counts every claim; records exist only below the budget
+    const uint32_t nl = min(ws[kWsLongs], kPieceBudget / 2);
     if (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64) >= nl) return;  // block-uniform
 #if !LVK_LONG_TABS
     __shared__ uint32_t M[kBaseMats * 32];
@@ -2869,12 +2878,25 @@ struct DevCtx {
 
 constexpr size_t kStageBytes = 64ull << 20;  // pinned staging slot for pageable input
 
+// lv_device_counters: per-device host-path traffic and allocations
+struct DevCounters {
+    std::atomic<uint64_t> h2d{0}, d2h{0}, allocs{0};
+};
+DevCounters g_count[64];
+
+DevCounters &counters() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) d = 0;
+    return g_count[d];
+}
+
 int grow_dev(uint8_t **p, size_t *cap, size_t need) {
     if (*cap >= need) return 0;
     if (*p) LV_HIP(hipFree(*p));
     *p = nullptr;
     *cap = 0;
     LV_HIP(hipMalloc(p, need));
+    counters().allocs++;
     *cap = need;
     return 0;
 }
@@ -2885,6 +2907,7 @@ int grow_pinned(uint8_t **p, size_t *cap, size_t need) {
     *p = nullptr;
     *cap = 0;
     LV_HIP(hipHostMalloc(p, need, hipHostMallocDefault));
+    counters().allocs++;
     *cap = need;
     return 0;
 }
@@ -2935,6 +2958,7 @@ int current_ctx(DevCtx **out) {
         for (int i = 0; i < kImages; ++i) {
             const auto &im = host_image(i);
             LV_HIP(hipMalloc(&c.image[i], im.size() * 4));
+            counters().allocs++;
             LV_HIP(hipMemcpy(c.image[i], im.data(), im.size() * 4, hipMemcpyHostToDevice));
         }
         {
@@ -2945,6 +2969,7 @@ int current_ctx(DevCtx **out) {
                 m = m.then(m);  // Shift_{2^(i+1)}
             }
             LV_HIP(hipMalloc(&c.base_mats, bm.size() * 4));
+            counters().allocs++;
             LV_HIP(hipMemcpy(c.base_mats, bm.data(), bm.size() * 4, hipMemcpyHostToDevice));
             std::vector<uint32_t> bt(lvk::kBaseMats * 1024);
             for (uint32_t i = 0; i < lvk::kBaseMats; ++i) {
@@ -2954,6 +2979,7 @@ int current_ctx(DevCtx **out) {
                     for (int e = 0; e < 256; ++e) bt[i * 1024 + j * 256 + e] = S[j][e];
             }
             LV_HIP(hipMalloc(&c.base_tabs, bt.size() * 4));
+            counters().allocs++;
             LV_HIP(hipMemcpy(c.base_tabs, bt.data(), bt.size() * 4, hipMemcpyHostToDevice));
         }
         c.ready = true;
@@ -3083,6 +3109,7 @@ int stream_ws_bytes(DevCtx &c, hipStream_t s, size_t need, uint8_t **out, std::u
         w->p = nullptr;
         w->cap = 0;
         LV_HIP(hipMalloc(&w->p, need));
+        counters().allocs++;
         w->cap = need;
     }
     *out = w->p;
@@ -3109,6 +3136,7 @@ int piece_mats(DevCtx &c, uint64_t plen, const uint32_t **out) {
         }
         uint32_t *p = nullptr;
         LV_HIP(hipMalloc(&p, h.size() * 4));
+        counters().allocs++;
         LV_HIP(hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         d = p;
     }
@@ -3131,6 +3159,7 @@ int piece_tabs(DevCtx &c, uint64_t plen, const uint32_t **out) {
         }
         uint32_t *p = nullptr;
         LV_HIP(hipMalloc(&p, h.size() * 4));
+        counters().allocs++;
         LV_HIP(hipMemcpy(p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
         d = p;
     }
@@ -3289,6 +3318,13 @@ const char *lv_last_error(void) { return g_err.c_str(); }
 const char *lv_version(void) { return "lvgpu 0.2.0 gfx950"; }
 
 const char *lv_crc32c_last_kernel(void) { return g_kernel; }
+
+int lv_device_counters(int device, uint64_t *out, size_t n) {
+    if (device < 0 || device >= 64 || (!out && n)) return set_err(LV_ERR_INVALID, "device index or null pointer");
+    const uint64_t v[3] = {g_count[device].h2d.load(), g_count[device].d2h.load(), g_count[device].allocs.load()};
+    for (size_t i = 0; i < n && i < 3; ++i) out[i] = v[i];
+    return LV_OK;
+}
 
 int lv_device_init(void) {
     DevCtx *c = nullptr;
@@ -3514,6 +3550,7 @@ static int upload_locked(DevCtx &c, const uint8_t *h, size_t bytes, size_t pad) 
     // DMA straight from pinned/registered memory; otherwise a two-slot
     // pipeline (parallel memcpy into one pinned slot while the other slot's
     // H2D runs)
+    counters().h2d += bytes;
     if (is_pinned(h)) {
         LV_HIP(hipMemcpyAsync(c.d_arena, h, bytes, hipMemcpyHostToDevice, s));
         return LV_OK;
@@ -3591,6 +3628,9 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     }
     return check_launch();
 }
+
+void count_h2d(uint64_t bytes) { counters().h2d += bytes; }
+void count_d2h(uint64_t bytes) { counters().d2h += bytes; }
 
 int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d) {
     (void)hp;  // the lock it holds is the device's host_m
@@ -3692,6 +3732,7 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     std::memcpy(c->h_meta + n * 8, h_len, n * 4);
     if (h_seed) std::memcpy(c->h_meta + n * 12, h_seed, n * 4);
     LV_HIP(hipMemcpyAsync(d_off, c->h_meta, n * (h_seed ? 16 : 12), hipMemcpyHostToDevice, s));
+    counters().h2d += n * (h_seed ? 16 : 12);
     uint8_t *ws = nullptr;
     std::unique_lock<std::mutex> ws_lk;
     if (int rc = stream_ws(*c, s, n, &ws, &ws_lk)) return rc;
@@ -3699,6 +3740,7 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
         return rc;
     if (int rc = check_launch()) return rc;
     LV_HIP(hipMemcpyAsync(c->h_meta, d_out, n * 4, hipMemcpyDeviceToHost, s));
+    counters().d2h += n * 4;
     LV_HIP(hipStreamSynchronize(s));
     std::memcpy(h_out, c->h_meta, n * 4);
     return LV_OK;

@@ -1,10 +1,22 @@
 // Multi-GPU host batch (SURVEY 8b `lv_crc32c_batch_multi`, 8e): buffers are
 // independent, so the batch is split into contiguous buffer ranges balanced
 // by payload bytes (prefix sum of lengths), one range per device and one host
-// thread per device; each device receives only its range's arena span and
+// thread per device; each device receives only its range's buffers and
 // metadata and writes back its slice of out[].  No collective, no peer
 // traffic.
+//
+// What "its range's buffers" costs on the bus depends on where they lie.
+// Byte-packed buffers in index order (a log, a table file) occupy one span
+// about the size of their payload, which ships as is.  Buffers listed in any
+// other order (shuffled offsets, a gather over a large arena) can spread a
+// range over the whole arena: shipping the span [min off, max end) would send
+// every device ~the whole arena.  When the span exceeds kPackRatio x the
+// range's payload (plus kPackSlack), the range's buffers are packed into a
+// contiguous host copy first, in index order, so the device receives its
+// payload and nothing else; the pack is one host memcpy of the payload,
+// the same work the pageable upload's staging copy does anyway.
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -33,6 +45,9 @@ struct Shard {
     std::string err;
 };
 
+constexpr double kPackRatio = 1.5;
+constexpr uint64_t kPackSlack = 1ull << 20;
+
 }  // namespace
 
 extern "C" {
@@ -54,14 +69,30 @@ int lv_crc32c_batch_multi_devices(const uint8_t *h_arena, size_t arena_bytes, co
         if (b[r] == b[r + 1]) continue;
         th.emplace_back([&, r] {
             const size_t lo = b[r], cnt = b[r + 1] - b[r];
-            uint64_t first = UINT64_MAX, last = 0;
+            uint64_t first = UINT64_MAX, last = 0, payload = 0;
             for (size_t i = lo; i < lo + cnt; ++i) {
                 first = std::min(first, h_off[i]);
                 last = std::max(last, h_off[i] + h_len[i]);
+                payload += h_len[i];
             }
             std::vector<uint64_t> off(h_off + lo, h_off + lo + cnt);
-            for (auto &o : off) o -= first;  // this device's span starts at `first`
-            res[r].rc = lv_crc32c_batch_host(h_arena + first, last - first, off.data(), h_len + lo,
+            const uint8_t *span = h_arena + first;
+            uint64_t span_bytes = last - first;
+            std::vector<uint8_t> packed;
+            if (static_cast<double>(span_bytes) > kPackRatio * static_cast<double>(payload) + kPackSlack) {
+                packed.resize(payload ? payload : 1);  // non-null even for all-empty buffers
+                uint64_t pos = 0;
+                for (size_t k = 0; k < cnt; ++k) {
+                    std::memcpy(packed.data() + pos, h_arena + h_off[lo + k], h_len[lo + k]);
+                    off[k] = pos;
+                    pos += h_len[lo + k];
+                }
+                span = packed.data();
+                span_bytes = payload;
+            } else {
+                for (auto &o : off) o -= first;  // this device's span starts at `first`
+            }
+            res[r].rc = lv_crc32c_batch_host(span, span_bytes, off.data(), h_len + lo,
                                              h_seed ? h_seed + lo : nullptr, h_out + lo, cnt, flags, devices[r]);
             if (res[r].rc) res[r].err = lv_last_error();
         });

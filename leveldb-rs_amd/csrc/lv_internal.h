@@ -47,4 +47,8 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
                       const uint8_t *d_types, size_t n, uint32_t *d_status, uint32_t *d_crc, void *stream);
 // Cached device scratch buffer `slot` (0..1) of the HostPath's device, >= bytes.
 int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d);
+// lv_device_counters bookkeeping for host copies made outside
+// crc32c_batch.hip (current device).
+void count_h2d(uint64_t bytes);
+void count_d2h(uint64_t bytes);
 }

@@ -46,38 +46,40 @@ int lv_sst_verify_blocks_device(const uint8_t *d_file, uint64_t file_bytes, cons
     return lvgpu_internal::launch_sst_blocks(false, d_file, file_bytes, d_handles, nullptr, n, d_status, d_crc, stream);
 }
 
+// The file goes to the device through the device's host path (cached arena;
+// pinned input: one DMA, pageable: pipelined pinned staging), the handles and
+// the status words through its cached scratch buffer, as lv_wal_scan_host
+// does: after the first call of a given size nothing is allocated on the
+// device.
 int lv_sst_verify_blocks_host(const uint8_t *file, uint64_t file_bytes, const uint64_t *handles, size_t n,
                               uint32_t *status, int device) {
     lvgpu_internal::clear_error();
     if (n == 0) return LV_OK;
     if ((!file && file_bytes) || !handles || !status)
         return lvgpu_internal::set_error(LV_ERR_INVALID, "null host pointer");
-    hipStream_t s = nullptr;
-    uint8_t *d_file = nullptr;
-    uint64_t *d_h = nullptr;
-    uint32_t *d_st = nullptr;
-    int rc = LV_OK;
+    if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 blocks per call");
+    lvgpu_internal::HostPath hp;
+    if (int rc = lvgpu_internal::host_upload(device, file, file_bytes, 16, &hp)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(hp.stream);
+    const size_t hbytes = n * 16, sbytes = (n * 4 + 15) & ~static_cast<size_t>(15);
+    uint8_t *scr = nullptr;
+    if (int rc = lvgpu_internal::host_scratch(&hp, 0, hbytes + sbytes, &scr)) return rc;
+    uint64_t *d_h = reinterpret_cast<uint64_t *>(scr);
+    uint32_t *d_st = reinterpret_cast<uint32_t *>(scr + hbytes);
     auto hip = [&](hipError_t e, const char *what) {
-        if (e != hipSuccess && rc == LV_OK)
-            rc = lvgpu_internal::set_error(static_cast<int>(e), (std::string(what) + ": " + hipGetErrorString(e)).c_str());
-        return rc == LV_OK;
+        if (e == hipSuccess) return LV_OK;
+        (void)hipStreamSynchronize(s);
+        return lvgpu_internal::set_error(static_cast<int>(e), (std::string(what) + ": " + hipGetErrorString(e)).c_str());
     };
-    lvgpu_internal::DeviceGuard dg;  // the caller's current device comes back on return
-    if (int e = dg.set(device)) return e;
-    if (hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream") &&
-        hip(hipMalloc(&d_file, file_bytes + 16), "hipMalloc") && hip(hipMalloc(&d_h, n * 16), "hipMalloc") &&
-        hip(hipMalloc(&d_st, n * 4), "hipMalloc") &&
-        hip(hipMemcpyAsync(d_file, file, file_bytes, hipMemcpyHostToDevice, s), "H2D") &&
-        hip(hipMemcpyAsync(d_h, handles, n * 16, hipMemcpyHostToDevice, s), "H2D")) {
-        rc = lv_sst_verify_blocks_device(d_file, file_bytes, d_h, n, d_st, nullptr, s);
-        if (rc == LV_OK) hip(hipMemcpyAsync(status, d_st, n * 4, hipMemcpyDeviceToHost, s), "D2H");
-        if (rc == LV_OK) hip(hipStreamSynchronize(s), "sync");
+    if (int rc = hip(hipMemcpyAsync(d_h, handles, hbytes, hipMemcpyHostToDevice, s), "H2D")) return rc;
+    lvgpu_internal::count_h2d(hbytes);
+    if (int rc = lv_sst_verify_blocks_device(hp.d_arena, file_bytes, d_h, n, d_st, nullptr, s)) {
+        (void)hipStreamSynchronize(s);
+        return rc;
     }
-    if (s) (void)hipStreamSynchronize(s);
-    for (void *p : {static_cast<void *>(d_file), static_cast<void *>(d_h), static_cast<void *>(d_st)})
-        if (p) (void)hipFree(p);
-    if (s) (void)hipStreamDestroy(s);
-    return rc;
+    if (int rc = hip(hipMemcpyAsync(status, d_st, n * 4, hipMemcpyDeviceToHost, s), "D2H")) return rc;
+    lvgpu_internal::count_d2h(n * 4);
+    return hip(hipStreamSynchronize(s), "sync");
 }
 
 }  // extern "C"

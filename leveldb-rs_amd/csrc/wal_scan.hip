@@ -65,6 +65,7 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
             cap = count;
             continue;
         }
+        lvgpu_internal::count_d2h(8 + count * 16);
         scan->off.resize(count);
         scan->crc.resize(count);
         scan->info.resize(count);

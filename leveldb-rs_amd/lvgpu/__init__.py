@@ -110,6 +110,8 @@ def lib() -> ctypes.CDLL:
     L.lv_version.argtypes = []
     L.lv_crc32c_last_kernel.restype = ctypes.c_char_p
     L.lv_crc32c_last_kernel.argtypes = []
+    L.lv_device_counters.restype = ctypes.c_int
+    L.lv_device_counters.argtypes = [ctypes.c_int, vp, sz]
     L.lv_fill_splitmix.restype = ctypes.c_int
     L.lv_fill_splitmix.argtypes = [vp, u64, u64, u64, vp]
     _lib = L
@@ -306,3 +308,11 @@ def version() -> str:
 def last_kernel() -> str:
     """Kernel the calling thread's last batch call launched (debug query)."""
     return lib().lv_crc32c_last_kernel().decode()
+
+
+def device_counters(device: int = 0) -> dict:
+    """What the host entry points have copied / allocated on `device` so far
+    (lv_device_counters): {"h2d": bytes, "d2h": bytes, "allocs": count}."""
+    v = (ctypes.c_uint64 * 3)()
+    _check(lib().lv_device_counters(device, ctypes.cast(v, ctypes.c_void_p), 3))
+    return {"h2d": int(v[0]), "d2h": int(v[1]), "allocs": int(v[2])}

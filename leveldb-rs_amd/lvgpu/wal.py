@@ -122,8 +122,12 @@ def scan_device(log, cap: int, workspace=None, stream=None):
     CUDA tensors, asynchronous on `stream`.  count[0] > cap means the capacity
     was too small and nothing else was written."""
     import torch
-    from . import _dev_ptr, _stream_ptr
+    from . import LvError, _dev_ptr, _stream_ptr
     L = _bind()
+    if log.dtype != torch.uint8:
+        raise LvError(f"log must be a uint8 tensor (got {log.dtype}: numel() would not count bytes)")
+    if workspace is not None and (workspace.dtype != torch.uint8 or workspace.device != log.device):
+        raise LvError("workspace must be a uint8 tensor on the log's device")
     dev = log.device
     hdr = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
     crc = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
@@ -132,9 +136,10 @@ def scan_device(log, cap: int, workspace=None, stream=None):
     need = L.lv_wal_scan_workspace_bytes(log.numel(), cap)
     if workspace is None:
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
-    rc = L.lv_wal_scan_device(_dev_ptr(log, "log"), log.numel(), _dev_ptr(hdr, "hdr"), _dev_ptr(crc, "crc"),
-                              _dev_ptr(info, "info"), cap, _dev_ptr(count, "count"), _dev_ptr(workspace, "workspace"),
-                              workspace.numel(), _stream_ptr(stream))
+    with torch.cuda.device(dev):  # the C call runs on the current device
+        rc = L.lv_wal_scan_device(_dev_ptr(log, "log"), log.numel(), _dev_ptr(hdr, "hdr"), _dev_ptr(crc, "crc"),
+                                  _dev_ptr(info, "info"), cap, _dev_ptr(count, "count"),
+                                  _dev_ptr(workspace, "workspace"), workspace.numel(), _stream_ptr(stream))
     if rc != 0:
         _err("lv_wal_scan_device")
     return hdr, crc, info, count

@@ -305,6 +305,39 @@ def test_batch_multi_devices(gpu):
         lvgpu.batch_multi(arena, offs, lens, seeds, ngpu=torch.cuda.device_count() + 1)
 
 
+def test_batch_multi_ships_each_device_its_buffers(gpu):
+    """A shuffled gather over a 96 MiB arena: every device range spans ~the
+    whole arena, so the range's buffers are packed and each device receives
+    its payload share plus metadata -- not the arena.
+    Byte-packed buffers in index order ship their span as is.  CRCs equal
+    the oracle either way."""
+    import numpy as np
+    rng = np.random.default_rng(123)
+    n = 4000
+    lens = rng.integers(0, 4000, size=n).astype(np.uint32)
+    arena_n = 96 << 20
+    arena = rng.integers(0, 256, size=arena_n, dtype=np.uint8)
+    offs = rng.integers(0, arena_n - lens.astype(np.int64), dtype=np.int64).astype(np.uint64)
+    payload = int(lens.sum(dtype=np.uint64))
+    want = np.zeros(n, dtype=np.uint32)
+    W.lib().oracle_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, want.ctypes.data, n, 0)
+    for devs in ([0], [0, 0, 0, 0]):
+        before = lvgpu.device_counters(0)
+        got = lvgpu.batch_multi(arena, offs, lens, None, devices=devs)
+        moved = lvgpu.device_counters(0)["h2d"] - before["h2d"]
+        assert np.array_equal(got, want), devs
+        assert moved <= payload + 16 * n, (devs, moved, payload)
+    # in index order and byte-packed: one span per range, no pack needed
+    packed_offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    want2 = np.zeros(n, dtype=np.uint32)
+    W.lib().oracle_batch(arena.ctypes.data, packed_offs.ctypes.data, lens.ctypes.data, None, want2.ctypes.data, n, 0)
+    before = lvgpu.device_counters(0)
+    got = lvgpu.batch_multi(arena, packed_offs, lens, None, devices=[0, 0, 0])
+    moved = lvgpu.device_counters(0)["h2d"] - before["h2d"]
+    assert np.array_equal(got, want2)
+    assert moved <= payload + 16 * n
+
+
 def test_sorted_walk_edges(torch_dev, arena):
     """Offsets API edge geometry for the wave-uniform walk: lengths at the
     class edges (256/257, 2048/2049, 32768/32769) and at batch-count edges of
@@ -637,3 +670,29 @@ def test_offsets_api_small_batches_random(torch_dev, trial):
     want = oracle_batch(arena.cpu().numpy().tobytes(), offs, lens, seeds, masked)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("n,L,distinct", [(300, 1 << 30, 5), (2000, 256 << 20, 7), (40000, (8 << 20) + 1, 3)])
+def test_offsets_api_huge_batch_piece_budget(torch_dev, n, L, distinct):
+    """Batches of 300-500 GiB of heavily overlapping buffers: the
+    piece length P must stay >= batch bytes / 16,384 however large the batch,
+    or the split overruns the piece budget (300 x 1 GiB: 256 pieces each,
+    76,800 > 65,536) or the long-record budget (40,000 x 8 MiB: 32,768
+    records).  The buffers repeat `distinct` (offset, length) pairs, so the
+    oracle runs once per pair; every output is checked."""
+    torch, dev = torch_dev
+    arena = torch.empty(L + 4096, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, 0xB16B + n)
+    k = np.arange(n) % distinct
+    offs = (k * 517 + 3).astype(np.int64)
+    lens = (L - k * 1031).astype(np.int64)
+    assert int((offs + lens).max()) <= arena.numel()
+    o = torch.from_numpy(offs).to(dev)
+    ln = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    out = lvgpu.batch(arena, o, ln, None, masked=True)
+    got = out.cpu().numpy().view(np.uint32)
+    host = arena.cpu().numpy().tobytes()
+    want_pair = oracle_batch(host, offs[:distinct], lens[:distinct], None, True)
+    want = want_pair[k]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad.size, bad[:10])

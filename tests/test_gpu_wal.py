@@ -193,3 +193,20 @@ def test_scan_device_capacity(gpu):
     n = len(W.scan_log(tiny)[0])
     for cap in (n - 1, n, n + 1, 2 * n):
         _check_scan_device(tiny, cap=cap)
+
+
+def test_scan_device_rejects_non_byte_views(gpu):
+    """A log passed as an int32/int64 view would scan numel() < bytes; a
+    workspace on another dtype is rejected too."""
+    import torch
+
+    import lvgpu
+    import lvgpu.wal as LW
+    log = _oracle_encode([b"abc" * 100, b"x" * 5000])
+    pad = bytes(-len(log) % 8)
+    d = torch.frombuffer(bytearray(log + pad), dtype=torch.uint8).to(gpu)
+    for view in (d.view(torch.int32), d.view(torch.int64)):
+        with pytest.raises(lvgpu.LvError):
+            LW.scan_device(view, 16)
+    with pytest.raises(lvgpu.LvError):
+        LW.scan_device(d, 16, workspace=torch.empty(1 << 20, dtype=torch.int32, device=gpu))

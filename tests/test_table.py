@@ -150,6 +150,12 @@ def test_gpu_verify_detects_corruption_and_range(gpu):
     got = LT.verify_blocks(d, h).cpu().numpy().tolist()
     assert got == want
     assert LT.verify_blocks_host(bytes(sealed), np.array(allh, dtype=np.uint64)).tolist() == want
+    # the host path reuses the device's cached arena and scratch: a second
+    # call of the same size allocates nothing
+    import lvgpu
+    before = lvgpu.device_counters(0)["allocs"]
+    assert LT.verify_blocks_host(bytes(sealed), np.array(allh, dtype=np.uint64)).tolist() == want
+    assert lvgpu.device_counters(0)["allocs"] == before
 
 
 @pytest.mark.gpu
