@@ -45,6 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "leveldb-rs_amd"))
 METRIC = "GiB/s device-resident batched CRC32C, 4KiB blocks; %HBM-peak at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md), GB/s
 PAYLOAD_SEED = 0x4C444231
+SETTLE = True  # --no-settle clears it (the event-timed diagnostics honour it too)
 
 
 def parse():
@@ -407,7 +408,8 @@ def c1_sweep(args):
 def _event_times(torch, fn, steps, warmup):
     """Median and mean ms of `fn` by HIP events on the current stream, after
     the settle phase (see settle()) and `warmup` calls."""
-    settle(torch, fn, torch.cuda.current_stream())
+    if SETTLE:
+        settle(torch, fn, torch.cuda.current_stream())
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -912,7 +914,9 @@ def global_lengths(name):
 
 
 def main():
+    global SETTLE
     args = parse()
+    SETTLE = args.settle
     single = [m for m in ("wal", "c1", "e2e", "sweep", "table", "hash", "long", "wal_device") if getattr(args, m)]
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")

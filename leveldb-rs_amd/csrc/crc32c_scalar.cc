@@ -1,7 +1,7 @@
 // Host scalar drop-ins for the reference's crc32c module (src/util/crc32c.rs).
 // These serve single-record callers (the WAL writer emits one record at a
 // time, log_writer.rs:112-134) where a kernel launch would cost 100x the
-// checksum.  The GPU batch path (crc32c_batch.hip) never calls into here.
+// checksum.  The GPU batch path (blocks.hip, classes.hip, ...) never calls into here.
 #include <nmmintrin.h>
 
 #include <cstring>

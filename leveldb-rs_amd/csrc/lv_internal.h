@@ -13,14 +13,14 @@ struct lv_wal_scan {
 #include <mutex>
 
 namespace lvgpu_internal {
-int set_error(int code, const char *msg);  // lv_last_error plumbing (crc32c_batch.hip)
+int set_error(int code, const char *msg);  // lv_last_error plumbing (context.hip)
 void clear_error();
 int launch_status();                       // hipGetLastError -> LV status + message
 
 // Selects a device for the calling thread and restores the thread's previous
 // current device when it goes out of scope: the host entry points take a
 // `device` argument, and a drop-in C ABI must not leave the caller's thread
-// pointed at another GPU (crc32c_batch.hip).
+// pointed at another GPU (context.hip).
 struct DeviceGuard {
     int prev = -1;
     DeviceGuard() = default;
@@ -30,7 +30,7 @@ struct DeviceGuard {
     ~DeviceGuard();
 };
 
-// Host-memory path of one device (crc32c_batch.hip): holds the device's
+// Host-memory path of one device (context.hip): holds the device's
 // host-path lock while alive.  host_upload copies `bytes` of host memory into
 // the device's cached arena (pinned input: one DMA; pageable: a pipelined
 // pinned staging copy) followed by `pad` zero bytes, on the device's stream.
@@ -42,13 +42,13 @@ struct HostPath {
 };
 int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath *hp);
 // SSTable trailer seal (d_types may be NULL) or verify (d_status, optional
-// d_crc) of n blocks in one launch on the current device (crc32c_batch.hip).
+// d_crc) of n blocks in one launch on the current device (sst.hip).
 int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, const uint64_t *d_handles,
                       const uint8_t *d_types, size_t n, uint32_t *d_status, uint32_t *d_crc, void *stream);
 // Cached device scratch buffer `slot` (0..1) of the HostPath's device, >= bytes.
 int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d);
 // lv_device_counters bookkeeping for host copies made outside
-// crc32c_batch.hip (current device).
+// context.hip (current device).
 void count_h2d(uint64_t bytes);
 void count_d2h(uint64_t bytes);
 }

@@ -1,0 +1,132 @@
+// Kernel tuning switches (LVK_*) of the product library.
+//
+// The defaults below ARE the product: each switch records a measured
+// alternative (documented where it is used), and the GPU suite tests the
+// kernels only at these values.  Setting any of them is therefore an error
+// unless the build declares itself an experiment variant: tools/build_variant.sh
+// defines LVK_EXPERIMENT_BUILD and writes the library to lib/variants/, which
+// never ships to the GPU box and which the Python binding loads only with
+// LVGPU_EXPERIMENT=1.  tests/test_abi.py checks that every switch is listed
+// in the guard.
+#pragma once
+
+#if !defined(LVK_EXPERIMENT_BUILD) && ( \
+    defined(LVK_XOR3) || \
+    defined(LVK_EXP_NOSHIFT) || \
+    defined(LVK_EXP_NOFOLD) || \
+    defined(LVK_STAGGER) || \
+    defined(LVK_EXP_NOSTAGE) || \
+    defined(LVK_EXP_NOTAIL) || \
+    defined(LVK_EXP_NOFIX) || \
+    defined(LVK_EXP_NOMERGE) || \
+    defined(LVK_EXP_NOSEALWRITE) || \
+    defined(LVK_FUSE_INFLIGHT) || \
+    defined(LVK_AL_ROWS) || \
+    defined(LVK_ALIGNED_ROWS) || \
+    defined(LVK_IDENT) || \
+    defined(LVK_MAX_PIECES) || \
+    defined(LVK_SMALL_SORT) || \
+    defined(LVK_WAL_TOUCH_HOPS) || \
+    defined(LVK_PERMLANE) || \
+    defined(LVK_AL_RT_LAST) || \
+    defined(LVK_ZERO_PAGE) || \
+    defined(LVK_SKIP_PAD) || \
+    defined(LVK_SMALL_WAVES) || \
+    defined(LVK_SMALL_ALL) || \
+    defined(LVK_CLASS_STAGGER) || \
+    defined(LVK_SEAL_FLUSH) || \
+    defined(LVK_SST_ROWS) || \
+    defined(LVK_LONG_TABS) || \
+    defined(LVK_LONG_LDSP) || \
+    defined(LVK_SORT_MIN_WGS) || \
+    defined(LVK_VERIFY_WIDE))
+#error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
+#endif
+
+#ifndef LVK_XOR3
+#define LVK_XOR3 1
+#endif
+#ifndef LVK_EXP_NOSHIFT
+#define LVK_EXP_NOSHIFT 0
+#endif
+#ifndef LVK_EXP_NOFOLD
+#define LVK_EXP_NOFOLD 0
+#endif
+#ifndef LVK_STAGGER  // s_sleep(32) units between the start of successive waves (blocks kernel, >= 8 KiB)
+#define LVK_STAGGER 1u
+#endif
+#ifndef LVK_EXP_NOSTAGE
+#define LVK_EXP_NOSTAGE 0
+#endif
+#ifndef LVK_EXP_NOTAIL
+#define LVK_EXP_NOTAIL 0
+#endif
+#ifndef LVK_EXP_NOFIX
+#define LVK_EXP_NOFIX 0
+#endif
+#ifndef LVK_EXP_NOMERGE
+#define LVK_EXP_NOMERGE 0
+#endif
+#ifndef LVK_EXP_NOSEALWRITE  // the seal computes its trailers but stores none
+#define LVK_EXP_NOSEALWRITE 0
+#endif
+#ifndef LVK_FUSE_INFLIGHT
+#define LVK_FUSE_INFLIGHT 1
+#endif
+#ifndef LVK_AL_ROWS
+#define LVK_AL_ROWS 4
+#endif
+#ifndef LVK_ALIGNED_ROWS
+#define LVK_ALIGNED_ROWS 1
+#endif
+#ifndef LVK_IDENT
+#define LVK_IDENT 1
+#endif
+#ifndef LVK_MAX_PIECES  // pieces per split buffer (a lone 16 MiB buffer: 4,096 of 4 KiB, as the strided API cuts it)
+#define LVK_MAX_PIECES 4096
+#endif
+#ifndef LVK_SMALL_SORT
+#define LVK_SMALL_SORT 1
+#endif
+#ifndef LVK_WAL_TOUCH_HOPS
+#define LVK_WAL_TOUCH_HOPS 16
+#endif
+#ifndef LVK_PERMLANE
+#define LVK_PERMLANE 1
+#endif
+#ifndef LVK_AL_RT_LAST
+#define LVK_AL_RT_LAST 0
+#endif
+#ifndef LVK_ZERO_PAGE
+#define LVK_ZERO_PAGE 1
+#endif
+#ifndef LVK_SKIP_PAD
+#define LVK_SKIP_PAD 1
+#endif
+#ifndef LVK_SMALL_WAVES
+#define LVK_SMALL_WAVES 4
+#endif
+#ifndef LVK_SMALL_ALL
+#define LVK_SMALL_ALL 1
+#endif
+#ifndef LVK_CLASS_STAGGER
+#define LVK_CLASS_STAGGER 1
+#endif
+#ifndef LVK_SEAL_FLUSH  // rounds per seal flush (<= 16: 64 two-word slots)
+#define LVK_SEAL_FLUSH 16
+#endif
+#ifndef LVK_SST_ROWS
+#define LVK_SST_ROWS 3
+#endif
+#ifndef LVK_LONG_TABS
+#define LVK_LONG_TABS 1
+#endif
+#ifndef LVK_LONG_LDSP  // Shift_P staged per wave for the Horner steps (d >= 2)
+#define LVK_LONG_LDSP 1
+#endif
+#ifndef LVK_SORT_MIN_WGS
+#define LVK_SORT_MIN_WGS 1024
+#endif
+#ifndef LVK_VERIFY_WIDE  // experiment: the four-word verify staging even without crc_out
+#define LVK_VERIFY_WIDE 0
+#endif

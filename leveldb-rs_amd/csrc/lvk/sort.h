@@ -1,0 +1,103 @@
+// Length sort of the offsets API: keys, workspace layout and the wave-level
+// counting helpers shared by the sort passes (sort.hip), the WAL framing
+// (wal_scan.hip) and the walks (lvk/walk.h).
+#pragma once
+#include "core.h"
+
+namespace lvk {
+
+// Length classes of the offsets API.  Buffers are counting-sorted by key =
+// (class, batches descending): each class runs with the group size that keeps
+// ~1-32 batches per buffer, and consecutive list entries -- the groups of one
+// wave -- have the same batch count, so they finish buffers in lockstep.
+constexpr uint32_t kBuckets = 64;                 // batch-count buckets per class
+constexpr uint32_t kKeys = 4 * kBuckets;
+constexpr uint32_t kSortThreads = 256;
+constexpr uint32_t kSortE = 16;  // elements per thread per register block in the sort passes
+
+__device__ __forceinline__ uint32_t len_class(uint32_t len) {
+    return len <= 256u ? 0u : len <= 2048u ? 1u : len <= 32768u ? 2u : 3u;
+}
+
+// Rows per batch of the G = 16 classes' aligned-row walk (sorted_stream).
+constexpr uint32_t kAlRows = LVK_ALIGNED_ROWS ? LVK_AL_ROWS : U;
+
+__device__ __forceinline__ uint32_t sort_key(uint32_t len) {
+    const uint32_t c = len_class(len);
+    const uint32_t gu16 = 16u * (c >= 2 ? kAlRows : U) * (c == 0 ? 1u : c == 1 ? 4u : 16u);
+    uint32_t nb = (len + gu16 - 1) / gu16;  // batches, ignoring start alignment
+    nb = nb < kBuckets - 1 ? nb : kBuckets - 1;
+    return c * kBuckets + (kBuckets - 1 - nb);
+}
+
+// Sort workspace, 16-B aligned.  Header (u32 words): [0, 4) the long-buffer
+// split's piece and long-buffer counters and the batch's payload bytes (u64);
+// [4, 256) unused; [256, 264) class start x4, count x4; [264, 520) per-key
+// totals; [520, 528) unused.  Then the per-workgroup histogram matrix
+// M[wgs][256], the per-workgroup payload sums (u64), n + kPieceBudget sorted
+// 16-B entries (the pieces of split long buffers follow the n sorted ones),
+// as many seeds in entry order, kPieceBudget piece registers and
+// kPieceBudget / 2 long-buffer records {buffer, first piece, pieces, log2 piece}.
+constexpr uint32_t kWsPieces = 0;
+constexpr uint32_t kWsLongs = 1;
+constexpr uint32_t kWsBytes = 2;
+constexpr uint32_t kWsIdent = 4;  // 1: the sorted list is the identity (one key, no split): see sort_scatter
+constexpr uint32_t kPieceBudget = 65536;  // piece entries per call (each split buffer takes <= kMaxPieces)
+constexpr uint32_t kMaxPieces = LVK_MAX_PIECES;
+constexpr uint32_t kPieceFlag = 0x80000000u;  // output slot flag of a piece entry (slot < kPieceBudget)
+constexpr uint32_t kWsCls = kKeys;
+constexpr uint32_t kWsTot = kKeys + 8;
+constexpr uint32_t kWsHeader = kWsTot + kKeys + 8;  // 528 words, 16-B multiple
+constexpr uint32_t kSortChunk = kSortThreads * kSortE;  // elements per sorting workgroup (n <= 4M)
+constexpr uint32_t kSortMaxWgs = 1024;
+constexpr uint32_t kScanWgs = kKeys / 16;  // 16 keys per scan workgroup
+constexpr uint32_t kScanThreads = 1024;    // 16 keys x 64 row ranges
+static_assert(kSortMaxWgs <= 64 * 16, "scan: 64 row ranges of <= 16 rows");
+
+// h[k] += 1 for each valid lane's key k.  A wave whose valid lanes share one
+// key (a uniform batch: thousands of same-address LDS atomics would
+// serialize) adds its count with one atomic; otherwise each lane adds its own.
+__device__ __forceinline__ void wave_count(uint32_t *h, uint32_t k, bool valid, uint32_t lane) {
+    const uint64_t act = __ballot(valid);
+    if (!act) return;  // wave-uniform
+    const int leader = __ffsll(static_cast<long long>(act)) - 1;
+    const uint32_t kl = __shfl(k, leader);
+    if (__ballot(valid && k != kl) == 0) {
+        if (static_cast<int>(lane) == leader) atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(act)));
+    } else if (valid) {
+        atomicAdd(&h[k], 1u);
+    }
+}
+
+// Like wave_count, but returns each valid lane's claimed slot h[k]++.
+__device__ __forceinline__ uint32_t wave_claim(uint32_t *h, uint32_t k, bool valid, uint32_t lane) {
+    const uint64_t act = __ballot(valid);
+    if (!act) return 0;  // wave-uniform
+    const int leader = __ffsll(static_cast<long long>(act)) - 1;
+    const uint32_t kl = __shfl(k, leader);
+    if (__ballot(valid && k != kl) == 0) {
+        uint32_t base = 0;
+        if (static_cast<int>(lane) == leader) base = atomicAdd(&h[kl], static_cast<uint32_t>(__popcll(act)));
+        base = __shfl(base, leader);
+        return base + static_cast<uint32_t>(__popcll(act & ((1ull << lane) - 1ull)));
+    }
+    return valid ? atomicAdd(&h[k], 1u) : 0u;
+}
+
+// Exclusive scan of the 256 key totals (one per thread of a 256-thread
+// workgroup) into sc[]; returns this thread's key start.
+__device__ __forceinline__ uint32_t key_starts(const uint32_t *ws, uint32_t *sc) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t mine = ws[kWsTot + t];
+    sc[t] = mine;
+    __syncthreads();
+    for (uint32_t d = 1; d < kKeys; d <<= 1) {
+        const uint32_t x = t >= d ? sc[t - d] : 0u;
+        __syncthreads();
+        sc[t] += x;
+        __syncthreads();
+    }
+    return sc[t] - mine;
+}
+
+}  // namespace lvk

@@ -1,9 +1,8 @@
 // SSTable block trailers on MI355X: seal (builder side)
 // and verify (ReadOptions::verify_checksums, options.rs:84) of many blocks
 // at once.  Each block's CRC unit is contents||type, contiguous in the file;
-// the kernel (one launch: handles -> CRC -> trailer epilogue) lives with the
-// other CRC kernels in crc32c_batch.hip.  Trailer layout: see
-// include/lvgpu/table.h.
+// one kernel launch (handles -> CRC walk of lvk/walk.h -> trailer epilogue).
+// Trailer layout: see include/lvgpu/table.h.
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -11,6 +10,169 @@
 #include "../../include/lvgpu/crc32c.h"
 #include "../../include/lvgpu/table.h"
 #include "lv_internal.h"
+#include "lvh.h"
+#include "lvk/walk.h"
+
+namespace lvk {
+
+// ---------------------------------------------------------------------------
+// SSTable block trailers in ONE launch (include/lvgpu/table.h).
+// The table's blocks are walked in file order, four per wave round, by the
+// G = 16 aligned-row walk: blocks of one table have similar sizes (block_size
+// plus at most one entry), so consecutive blocks give a near-uniform round
+// with no length sort.  The handles (BlockHandle extents, table/format.rs:
+// 29-50) are read directly, and the trailer work is the epilogue:
+//  * verify: unit = contents || type (size + 1 bytes); the stored LE32 after
+//    it is loaded with the tail and compared after unmask;
+//  * seal: unit = contents; the type byte enters the register by one table
+//    step, R(s, D || t) = T0-step(R(s, D), t), so no byte is written before
+//    it is read, and type + LE32(mask(crc)) are written in the flush.
+// (Round 1 ran units -> 3 sort passes -> class kernel -> trailer kernel.)
+__device__ __forceinline__ bool sst_in_range(uint64_t o, uint64_t sz, uint64_t file_bytes) {
+    return sz < 0xffffffffull && o <= file_bytes && sz <= file_bytes - o && file_bytes - o - sz >= 5u;
+}
+
+template <bool SEAL, bool CRCOUT = false>
+struct TableUnits {
+    const uint2 *handles;  // {offset, size} u64 pairs per block
+    const uint8_t *types;  // seal: per-block type byte (NULL: 0 = no compression)
+    uint32_t *status;      // verify: LV_SST_BLOCK_* per block
+    uint32_t *crc_out;     // verify: optional crc32c(contents || type)
+    uint64_t file_bytes;
+    // seal: 64 slots of {block, masked crc} (16 rounds of 4 blocks per flush;
+    // the trailer stores are partial-line writes, and fewer, larger bursts of
+    // them measured faster); verify: 64 slots of {block, status}, or with
+    // crc_out 32 slots of four words
+    static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
+
+    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
+        const bool valid = e < P.n;
+        const uint64_t ec = valid ? e : P.n - 1;
+        const uint2 ho = handles[2 * ec], hs = handles[2 * ec + 1];  // u64 pairs: 8-B alignment is enough
+        const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
+        const bool ok = sst_in_range(o, sz, file_bytes);
+        RGeo q;
+        q.len = ok ? static_cast<uint32_t>(SEAL ? sz : sz + 1) : 0u;
+        // in range: the block's own offset even when empty (its trailer goes
+        // there; its loads stay inside the file); otherwise the file start
+        q.a = ok ? P.base + o : P.base;
+        q.seed = 0;
+        q.bid = valid ? static_cast<uint32_t>(ec) : 0xffffffffu;
+        uint32_t t = 0;
+        if (SEAL && types && ok) t = types[ec];
+        q.aux = (ok ? 1u : 0u) | (t << 8);
+        return q;
+    }
+    // verify: the stored masked crc at the unit's end (two aligned dwords)
+    __device__ __forceinline__ uint2 trailer(const RGeo &q, uint32_t gl) const {
+        if (SEAL || gl != 0 || !(q.aux & 1u)) return make_uint2(0, 0);
+        const uint64_t end = q.a + q.len;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(end & ~static_cast<uint64_t>(3));
+        return make_uint2(w[0], (end & 3u) ? w[1] : 0u);
+    }
+    __device__ __forceinline__ void stage(const Params &, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
+                                          uint2 tr) const {
+        const bool ok = q.aux & 1u;
+        if constexpr (SEAL) {
+            const uint32_t t = (q.aux >> 8) & 0xffu;
+            const uint32_t crc = ~byte_step(X, t);
+            g_oidx[wave][slot] = ok ? q.bid : 0xffffffffu;  // the flush re-reads the handle and type
+            g_ocrc[wave][slot] = mask_crc(crc);
+        } else {
+            const uint32_t crc = ~X;
+            const uint32_t k = static_cast<uint32_t>(q.a + q.len) & 3u;
+            const uint32_t stored = k ? (tr.x >> (8 * k)) | (tr.y << (32 - 8 * k)) : tr.x;
+            const uint32_t r = stored - 0xa282ead8u;  // unmask, crc32c.rs:59-63
+            const uint32_t st = !ok ? LV_SST_BLOCK_OUT_OF_RANGE
+                                    : (((r >> 17) | (r << 15)) == crc ? LV_SST_BLOCK_OK : LV_SST_BLOCK_CHECKSUM_MISMATCH);
+            g_oidx[wave][slot] = q.bid;
+            g_ocrc[wave][slot] = st;
+            if (CRCOUT) g_ocrc[wave][32 + slot] = ok ? crc : 0u;
+        }
+    }
+    __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
+        if constexpr (SEAL) {
+            if (lane >= nslots) return;
+            const uint32_t bi = g_oidx[wave][lane];
+            if (bi == 0xffffffffu || LVK_EXP_NOSEALWRITE) return;
+            const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
+            const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
+            uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
+            const uint32_t f = types ? types[bi] : 0u;
+            const uint32_t m = g_ocrc[wave][lane];
+            p[0] = static_cast<uint8_t>(f);
+            p[1] = static_cast<uint8_t>(m);
+            p[2] = static_cast<uint8_t>(m >> 8);
+            p[3] = static_cast<uint8_t>(m >> 16);
+            p[4] = static_cast<uint8_t>(m >> 24);
+        } else if constexpr (!CRCOUT) {
+            if (lane >= nslots) return;
+            const uint32_t bi = g_oidx[wave][lane];
+            if (bi != 0xffffffffu) status[bi] = g_ocrc[wave][lane];
+        } else {
+            const uint32_t sl = lane & 31u;
+            if (sl >= nslots) return;
+            const uint32_t bi = g_oidx[wave][sl];
+            if (bi == 0xffffffffu) return;
+            if (lane < 32)
+                status[bi] = g_ocrc[wave][sl];
+            else if (crc_out)
+                crc_out[bi] = g_ocrc[wave][32 + sl];
+        }
+    }
+};
+
+
+template <bool SEAL, bool CRCOUT>
+__global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
+                                                              TableUnits<SEAL, CRCOUT> src) {
+    stage_tables(image);
+    if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const Lut L = make_lut(lane);
+    const uint64_t grid = gridDim.x;
+    auto pool = [&]() -> uint64_t {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
+        return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+    };
+    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
+}
+
+}  // namespace lvk
+
+namespace lvgpu_internal {
+using namespace lvh;
+// SSTable trailers (csrc/sst.hip): one sst_blocks_kernel launch.
+int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, const uint64_t *d_handles,
+                      const uint8_t *d_types, size_t n, uint32_t *d_status, uint32_t *d_crc, void *stream) {
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    lvk::Params P{};
+    P.base = reinterpret_cast<uint64_t>(d_file);
+    P.n = n;
+    P.flags = 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (n + 3) / 4))), block(lvk::kThreads);
+    if (seal) {
+        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
+        g_kernel = "sst_blocks_kernel<seal>";
+        hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P, c->image[kTableImage], u);
+    } else if (d_crc || LVK_VERIFY_WIDE) {
+        lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
+        g_kernel = "sst_blocks_kernel<verify,crc>";
+        hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, true>), grid, block, 0, s, P, c->image[kTableImage], u);
+    } else {
+        lvk::TableUnits<false, false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, nullptr,
+                                        file_bytes};
+        g_kernel = "sst_blocks_kernel<verify>";
+        hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, false>), grid, block, 0, s, P, c->image[kTableImage], u);
+    }
+    return check_launch();
+}
+
+}  // namespace lvgpu_internal
 
 namespace lvs {
 
@@ -26,7 +188,7 @@ int check_args(const void *file, const uint64_t *handles, size_t n) {
 extern "C" {
 
 // Both device entry points are ONE kernel launch (lvk::sst_blocks_kernel,
-// crc32c_batch.hip): the handles are read in file order, the CRC walk is the
+// above): the handles are read in file order, the CRC walk is the
 // offsets API's G = 16 aligned-row walk, and the trailer compare / write is
 // its epilogue.
 int lv_sst_seal_blocks_device(uint8_t *d_file, uint64_t file_bytes, const uint64_t *d_handles,

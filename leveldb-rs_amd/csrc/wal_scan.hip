@@ -1,5 +1,5 @@
 // Host-memory WAL scan (the reader side of SURVEY 8f row 1): upload, then
-// the device scan lv_wal_scan_device (crc32c_batch.hip: each 32 KiB block's
+// the device scan lv_wal_scan_device (below: each 32 KiB block's
 // header chain is walked inside the length sort's passes, as
 // Reader::read_physical_record frames it, log_reader.rs:271-331, and every
 // [type || payload] unit is checksummed), then the arrays come back.
@@ -14,6 +14,377 @@
 #include "../../include/lvgpu/crc32c.h"
 #include "../../include/lvgpu/wal.h"
 #include "lv_internal.h"
+#include "lvh.h"
+#include "lvk/sort.h"
+
+namespace lvk {
+
+// ---------------------------------------------------------------------------
+// WAL scan with the framing fused into the sort passes (the
+// reader side, log_reader.rs:271-364).  Records never straddle a 32 KiB block
+// (log_writer.rs:67-80), so every block's header chain can be walked on its
+// own, exactly as read_physical_record frames it (log_reader.rs:271-331):
+// stop when fewer than HEADER_SIZE bytes remain, at a length that overruns
+// the block (BAD_LENGTH) or at a ZERO/0 header (ZERO).  wal_hist walks each
+// block (one thread per block) and counts the records' CRC units
+// [type || payload] (log_reader.rs:336) into the length-sort histogram, plus
+// the records per block, and keeps each block's first kHdrCache headers; sort_scan
+// is shared; wal_scatter takes those headers from the cache, one thread per
+// record (no dependent chain step), walks on only for blocks with more
+// records, and writes every record straight into its sorted slot, plus its
+// log-order header offset and info word.  The class kernel then checksums the
+// units.  Four launches, no host synchronisation (round 1: count pass, hipCUB
+// scan, host readback of the total, emit pass, then the whole offsets API).
+constexpr uint32_t kWalBlock = 32768;  // log_format.rs:63
+constexpr uint32_t kWalHeader = 7;     // log_format.rs:66
+constexpr uint32_t kHdrCache = 64;     // headers per block wal_hist keeps for wal_scatter
+
+// A cached header: position in its block | length << 16 | type << 32.
+__device__ __forceinline__ uint64_t hdr_pack(uint32_t pos, uint32_t len, uint32_t type) {
+    return pos | (static_cast<uint64_t>(len) << 16) | (static_cast<uint64_t>(type) << 32);
+}
+
+// The 8 bytes at log offset pos (bytes past the log read as 0): aligned
+// 8-B words, each read only if it holds a byte of the log (an aligned word
+// never crosses a page), and a funnel shift.  (A per-thread 64-B LDS window
+// of the log, which would keep several short records' headers per load,
+// measured slower: wal_hist 36.6 -> 41.6 us; so did a 64-B register window
+// parsed divergently, one load per record that leaves it: 38.9 -> 49.6 us;
+// and 32-B / 64-B register windows in the uniform one-header-per-step loop:
+// scan -1.5 / -2.8 %.
+// The chains that bound the walk are hops over longer records, one HBM
+// round trip each.)
+__device__ __forceinline__ uint64_t wal_load8(const uint8_t *log, uint64_t size, uint64_t pos) {
+    const uint64_t a = pos & ~7ull;
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(log + a);
+    const uint64_t lo = a < size ? w[0] : 0ull;
+    const uint32_t sh = static_cast<uint32_t>(pos & 7u) * 8u;
+    if (!sh) return lo;
+    const uint64_t hi = a + 8 < size ? w[1] : 0ull;
+    return (lo >> sh) | (hi << (64u - sh));
+}
+
+// One step of a block's header chain: the record at pos (status, unit
+// length); the next header is at pos + HEADER_SIZE + len.
+struct WalRec {
+    uint32_t len, type, status, ulen;
+};
+
+__device__ __forceinline__ WalRec wal_decode(uint64_t h, uint32_t blen, uint32_t pos) {  // crc(4) | length(2) | type(1)
+    WalRec r;
+    r.len = static_cast<uint32_t>(h >> 32) & 0xffffu;
+    r.type = static_cast<uint32_t>(h >> 48) & 0xffu;
+    r.status = LV_WAL_REC_OK;
+    if (kWalHeader + r.len > blen - pos)
+        r.status = LV_WAL_REC_BAD_LENGTH;  // log_reader.rs:312-324
+    else if (r.type == 0 && r.len == 0)
+        r.status = LV_WAL_REC_ZERO;        // log_reader.rs:326-331
+    r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
+    return r;
+}
+
+__device__ __forceinline__ WalRec wal_record(const uint8_t *log, uint64_t size, uint64_t start, uint32_t blen,
+                                             uint32_t pos) {
+    return wal_decode(wal_load8(log, size, start + pos), blen, pos);
+}
+
+// Long chains: after LVK_WAL_TOUCH_HOPS hops, the wave loads one dword of
+// every 128-B line of the rest of each block still being walked (a block with
+// that many records has short ones: its remaining headers are close
+// together), four blocks at a time (16 loads per lane in flight, one HBM round
+// trip per four blocks), so the remaining hops hit L2 (~200 cycles) instead
+// of HBM (~900).  In the bench log 5 % of the blocks hold > 16 records and the
+// longest chain is 54.
+__device__ __forceinline__ uint32_t wal_touch(const uint8_t *log, uint64_t b0, uint32_t pos, uint32_t blen,
+                                              bool active, uint32_t lane) {
+    uint64_t dm = __ballot(active);
+    uint32_t x = 0;
+    while (dm) {  // wave-uniform
+        uint32_t v[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int l0 = dm ? __ffsll(static_cast<long long>(dm)) - 1 : 0;
+            const bool on = dm != 0;
+            dm &= dm - 1;
+            const uint32_t p0 = __shfl(pos, l0), bl = on ? __shfl(blen, l0) : 0u;
+            const uint8_t *blk = log + (b0 + static_cast<uint64_t>(l0)) * kWalBlock;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t o = (p0 & ~127u) + 128u * (lane + 64u * k);
+                v[g][k] = o < bl ? *reinterpret_cast<const uint32_t *>(blk + o) : 0u;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) x ^= xor3(v[g][0], v[g][1], v[g][2]) ^ v[g][3];
+    }
+    return x;
+}
+
+__global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
+                                                         uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ M,
+                                                         uint64_t *__restrict__ wgrec, uint32_t *__restrict__ blkcnt,
+                                                         uint64_t *__restrict__ hcache) {
+    __shared__ uint32_t h[kKeys];
+    __shared__ uint64_t wsum[kSortThreads / 64];
+    __shared__ uint64_t hcl[kSortThreads * (kHdrCache + 1)];  // per-thread header cache (130 KiB)
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    h[t] = 0;
+    __syncthreads();
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
+    uint64_t mine = 0;
+    uint32_t touched = 0;
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
+        const uint64_t b = b0 + t;
+        const uint64_t start = b * kWalBlock;
+        const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
+        uint32_t pos = 0, cnt = 0, hops = 0;
+        bool active = blen >= kWalHeader;
+        // The header cache is filled in LDS and stored after the walk: a
+        // global store in the hop (vmcnt counts stores too, in order) made
+        // every hop's wait for its header load also wait for the previous
+        // hop's store.
+        uint64_t *const hl = hcl + t * (kHdrCache + 1);  // stride 65 words: lanes spread over the banks
+        while (__any(active)) {  // wave-uniform: the longest chain of the wave
+            if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
+                touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
+            uint32_t key = 0;
+            const bool rec = active;
+            if (active) {
+                const WalRec r = wal_record(log, size, start, blen, pos);
+                key = sort_key(r.ulen);
+                if (cnt < kHdrCache) hl[cnt] = hdr_pack(pos, r.len, r.type);
+                ++cnt;
+                pos += kWalHeader + r.len;
+                active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
+            }
+            wave_count(h, key, rec, lane);
+        }
+        for (uint32_t c = 0; c < cnt && c < kHdrCache; ++c) hcache[b * kHdrCache + c] = hl[c];
+        if (b < hi) blkcnt[b] = cnt;
+        mine += cnt;
+    }
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) mine += __shfl_xor(mine, k);
+    if (lane == 0) wsum[t >> 6] = mine;
+    asm volatile("" ::"v"(touched));  // the touches are kept
+    __syncthreads();
+    M[static_cast<uint64_t>(blockIdx.x) * kKeys + t] = h[t];
+    if (t == 0) wgrec[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // sort_scan sums these
+}
+
+// Output of the WAL scan, in log order (lv_wal_scan_device).
+struct WalOut {
+    uint64_t *hdr_off;
+    uint32_t *info;  // type | status << 8 | length << 16
+    uint64_t *count;
+    uint64_t cap;
+};
+
+__global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__restrict__ log, uint64_t size,
+                                                            uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ ws,
+                                                            const uint32_t *__restrict__ M,
+                                                            const uint64_t *__restrict__ wgrec,
+                                                            const uint32_t *__restrict__ blkcnt,
+                                                            const uint64_t *__restrict__ hcache, uint4 *__restrict__ ent,
+                                                            WalOut o) {
+    __shared__ uint32_t cur[kKeys];
+    __shared__ uint32_t sc[kKeys];
+    __shared__ uint64_t red[kSortThreads];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const uint64_t total = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];  // records
+    const bool over = total > o.cap;  // nothing is written past the capacity: the caller retries
+    const uint32_t mrow = M[static_cast<uint64_t>(blockIdx.x) * kKeys + t];
+    const uint32_t ks = key_starts(ws, sc);
+    cur[t] = ks + mrow;
+    if (blockIdx.x == 0 && t % kBuckets == 0) {  // per-class [start, count) for the CRC kernel
+        const uint32_t c = t / kBuckets;
+        ws[kWsCls + c] = over ? 0u : ks;
+        ws[kWsCls + 4 + c] = over ? 0u : sc[t + kBuckets - 1] - ks;
+    }
+    if (blockIdx.x == 0 && t == 0) {
+        *o.count = total;
+        ws[kWsIdent] = 0u;  // the class kernel reads the sorted entries
+    }
+    // this workgroup's first record in log order: the records of the ones before
+    uint64_t pre = 0;
+    for (uint32_t v = t; v < blockIdx.x; v += kSortThreads) pre += wgrec[v];
+    red[t] = pre;
+    __syncthreads();
+    for (uint32_t d = kSortThreads / 2; d >= 1; d >>= 1) {
+        if (t < d) red[t] += red[t + d];
+        __syncthreads();
+    }
+    uint64_t run = red[0];
+    __syncthreads();
+    if (over) return;  // block-uniform
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
+    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
+        const uint64_t b = b0 + t;
+        const uint32_t c = b < hi ? blkcnt[b] : 0u;
+        red[t] = c;  // inclusive scan of the block counts (Hillis-Steele in LDS)
+        __syncthreads();
+        for (uint32_t d = 1; d < kSortThreads; d <<= 1) {
+            const uint64_t x = t >= d ? red[t - d] : 0u;
+            __syncthreads();
+            red[t] += x;
+            __syncthreads();
+        }
+        const uint32_t tot = static_cast<uint32_t>(red[kSortThreads - 1]);  // records of these blocks
+        // The chunk's cached records, thread-parallel in log order: record q
+        // belongs to the block j whose inclusive prefix first exceeds q (a
+        // binary search over red), as its record k = q - excl(j).  (Round 2
+        // first ran one thread per block over its records: a wave then took
+        // as many claim-and-store steps as its longest block has records,
+        // ~30 us for the bench log.)
+        for (uint32_t q0 = 0; q0 < tot; q0 += kSortThreads) {  // block-uniform
+            const uint32_t q = q0 + t;
+            uint32_t j = 0;
+            for (uint32_t step = kSortThreads / 2; step >= 1; step >>= 1)
+                if (red[j + step - 1] <= q) j += step;
+            const uint32_t ex = j ? static_cast<uint32_t>(red[j - 1]) : 0u;
+            const uint32_t k = q - ex;
+            const bool rec = q < tot && k < kHdrCache;
+            const uint64_t bj = b0 + j;
+            const uint64_t start = bj * kWalBlock;
+            WalRec r{};
+            uint32_t pos = 0;
+            if (rec) {
+                const uint64_t h = hcache[bj * kHdrCache + k];
+                const uint32_t blen = static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock);
+                pos = static_cast<uint32_t>(h) & 0xffffu;
+                r.len = static_cast<uint32_t>(h >> 16) & 0xffffu;
+                r.type = static_cast<uint32_t>(h >> 32) & 0xffu;
+                r.status = kWalHeader + r.len > blen - pos ? LV_WAL_REC_BAD_LENGTH
+                                                           : (r.type == 0 && r.len == 0 ? LV_WAL_REC_ZERO : LV_WAL_REC_OK);
+                r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
+            }
+            const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
+            if (rec) {
+                const uint64_t rid = run + q;  // log order: blocks in order, records in chain order
+                const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
+                ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
+                                       static_cast<uint32_t>(rid));
+                o.hdr_off[rid] = start + pos;
+                o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
+            }
+        }
+        // blocks with more records than the cache holds walk on from there
+        // (one thread per block; rare: a 32 KiB block holds > 64 records only
+        // when most of them are a few bytes long)
+        {
+            const uint64_t start = b * kWalBlock;
+            const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
+            bool active = c > kHdrCache;
+            uint32_t pos = 0;
+            uint64_t rid = run + static_cast<uint64_t>(red[t]) - c + kHdrCache;
+            if (active) {
+                const uint64_t h = hcache[b * kHdrCache + kHdrCache - 1];
+                pos = (static_cast<uint32_t>(h) & 0xffffu) + kWalHeader + (static_cast<uint32_t>(h >> 16) & 0xffffu);
+            }
+            while (__any(active)) {
+                WalRec r{};
+                const bool rec = active;
+                if (active) r = wal_record(log, size, start, blen, pos);
+                const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
+                if (rec) {
+                    const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
+                    ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
+                                           static_cast<uint32_t>(rid));
+                    o.hdr_off[rid] = start + pos;
+                    o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
+                    ++rid;
+                    pos += kWalHeader + r.len;
+                    active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
+                }
+            }
+        }
+        run += tot;
+        __syncthreads();  // red is rewritten by the next chunk
+    }
+}
+
+}  // namespace lvk
+
+using namespace lvh;
+
+extern "C" {
+
+// ---- WAL scan of a log in HBM (include/lvgpu/wal.h) ----
+static uint64_t wal_wgs(uint64_t nblocks, uint64_t *chunk) {
+    uint64_t wgs = (nblocks + lvk::kSortThreads - 1) / lvk::kSortThreads;
+    wgs = std::max<uint64_t>(1, std::min<uint64_t>(wgs, lvk::kSortMaxWgs));
+    *chunk = (nblocks + wgs - 1) / wgs;
+    return wgs;
+}
+
+struct WalWs {
+    size_t m, wgrec, blk, hc, ent, total;
+};
+
+static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
+    const uint64_t nblocks = (bytes + lvk::kWalBlock - 1) / lvk::kWalBlock;
+    uint64_t chunk = 0;
+    const uint64_t wgs = wal_wgs(nblocks, &chunk);
+    WalWs w;
+    w.m = lvk::kWsHeader * sizeof(uint32_t);
+    w.wgrec = w.m + al16(wgs * lvk::kKeys * sizeof(uint32_t));
+    w.blk = w.wgrec + al16(wgs * sizeof(uint64_t));
+    w.hc = w.blk + al16(nblocks * sizeof(uint32_t));
+    w.ent = w.hc + nblocks * lvk::kHdrCache * sizeof(uint64_t);
+    w.total = w.ent + cap * sizeof(uint4);
+    return w;
+}
+
+size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) { return wal_ws_layout(bytes, cap).total; }
+
+int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
+                       size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream) {
+    g_err.clear();
+    if (!d_count) return set_err(LV_ERR_INVALID, "null count pointer");
+    if ((!d_log && bytes) || (cap && (!d_hdr_off || !d_crc || !d_info)) || !d_workspace)
+        return set_err(LV_ERR_INVALID, "null device pointer");
+    if (reinterpret_cast<uintptr_t>(d_log) % 8) return set_err(LV_ERR_INVALID, "log must be 8-byte aligned");
+    if (reinterpret_cast<uintptr_t>(d_workspace) % 16) return set_err(LV_ERR_INVALID, "workspace must be 16-byte aligned");
+    if (bytes / lvk::kWalHeader >= 0xffffffffull || cap > 0xffffffffull)
+        return set_err(LV_ERR_INVALID, "log too large for one scan");
+    const WalWs lay = wal_ws_layout(bytes, cap);
+    if (workspace_bytes < lay.total) return set_err(LV_ERR_INVALID, "workspace too small");
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t nblocks = (bytes + lvk::kWalBlock - 1) / lvk::kWalBlock;
+    if (nblocks == 0) {
+        LV_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), s));
+        return LV_OK;
+    }
+    uint8_t *wb = static_cast<uint8_t *>(d_workspace);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(wb);
+    uint32_t *M = reinterpret_cast<uint32_t *>(wb + lay.m);
+    uint64_t *wgrec = reinterpret_cast<uint64_t *>(wb + lay.wgrec);
+    uint32_t *blk = reinterpret_cast<uint32_t *>(wb + lay.blk);
+    uint64_t *hc = reinterpret_cast<uint64_t *>(wb + lay.hc);
+    uint4 *ent = reinterpret_cast<uint4 *>(wb + lay.ent);
+    uint64_t chunk = 0;
+    const uint64_t wgs = wal_wgs(nblocks, &chunk);
+    const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
+    hipLaunchKernelGGL(lvk::wal_hist, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk,
+                       hc);
+    launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgrec, s);
+    lvk::WalOut o{d_hdr_off, d_info, d_count, cap};
+    hipLaunchKernelGGL(lvk::wal_scatter, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws, M, wgrec,
+                       blk, hc, ent, o);
+    lvk::Params P{};
+    P.base = reinterpret_cast<uint64_t>(d_log);
+    P.out = d_crc;
+    P.n = cap;
+    P.nplain = cap;
+    P.ent = ent;
+    launch_classes(*c, false, P, ws, s);
+    g_kernel = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel";
+    return check_launch();
+}
+
+}  // extern "C"
 
 namespace {
 

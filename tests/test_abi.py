@@ -124,3 +124,46 @@ def test_workspace_bytes_cover_pieces():
     small, big = lvgpu.workspace_bytes(1), lvgpu.workspace_bytes(1 << 20)
     assert small >= 65536 * 16  # the piece entries alone
     assert big - small >= ((1 << 20) - 1) * 20  # 16-B entry + 4-B seed per buffer
+
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "leveldb-rs_amd", "csrc")
+
+
+def _knobs():
+    import re
+    with open(os.path.join(CSRC, "lvk", "knobs.h")) as f:
+        text = f.read()
+    guard = text[text.index("#if !defined(LVK_EXPERIMENT_BUILD)"):text.index("#error")]
+    return set(re.findall(r"#ifndef (LVK_\w+)", text)), set(re.findall(r"defined\((LVK_\w+)\)", guard))
+
+
+def test_every_kernel_switch_is_guarded():
+    """Every LVK_* switch the kernels read has its default in lvk/knobs.h and
+    is refused there outside experiment builds (no product-path
+    macro untested at a non-default value)."""
+    import glob
+    import re
+    defaults, guarded = _knobs()
+    guarded.discard("LVK_EXPERIMENT_BUILD")
+    assert defaults and defaults == guarded
+    used = set()
+    for path in glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) + \
+            glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cc")):
+        with open(path) as f:
+            used |= set(re.findall(r"\bLVK_[A-Z0-9_]+\b", f.read()))
+    used -= {"LVK_EXPERIMENT_BUILD", "LVK_EXP_"}  # "LVK_EXP_*" in comments
+    assert used <= defaults, sorted(used - defaults)
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+def test_product_build_refuses_kernel_switches():
+    """A product build with a non-default switch stops at lvk/knobs.h; the
+    same define in an experiment build passes the guard."""
+    import subprocess
+    src = os.path.join(CSRC, "sort.hip")
+    base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-E", "-o", os.devnull, src]
+    bad = subprocess.run(base + ["-DLVK_IDENT=0"], capture_output=True, text=True, timeout=300)
+    assert bad.returncode != 0 and "LVK_* kernel switches" in bad.stderr
+    ok = subprocess.run(base + ["-DLVK_IDENT=0", "-DLVK_EXPERIMENT_BUILD=1"], capture_output=True, text=True,
+                        timeout=300)
+    assert ok.returncode == 0, ok.stderr[-2000:]

@@ -20,7 +20,7 @@ def main():
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r["Kernel_Name"]
-            if "lvk::" in name and "fill_" not in name:
+            if ("lvk::" in name or "lvh::" in name) and "fill_" not in name:
                 per[name.split("(")[0].replace("void ", "")].append(
                     (int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0))
     out = {}
