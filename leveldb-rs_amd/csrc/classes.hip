@@ -89,13 +89,17 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
 // P = 2^p bytes aligned to the buffer end; piece 0's register is
 // R_0 = R(~seed, piece 0) and piece k > 0 was walked as a seed-0 buffer,
 // part = R(~0, piece k) = R(0, piece k) ^ Shift_P(~0) (the seed trick), so
-// R_k = part ^ Shift_P(~0) and R(~seed, buffer) = XOR_k Shift_{(m-1-k) P}(R_k).  One wave
-// per buffer, Horner within lanes and a tree across them, every shift a
-// wave-uniform base matrix (round 2 before: per-lane shifts by the set bits
-// of m - 1 - k, 9.9 us for 64 x 16 MiB).  A lane's run of c pieces is up to
-// 8 independent Horner chains joined by an in-lane tree: each Horner step is
-// a dependent L2 round trip (~0.18 us), and 4,096 pieces are c = 64.
-__global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__restrict__ ws,
+// R_k = part ^ Shift_P(~0) and R(~seed, buffer) = XOR_k Shift_{(m-1-k) P}(R_k).
+// Buffers of <= 64 pieces: one wave each, Horner within lanes and a tree
+// across them, every shift a wave-uniform base matrix (round 2 before:
+// per-lane shifts by the set bits of m - 1 - k, 9.9 us for 64 x 16 MiB).  A
+// lane's run of c pieces is up to 8 independent Horner chains joined by an
+// in-lane tree: each Horner step is a dependent L2 round trip (~0.18 us).
+// Buffers of more pieces: one workgroup each (round 3), with every table it
+// needs staged in LDS once -- a lone 16 MiB buffer (4,096 pieces) took 7.1 us
+// on one wave, 8 + 3 + 6 dependent L2 steps.
+constexpr uint32_t kWgJoinMin = 65;  // pieces: one workgroup per buffer from here on
+__global__ __launch_bounds__(1024) void combine_long_kernel(const uint32_t *__restrict__ ws,
                                                            const uint4 *__restrict__ longs,
                                                            const uint32_t *__restrict__ part,
                                                            const uint32_t *__restrict__ base,
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
                                                            uint32_t *__restrict__ out, uint32_t flags) {
     // the counter counts every claim; records exist only below the budget
     const uint32_t nl = min(ws[kWsLongs], kPieceBudget / 2);
-    if (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64) >= nl) return;  // block-uniform
+    if (blockIdx.x >= nl) return;  // block-uniform (every workgroup below nl has a wave or a record)
 #if !LVK_LONG_TABS
     __shared__ uint32_t M[kBaseMats * 32];
     for (uint32_t i = threadIdx.x; i < kBaseMats * 32; i += blockDim.x) M[i] = base[i];
@@ -116,14 +120,12 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
 #endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
-#if LVK_LONG_TABS && LVK_LONG_LDSP
-    __shared__ uint32_t TP[4][1024];  // per wave: Shift_P of its record
-    uint32_t *const tp = TP[threadIdx.x >> 6];
-#endif
     for (uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < nl; w += nw) {
         const uint4 r = longs[w];  // {buffer, first, m, p}
         const uint32_t m = r.z, p = r.w;
-        if (m == 0) continue;  // a claim past the piece budget: the buffer was walked whole
+        // m = 0: a claim past the piece budget, the buffer was walked whole;
+        // m >= kWgJoinMin: the workgroup loop below
+        if (m == 0 || m >= kWgJoinMin) continue;
         // pad the m pieces at the FRONT to 64 c (c = the power of two >= m / 64;
         // leading zero pieces add nothing): lane l runs Horner with Shift_P over
         // its c consecutive pieces, then a 6-level tree joins lane pairs with
@@ -150,28 +152,6 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
         };
 #pragma unroll
         for (uint32_t q = 0; q < 8; ++q) ch[q] = piece(q, 0);
-#if LVK_LONG_TABS && LVK_LONG_LDSP
-        // d - 1 dependent Shift_P steps: from an LDS copy (one HBM round trip
-        // to stage 4 KiB) instead of an L2 / HBM round trip each
-        if (d > 1) {  // wave-uniform
-            const uint4 *src = reinterpret_cast<const uint4 *>(tabs + p * 1024u);
-            uint4 *dst = reinterpret_cast<uint4 *>(tp);
-            const uint4 v0 = src[lane], v1 = src[64u + lane], v2 = src[128u + lane], v3 = src[192u + lane];
-            __builtin_amdgcn_wave_barrier();  // the previous record's reads of tp are done
-            dst[lane] = v0;
-            dst[64u + lane] = v1;
-            dst[128u + lane] = v2;
-            dst[192u + lane] = v3;
-            __builtin_amdgcn_wave_barrier();
-        }
-        for (uint32_t i = 1; i < d; ++i) {  // wave-uniform trip count
-            uint32_t rk[8];
-#pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) rk[q] = piece(q, i);
-#pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) ch[q] = tab_shift(tp, ch[q]) ^ rk[q];
-        }
-#else
         for (uint32_t i = 1; i < d; ++i) {  // wave-uniform trip count
             uint32_t rk[8];
 #pragma unroll
@@ -179,7 +159,6 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
 #pragma unroll
             for (uint32_t q = 0; q < 8; ++q) ch[q] = shift(p, ch[q]) ^ rk[q];
         }
-#endif
 #pragma unroll
         for (uint32_t t = 0; t < 3; ++t) {  // chain q joins chain q + 2^t: Shift_{d 2^t P}(left) ^ right
             if (t < lq) {
@@ -199,6 +178,249 @@ __global__ __launch_bounds__(256) void combine_long_kernel(const uint32_t *__res
             out[r.x] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
         }
     }
+    // Buffers of >= kWgJoinMin pieces, one workgroup each: the m pieces are
+    // padded at the FRONT to 1024 c (c = the power of two >= m / 1024) and
+    // staged in LDS; thread j runs Q = min(c, 4) Horner chains of d = c / Q
+    // pieces with Shift_P and an in-thread tree, then a 6-level lane tree
+    // with Shift_{c 2^t P} and a 4-level tree over the 16 wave partials with
+    // Shift_{64 c 2^t P}.  Every shift is Shift_{2^v P} for v < lc + 10 <= 12
+    // (c <= 4: m <= kMaxPieces = 4,096): the base tables p .. p + lc + 9,
+    // staged in LDS with the pieces in one round trip.  (LDS kept small: a
+    // version of this kernel at 153 KiB ran every launch several times
+    // slower.)
+    static_assert(kMaxPieces <= 4096, "join: c <= 4 pieces per thread");
+    __shared__ uint32_t TW[12 * 1024];
+    __shared__ uint32_t PW[4 * 1024 + 64];  // + one pad word per 64
+    __shared__ uint32_t wpart[kWaves];
+    const uint32_t t = threadIdx.x, wv = t >> 6, nt = blockDim.x;
+    for (uint32_t ri = blockIdx.x; ri < nl; ri += gridDim.x) {  // block-uniform
+        const uint4 r = longs[ri];
+        const uint32_t m = r.z, p = r.w;
+        if (m < kWgJoinMin) continue;
+        uint32_t c = 1, lc = 0;
+        while (nt * c < m) {
+            c <<= 1;
+            ++lc;
+        }
+        const uint32_t lq = lc < 2u ? lc : 2u, Q = 1u << lq, ld = lc - lq, d = 1u << ld;
+        const uint32_t pad = nt * c - m;
+        const uint32_t corr = tab_shift(tabs + p * 1024u, 0xffffffffu);  // Shift_P(~0): pieces k > 0 started from ~0
+        __syncthreads();  // the previous record's readers of TW / PW are done
+        // padded piece x at PW[x + x / 64]: coalesced loads, conflict-free
+        // stores, and thread t's run t c + i reads 64 distinct banks for any
+        // power of two c <= 64.  (Named registers, not an array: arrays in
+        // these copy loops were placed in LDS by the compiler.)
+        auto ldp = [&](uint32_t x) {
+            const uint32_t kp = x - pad;
+            const bool on = x < nt * c && x >= pad;
+            const uint32_t v = part[r.y + (on ? kp : 0u)];
+            return on ? v ^ (kp ? corr : 0u) : 0u;
+        };
+        auto st = [&](uint32_t x, uint32_t v) {
+            if (x < nt * c) PW[x + (x >> 6)] = v;
+        };
+        for (uint32_t x0 = t; x0 < nt * c; x0 += 8u * nt) {  // block-uniform
+            const uint32_t v0 = ldp(x0), v1 = ldp(x0 + nt), v2 = ldp(x0 + 2u * nt), v3 = ldp(x0 + 3u * nt);
+            const uint32_t v4 = ldp(x0 + 4u * nt), v5 = ldp(x0 + 5u * nt), v6 = ldp(x0 + 6u * nt), v7 = ldp(x0 + 7u * nt);
+            st(x0, v0);
+            st(x0 + nt, v1);
+            st(x0 + 2u * nt, v2);
+            st(x0 + 3u * nt, v3);
+            st(x0 + 4u * nt, v4);
+            st(x0 + 5u * nt, v5);
+            st(x0 + 6u * nt, v6);
+            st(x0 + 7u * nt, v7);
+        }
+        stage_words(TW, tabs + p * 1024u, (lc + 10u) * 256u);
+        __syncthreads();
+        auto sh = [&](uint32_t v, uint32_t a) { return tab_shift(TW + v * 1024u, a); };
+        auto pw = [&](uint32_t i) {  // thread t's padded piece t c + i
+            const uint32_t x = t * c + i;
+            return PW[x + (x >> 6)];
+        };
+        uint32_t ch[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) ch[q] = q < Q ? pw(q * d) : 0u;
+        for (uint32_t i = 1; i < d; ++i) {  // block-uniform trip count
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q)
+                if (q < Q) ch[q] = sh(0, ch[q]) ^ pw(q * d + i);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u)  // chain q joins chain q + 2^u: Shift_{d 2^u P}
+            if (u < lq) {
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q += 2u << u) ch[q] = sh(ld + u, ch[q]) ^ ch[q + (1u << u)];
+            }
+        uint32_t acc = ch[0];
+#pragma unroll
+        for (uint32_t u = 0; u < 6; ++u) {  // lane l joins lane l + 2^u: Shift_{c 2^u P}
+            const uint32_t right = __shfl_down(acc, 1u << u);
+            const uint32_t shv = sh(lc + u, acc);
+            if ((lane & ((2u << u) - 1u)) == 0) acc = shv ^ right;
+        }
+        if (lane == 0) wpart[wv] = acc;
+        __syncthreads();
+        if (wv == 0) {  // wave w holds the w-th sixteenth: a 4-level tree over lanes 0..15
+            acc = lane < kWaves ? wpart[lane] : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t right = __shfl_down(acc, 1u << u);
+                const uint32_t shv = sh(lc + 6u + u, acc);
+                if ((lane & ((2u << u) - 1u)) == 0) acc = shv ^ right;
+            }
+            if (lane == 0) {
+                const uint32_t crc = ~acc;
+                out[r.x] = (flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+            }
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Small batches (n <= kFusedMax buffers) in ONE walk launch, no sort: every
+// workgroup reads all n lengths (<= 4 KiB, L2-resident), so each knows the
+// batch's payload bytes, every buffer's split (split_rule) and the exclusive
+// prefix of the units -- a buffer is one unit, or its m pieces -- and walks
+// its share of the units with the G = 16 aligned-row walk straight from that
+// prefix.  Unit u belongs to the buffer i with pre(i) <= u < pre(i + 1) (a
+// binary search in LDS); a piece parks its raw register in part[u] and
+// workgroup 0 writes the long records for combine_long_kernel.  This replaces
+// sort_small (one launch of ~8 us that every workgroup spent reading the
+// lengths anyway) for the reference bench's few long buffers
+// (benches/crc32c.rs:54-60: 1 MiB and 16 MiB) and any other small batch.
+// The prefix lives in combine table 4's LDS (Shift_256), which a G = 16 walk
+// never reads; the LDS is otherwise full (image + output staging).
+constexpr uint32_t kFusedMax = 1024;                   // buffers: one per thread
+// The sort's split (4 KiB pieces, <= kMaxPieces per buffer).  Measured with
+// 1 KiB pieces (up to 16,384 per buffer, so that a lone 16 MiB buffer gives
+// every G = 16 group of the grid a piece): the walk gained <= 1 us and the
+// join of 16,384 pieces cost 9.2 us against ~5 for 4,096.
+constexpr uint32_t kFusedPieceLog2 = 12;
+constexpr uint32_t kFusedMaxPieces = kMaxPieces;
+constexpr uint32_t kUnitPre = (kComb + 4 * 4096) / 4;  // LDS word: unit prefix | log2 piece << 24
+constexpr uint32_t kFusedScratch = kPoolWord + 1;      // LDS words: per-wave payload sums, scan totals
+static_assert(kFusedMax <= 1024 && kUnitPre + kFusedMax <= kPoolWord, "prefix fits combine table 4");
+
+template <bool SEEDED>
+struct FusedUnits {
+    static constexpr uint32_t kFlush = 16;
+    uint32_t nbuf;  // buffers (<= kFusedMax); P.n = units
+    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
+        const bool valid = e < P.n;
+        const uint32_t u = static_cast<uint32_t>(valid ? e : P.n - 1);
+        uint32_t i = 0;  // the last buffer whose first unit is <= u
+#pragma unroll
+        for (uint32_t step = kFusedMax / 2; step >= 1; step >>= 1)
+            if (i + step < nbuf && (g_lds[kUnitPre + i + step] & 0xffffffu) <= u) i += step;
+        const uint32_t w = g_lds[kUnitPre + i];
+        const uint32_t p = w >> 24, k = u - (w & 0xffffffu);
+        const uint32_t Lb = P.len[i];
+        const uint64_t a = P.base + P.off[i];
+        const uint32_t sd = SEEDED ? P.seed[i] : 0u;
+        RGeo q;
+        q.aux = 0;
+        if (p == 0) {  // a whole buffer
+            q.a = Lb ? a : P.base;  // an empty buffer reads nothing of its own
+            q.len = Lb;
+            q.seed = sd;
+            q.bid = valid ? i : 0xffffffffu;
+        } else {  // piece k of P = 2^p bytes, aligned to the buffer's end (piece 0: the rest)
+            const uint64_t PB = 1ull << p;
+            const uint32_t m = static_cast<uint32_t>((Lb + PB - 1) >> p);
+            const uint64_t first = Lb - (static_cast<uint64_t>(m) - 1) * PB;
+            q.a = a + (k ? first + (k - 1) * PB : 0u);
+            q.len = static_cast<uint32_t>(k ? PB : first);
+            q.seed = k ? 0u : sd;  // pieces k > 0 are walked as seed-0 buffers (combine_long_kernel)
+            q.bid = valid ? (u | kPieceFlag) : 0xffffffffu;
+        }
+        return q;
+    }
+    __device__ __forceinline__ uint2 trailer(const RGeo &, uint32_t) const { return make_uint2(0, 0); }
+    __device__ __forceinline__ void stage(const Params &P, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
+                                          uint2) const {
+        g_oidx[wave][slot] = q.bid;
+        g_ocrc[wave][slot] = q.bid != 0xffffffffu && (q.bid & kPieceFlag) ? X : final_crc(P, X);
+    }
+    __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
+        const uint32_t bi = g_oidx[wave][lane], cv = g_ocrc[wave][lane];
+        if (lane >= nslots || bi == 0xffffffffu) return;
+        if (bi & kPieceFlag)
+            P.part[bi & ~kPieceFlag] = cv;
+        else
+            P.out[bi] = cv;
+    }
+};
+
+// Exclusive scan of v over the workgroup's 1024 threads (wave scans, then
+// the earlier waves' totals); *total gets the sum.  `sc` is 16 LDS words.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *sc, uint32_t *total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(inc, d);
+        if (lane >= d) inc += x;
+    }
+    if (lane == 63) sc[w] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t k = 0; k < kWaves; ++k) {
+        const uint32_t t = sc[k];
+        before += k < w ? t : 0u;
+        all += t;
+    }
+    __syncthreads();  // sc is reused by the next scan
+    *total = all;
+    return before + inc - v;
+}
+
+template <bool SEEDED>
+__global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, const uint4 *__restrict__ image,
+                                                                      uint32_t *__restrict__ ws,
+                                                                      uint4 *__restrict__ longs) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t nbuf = static_cast<uint32_t>(P.nplain);
+    const uint32_t Lt = t < nbuf ? P.len[t] : 0u;  // requested before the staging: one round trip for both
+    stage_tables(image);  // ends with a barrier: combine table 4 may be overwritten now
+    uint64_t sum = Lt;
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) sum += __shfl_xor(sum, k);
+    uint32_t *sc = g_lds + kFusedScratch;  // 2 x 16 words of payload sums, then 16 scan words
+    if (lane == 0) {
+        sc[2 * w] = static_cast<uint32_t>(sum);
+        sc[2 * w + 1] = static_cast<uint32_t>(sum >> 32);
+    }
+    __syncthreads();
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < kWaves; ++k) total += (static_cast<uint64_t>(sc[2 * k + 1]) << 32) | sc[2 * k];
+    uint32_t p = 0;
+    const uint32_t m = t < nbuf ? split_rule(Lt, total, &p, kFusedPieceLog2, kFusedMaxPieces) : 0u;
+    const uint32_t units = t < nbuf ? (m ? m : 1u) : 0u;
+    uint32_t nunits = 0, nlong = 0;
+    const uint32_t pre = block_exscan(units, sc + 32, &nunits);
+    const uint32_t lpre = block_exscan(m ? 1u : 0u, sc + 32, &nlong);
+    if (t < nbuf) g_lds[kUnitPre + t] = pre | (p << 24);
+    if (blockIdx.x == 0) {
+        if (m) longs[lpre] = make_uint4(t, pre, m, p);
+        if (t == 0) {
+            ws[kWsLongs] = nlong;
+            ws[kWsPieces] = nunits;
+        }
+    }
+    if (t == 0) g_lds[kPoolWord] = 0;
+    __syncthreads();
+    const Lut L = make_lut(lane);
+    const uint64_t grid = gridDim.x;
+    auto pool = [&]() -> uint64_t {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
+        return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+    };
+    Params Q = P;
+    Q.n = nunits;
+    sorted_stream<16, FusedUnits<SEEDED>>(Q, FusedUnits<SEEDED>{nbuf}, lane, L, pool(), pool);
 }
 
 }  // namespace lvk
@@ -230,16 +452,31 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     P.blen = 0;
     P.flags = flags;
     P.nplain = n;
-    uint4 *longs = launch_sort(ws_bytes, off, len, seed, n, s, &P);
-    g_kernel = "sort+crc32c_classes_kernel";
-    launch_classes(c, seed != nullptr, P, ws, s);
+    uint4 *longs = nullptr;
+    if (n <= lvk::kFusedMax) {
+        // small batch: the split and the walk in one launch (no sort), then the join
+        const WsLayout lay = ws_layout(n);
+        longs = reinterpret_cast<uint4 *>(ws_bytes + lay.longs);
+        P.part = reinterpret_cast<uint32_t *>(ws_bytes + lay.part);
+        g_kernel = "crc32c_fused_small_kernel+combine_long_kernel";
+        if (seed)
+            hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<true>, dim3(static_cast<uint32_t>(c.cus)),
+                               dim3(lvk::kThreads), 0, s, P, c.image[2], ws, longs);
+        else
+            hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<false>, dim3(static_cast<uint32_t>(c.cus)),
+                               dim3(lvk::kThreads), 0, s, P, c.image[2], ws, longs);
+    } else {
+        longs = launch_sort(ws_bytes, off, len, seed, n, s, &P);
+        g_kernel = "sort+crc32c_classes_kernel";
+        launch_classes(c, seed != nullptr, P, ws, s);
+    }
     // joins split long buffers (exits at once when the sort split none).  (A
     // last-finisher join inside the class kernel -- agent-scope release and
     // acquire around a per-buffer counter -- measured 64 x 16 MiB 200 -> 345
     // us and 1,024 x 64 KiB 41 -> 177 us: every fence writes back or
     // invalidates the XCD's whole L2; and C3 via offsets -2 % from spills.)
     if (longs)
-        hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(256), 0, s, ws, longs,
+        hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(1024), 0, s, ws, longs,
                            P.part, c.base_mats, c.base_tabs, out, flags);
     return 0;
 }

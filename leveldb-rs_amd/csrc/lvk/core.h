@@ -637,11 +637,23 @@ __device__ __forceinline__ uint32_t tab_shift(const uint32_t *t, uint32_t a) {
     return t[a & 0xffu] ^ t[256 + ((a >> 8) & 0xffu)] ^ t[512 + ((a >> 16) & 0xffu)] ^ t[768 + (a >> 24)];
 }
 
-// Stage n4 uint4 of `src` into LDS `dst` (16-B loads, all issued first).
+// Stage n4 uint4 of `src` into LDS `dst`: 16-B loads in batches of four per
+// thread, each batch issued before its first LDS store (a plain copy loop
+// waits for every load before the next: one L2 round trip per 16 B per
+// thread).
 __device__ __forceinline__ void stage_words(uint32_t *dst, const uint32_t *src, uint32_t n4) {
     const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
     uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-    for (uint32_t i = threadIdx.x; i < n4; i += blockDim.x) d4[i] = s4[i];
+    const uint32_t b = blockDim.x;
+    uint32_t i = threadIdx.x;
+    for (; i + 3u * b < n4; i += 4u * b) {  // named registers: an array here went to LDS
+        const uint4 v0 = s4[i], v1 = s4[i + b], v2 = s4[i + 2u * b], v3 = s4[i + 3u * b];
+        d4[i] = v0;
+        d4[i + b] = v1;
+        d4[i + 2u * b] = v2;
+        d4[i + 3u * b] = v3;
+    }
+    for (; i < n4; i += b) d4[i] = s4[i];
 }
 
 // base: Shift_{2^i} bytes, i < kBaseMats, as GF(2) matrices (32 columns).

@@ -37,7 +37,6 @@
     defined(LVK_SEAL_FLUSH) || \
     defined(LVK_SST_ROWS) || \
     defined(LVK_LONG_TABS) || \
-    defined(LVK_LONG_LDSP) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_VERIFY_WIDE))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -120,9 +119,6 @@
 #endif
 #ifndef LVK_LONG_TABS
 #define LVK_LONG_TABS 1
-#endif
-#ifndef LVK_LONG_LDSP  // Shift_P staged per wave for the Horner steps (d >= 2)
-#define LVK_LONG_LDSP 1
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

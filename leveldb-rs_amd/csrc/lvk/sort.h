@@ -100,4 +100,45 @@ __device__ __forceinline__ uint32_t key_starts(const uint32_t *ws, uint32_t *sc)
     return sc[t] - mine;
 }
 
+// Long-buffer split of the offsets API (verdict r01: a batch of a few long
+// buffers left most of the grid idle, one 16-lane group walking each).  A
+// buffer longer than the larger of 16 KiB and twice its piece length is cut
+// into m <= kMaxPieces pieces of P = 2^p bytes, aligned to its END (piece 0
+// holds the ragged rest), with P the smallest power of two >= 4 KiB, >=
+// L / kMaxPieces and >= (payload bytes of the batch) / 16,384 (one pass of
+// the grid's 16-lane groups): buffers that are long relative to the batch
+// are split, C2/C4-sized ones are not.  The pieces go after the n sorted
+// entries (claimed with a device counter, at most kPieceBudget per call;
+// a buffer that does not fit stays whole), the walk stores their raw
+// registers, and combine_long_kernel joins them.  The buffer's own sorted
+// entry becomes an empty one with no output.
+
+__device__ __forceinline__ uint32_t ceil_log2(uint64_t x) {
+    return x <= 1 ? 0u : 64u - static_cast<uint32_t>(__clzll(static_cast<long long>(x - 1)));
+}
+
+// Pieces m of a buffer of L bytes in a batch of `total` payload bytes, and
+// log2 of their length in *p; 0 when the buffer stays whole.  P >= batch
+// bytes / 16,384 must hold for every batch (no cap below 31): it bounds the
+// pieces of a call, sum m <= 16,384 + 8,192, and the split buffers, <= 8,192,
+// inside kPieceBudget and kPieceBudget / 2.  A split needs L > 2P and
+// L < 2^32, so split buffers have p <= 30, and the join's shifts Shift_{2^i},
+// i <= p + lc + 5 <= 30 + 6 + 5, stay below kBaseMats.
+// (pmin, maxp: the smallest piece, log2, and the most pieces of a buffer;
+// the sort's split keeps 4 KiB and kMaxPieces, the fused small-batch path
+// cuts finer, crc32c_fused_small_kernel.)
+__device__ __forceinline__ uint32_t split_rule(uint32_t L, uint64_t total, uint32_t *p, uint32_t pmin = 12u,
+                                               uint32_t maxp = kMaxPieces) {
+    *p = 0;
+    if (L <= 16384u) return 0u;
+    uint32_t q = ceil_log2(total / 16384u);
+    const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + maxp - 1) / maxp);
+    q = q > pl ? q : pl;
+    q = q > pmin ? q : pmin;
+    q = q < 31u ? q : 31u;
+    if (L <= (2ull << q)) return 0u;
+    *p = q;
+    return static_cast<uint32_t>((L + (1ull << q) - 1) >> q);
+}
+
 }  // namespace lvk

@@ -110,22 +110,6 @@ __global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__
 // reads and CRC stores within one 4096-buffer window).  Entries carry
 // off/len/index so the CRC kernel reads one 16-B record per buffer; seeds are
 // permuted alongside.
-// Long-buffer split of the offsets API (verdict r01: a batch of a few long
-// buffers left most of the grid idle, one 16-lane group walking each).  A
-// buffer longer than the larger of 16 KiB and twice its piece length is cut
-// into m <= kMaxPieces pieces of P = 2^p bytes, aligned to its END (piece 0
-// holds the ragged rest), with P the smallest power of two >= 4 KiB, >=
-// L / kMaxPieces and >= (payload bytes of the batch) / 16,384 (one pass of
-// the grid's 16-lane groups): buffers that are long relative to the batch
-// are split, C2/C4-sized ones are not.  The pieces go after the n sorted
-// entries (claimed with a device counter, at most kPieceBudget per call;
-// a buffer that does not fit stays whole), the walk stores their raw
-// registers, and combine_long_kernel joins them.  The buffer's own sorted
-// entry becomes an empty one with no output.
-__device__ __forceinline__ uint32_t ceil_log2(uint64_t x) {
-    return x <= 1 ? 0u : 64u - static_cast<uint32_t>(__clzll(static_cast<long long>(x - 1)));
-}
-
 // Per-wave staging of the claiming lanes' geometry (sort_scatter's 4 waves).
 __shared__ uint4 g_split[kSortThreads / 64][64];     // {offset lo, hi, length, seed}
 __shared__ uint32_t g_split_pre[kSortThreads / 64][64];  // inclusive prefix of the piece counts
@@ -141,20 +125,8 @@ __device__ __forceinline__ bool split_wave(bool valid, uint64_t o, uint32_t L, u
                                            uint32_t *__restrict__ sseed, bool seeded, uint4 *__restrict__ longs,
                                            uint32_t lane) {
     if (!longs) return false;  // splitting is off for this call (wave-uniform)
-    uint32_t m = 0, p = 0;
-    if (valid && L > 16384u) {
-        p = ceil_log2(total / 16384u);
-        const uint32_t pl = ceil_log2((static_cast<uint64_t>(L) + kMaxPieces - 1) / kMaxPieces);
-        p = p > pl ? p : pl;
-        p = p > 12u ? p : 12u;
-        // No lower cap than 31: P >= batch bytes / 16,384 must hold for every
-        // batch (it bounds sum m <= 16,384 + 8,192 and the split buffers <= 8,192,
-        // inside kPieceBudget and kPieceBudget / 2).  A split needs L > 2P and
-        // L < 2^32, so split buffers have p <= 30, and the join's shifts
-        // Shift_{2^i}, i <= p + lc + 5 <= 30 + 6 + 5, stay below kBaseMats.
-        p = p < 31u ? p : 31u;
-        if (L > (2ull << p)) m = static_cast<uint32_t>((L + (1ull << p) - 1) >> p);
-    }
+    uint32_t p = 0;
+    const uint32_t m = valid ? split_rule(L, total, &p) : 0u;
     const uint64_t want = __ballot(m > 0);
     if (!want) return false;  // wave-uniform
     uint32_t incl = m;  // inclusive prefix of m over the wave
@@ -344,15 +316,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_small(const uint64_t *__res
         const uint32_t k = sort_key(l[e]);
         wave_count(hall, k, valid, lane);
         wave_count(hpre, k, valid && i < lo, lane);
-        uint32_t m = 0, p = 0;
-        if (longs && valid && l[e] > 16384u) {  // split_wave's rule
-            p = ceil_log2(total / 16384u);
-            const uint32_t pl = ceil_log2((static_cast<uint64_t>(l[e]) + kMaxPieces - 1) / kMaxPieces);
-            p = p > pl ? p : pl;
-            p = p > 12u ? p : 12u;
-            p = p < 31u ? p : 31u;  // split_wave's bound (see there)
-            if (l[e] > (2ull << p)) m = static_cast<uint32_t>((l[e] + (1ull << p) - 1) >> p);
-        }
+        uint32_t p = 0;
+        const uint32_t m = longs && valid ? split_rule(l[e], total, &p) : 0u;
         // exclusive scans over t of m and (m > 0), plus the running totals of rows e' < e
         uint32_t im = m, il = m > 0 ? 1u : 0u;
 #pragma unroll

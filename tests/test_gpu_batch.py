@@ -510,8 +510,8 @@ def test_two_threads_same_stream(torch_dev, arena):
 def test_kernel_choice_query(torch_dev):
     """lv_crc32c_last_kernel names the path a call took: aligned whole-batch
     blocks run the uniform-block kernel (G by block count), unaligned strided
-    geometry the generic strided kernel, the offsets API the sort + class
-    kernel."""
+    geometry the generic strided kernel, the offsets API the fused small-batch
+    kernel (<= 1,024 buffers) or the sort + class kernel."""
     torch, dev = torch_dev
     t = torch.zeros(4096 * 2048 + 64, dtype=torch.uint8, device=dev)
     lvgpu.batch_strided(t, 4096, 4096, 2048)
@@ -522,6 +522,10 @@ def test_kernel_choice_query(torch_dev):
     assert lvgpu.last_kernel().startswith("crc32c_batch_kernel<") and lvgpu.last_kernel().endswith(",strided>")
     o = torch.arange(16, dtype=torch.int64, device=dev) * 100
     ln = torch.full((16,), 100, dtype=torch.int32, device=dev)
+    lvgpu.batch(t, o, ln)  # <= 1,024 buffers: split + walk in one launch, then the join
+    assert lvgpu.last_kernel() == "crc32c_fused_small_kernel+combine_long_kernel"
+    o = torch.arange(1025, dtype=torch.int64, device=dev) * 100
+    ln = torch.full((1025,), 100, dtype=torch.int32, device=dev)
     lvgpu.batch(t, o, ln)
     assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel"
     torch.cuda.synchronize()
