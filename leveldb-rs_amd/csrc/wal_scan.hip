@@ -120,20 +120,27 @@ __device__ __forceinline__ uint32_t wal_touch(const uint8_t *log, uint64_t b0, u
     return x;
 }
 
-__global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
-                                                         uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ M,
-                                                         uint64_t *__restrict__ wgrec, uint32_t *__restrict__ blkcnt,
-                                                         uint64_t *__restrict__ hcache) {
+// One thread per block, kWalHistThreads per workgroup: with 64 (one wave,
+// 33 KiB of header cache) the 32,768 blocks of a 1 GiB log spread over 512
+// workgroups on all CUs; 256 threads (130 KiB each, one workgroup per CU)
+// left half the CUs idle and put two chains per SIMD.
+constexpr uint32_t kWalHistThreads = 64;
+__global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
+                                                            uint64_t nblocks, uint64_t chunk,
+                                                            uint32_t *__restrict__ M, uint64_t *__restrict__ wgrec,
+                                                            uint32_t *__restrict__ blkcnt,
+                                                            uint64_t *__restrict__ hcache) {
+    constexpr uint32_t T = kWalHistThreads;
     __shared__ uint32_t h[kKeys];
-    __shared__ uint64_t wsum[kSortThreads / 64];
-    __shared__ uint64_t hcl[kSortThreads * (kHdrCache + 1)];  // per-thread header cache (130 KiB)
+    __shared__ uint64_t wsum[T / 64];
+    __shared__ uint64_t hcl[T * (kHdrCache + 1)];  // per-thread header cache
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    h[t] = 0;
+    for (uint32_t k = t; k < kKeys; k += T) h[k] = 0;
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
     uint64_t mine = 0;
     uint32_t touched = 0;
-    for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
+    for (uint64_t b0 = lo; b0 < hi; b0 += T) {  // block-uniform
         const uint64_t b = b0 + t;
         const uint64_t start = b * kWalBlock;
         const uint32_t blen = b < hi ? static_cast<uint32_t>(size - start < kWalBlock ? size - start : kWalBlock) : 0u;
@@ -168,8 +175,12 @@ __global__ __launch_bounds__(kSortThreads) void wal_hist(const uint8_t *__restri
     if (lane == 0) wsum[t >> 6] = mine;
     asm volatile("" ::"v"(touched));  // the touches are kept
     __syncthreads();
-    M[static_cast<uint64_t>(blockIdx.x) * kKeys + t] = h[t];
-    if (t == 0) wgrec[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // sort_scan sums these
+    for (uint32_t k = t; k < kKeys; k += T) M[static_cast<uint64_t>(blockIdx.x) * kKeys + k] = h[k];
+    if (t == 0) {
+        uint64_t all = 0;
+        for (uint32_t w = 0; w < T / 64; ++w) all += wsum[w];
+        wgrec[blockIdx.x] = all;  // sort_scan sums these
+    }
 }
 
 // Output of the WAL scan, in log order (lv_wal_scan_device).
@@ -311,7 +322,7 @@ extern "C" {
 
 // ---- WAL scan of a log in HBM (include/lvgpu/wal.h) ----
 static uint64_t wal_wgs(uint64_t nblocks, uint64_t *chunk) {
-    uint64_t wgs = (nblocks + lvk::kSortThreads - 1) / lvk::kSortThreads;
+    uint64_t wgs = (nblocks + lvk::kWalHistThreads - 1) / lvk::kWalHistThreads;
     wgs = std::max<uint64_t>(1, std::min<uint64_t>(wgs, lvk::kSortMaxWgs));
     *chunk = (nblocks + wgs - 1) / wgs;
     return wgs;
@@ -367,7 +378,7 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     uint64_t chunk = 0;
     const uint64_t wgs = wal_wgs(nblocks, &chunk);
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
-    hipLaunchKernelGGL(lvk::wal_hist, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk,
+    hipLaunchKernelGGL(lvk::wal_hist, g, dim3(lvk::kWalHistThreads), 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk,
                        hc);
     launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgrec, s);
     lvk::WalOut o{d_hdr_off, d_info, d_count, cap};
