@@ -4,9 +4,12 @@
 #   bench defaults, C3 offsets, C2, C4, C5 (8 GiB per GPU) and C5 strong (the
 #   64 GiB global batch), the C1 CPU sweep, the host-memory E2E path, the WAL
 #   (host and device-resident) / table / hash rows of SURVEY 8f, the 4-64 KiB
-#   sweep, few-long-buffer batches, and rocprofv3 kernel-trace stats for C3
-#   (strided) / C2 / C4 / the WAL device scan.  Every GPU step has its own
-#   timeout and the chain stops at the first failure.
+#   sweep, few-long-buffer batches, rocprofv3 kernel-trace stats for C3
+#   (strided) / C2 / C4 / the WAL device scan / the SST and hash kernels (with
+#   FETCH_SIZE / WRITE_SIZE passes) / the few-long-buffer offsets calls, and
+#   the N=2 launcher rehearsal (gloo, both ranks on the one GPU).  Every GPU
+#   step has its own timeout and the chain stops at the first failure;
+#   tools/round_summary.py writes summary.md (events beside rocprof sums).
 # usage: tools/measure_round.sh OUTDIR
 set -o pipefail
 out=${1:-gpurun_out/round}
@@ -40,4 +43,9 @@ p c4 --workload c4 --api offsets &&
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_wal" -o wal -- \
    python3 "$root/bench.py" --wal-device --steps 50 --warmup 20) > "$out/prof_wal.log" 2>&1 &&
 python3 tools/kstats_steady.py "$(ls "$out/prof_wal"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_wal_steady.json" > /dev/null &&
+bash tools/prof_8f.sh "$out/prof8f" table hash &&
+bash tools/prof_long.sh "$out/prof_long" &&
+LVGPU_BENCH_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 > "$out/gloo2.json" 2> "$out/gloo2.err" &&
+for d in "$out"/prof_*/; do find "$d" -name '*kernel_trace.csv' -size +1M -delete; done;
+python3 tools/round_summary.py "$out" > "$out/summary.md" &&
 echo "all steps done"
