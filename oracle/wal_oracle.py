@@ -9,7 +9,7 @@ the GPU batched WAL encode / verify paths.  CRCs come from the C oracle
 cpu_baseline leg may import this module.
 
 Pinned by the reference's own WAL tests (`log_writer.rs:445-838`), replayed in
-`tests/test_wal_oracle.py`.
+`tests/test_wal_log.py` (and `tests/test_wal_boundary.py` for the host reader).
 """
 from __future__ import annotations
 
