@@ -167,3 +167,20 @@ def test_product_build_refuses_kernel_switches():
     ok = subprocess.run(base + ["-DLVK_IDENT=0", "-DLVK_EXPERIMENT_BUILD=1"], capture_output=True, text=True,
                         timeout=300)
     assert ok.returncode == 0, ok.stderr[-2000:]
+
+
+def test_device_counters_query():
+    """lv_device_counters: readable without a GPU (zero before any host-path
+    call), bounds-checked, and a short `n` fills only that many slots."""
+    import ctypes
+    L = lvgpu.lib()
+    out = (ctypes.c_uint64 * 4)(7, 7, 7, 7)
+    assert L.lv_device_counters(0, ctypes.cast(out, ctypes.c_void_p), 3) == 0
+    assert out[3] == 7  # only three counters exist
+    out2 = (ctypes.c_uint64 * 2)(9, 9)
+    assert L.lv_device_counters(1, ctypes.cast(out2, ctypes.c_void_p), 1) == 0 and out2[1] == 9
+    assert L.lv_device_counters(64, ctypes.cast(out, ctypes.c_void_p), 3) != 0
+    assert L.lv_device_counters(-1, ctypes.cast(out, ctypes.c_void_p), 3) != 0
+    assert L.lv_device_counters(0, None, 3) != 0
+    assert L.lv_device_counters(0, None, 0) == 0
+    assert set(lvgpu.device_counters(0)) == {"h2d", "d2h", "allocs"}
