@@ -306,6 +306,7 @@ static_assert(kFusedMax <= 1024 && kUnitPre + kFusedMax <= kPoolWord, "prefix fi
 template <bool SEEDED>
 struct FusedUnits {
     static constexpr uint32_t kFlush = 16;
+    static constexpr bool kAlMid = true;
     uint32_t nbuf;  // buffers (<= kFusedMax); P.n = units
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;

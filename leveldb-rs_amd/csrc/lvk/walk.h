@@ -233,11 +233,24 @@ __device__ __forceinline__ uint32_t round_jfix_al(const RGeo &q, uint32_t nbw) {
 // a clamp would.
 static __device__ __attribute__((aligned(256))) uint4 g_zero_granules[16];  // zero-initialised
 
+// jfix: the round's last head batch (round_jfix_al).  Past it and before the
+// last batch every group's granules lie inside its buffer (a group's rows end
+// at its last whole granule's row, and only that row holds granules past the
+// end), so those batches take plain addresses, no range selects (C2 / C4 /
+// WAL +0.3-1 %; the table walk, 6 batches of 3 rows per unit, measured
+// -0.7 % and passes no jfix: Src::kAlMid, profiles/r03/walk/ab_al_mid.txt).
 template <uint32_t NU>
 __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
-                                               uint4 (&v)[NU]) {
+                                               uint4 (&v)[NU], uint32_t jfix = 0xffffffffu) {
     const AGeo g = al_geo(q);
     const uint64_t ab = q.abase();
+    if (jfix != 0xffffffffu && j > jfix && j + 1u < nbw) {  // wave-uniform
+        const uint64_t a0 = ab + (static_cast<uint64_t>(static_cast<uint32_t>(
+                                      16 * al_row<NU>(g, nbw, j, 0) + static_cast<int32_t>(gl) - g.ph)) << 4);
+#pragma unroll
+        for (uint32_t i = 0; i < NU; ++i) v[i] = load16(a0 + 256u * i);
+        return;
+    }
     const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) {
@@ -382,6 +395,7 @@ __device__ __forceinline__ uint32_t finish_raw(const RGeo &q, uint32_t X, const 
 template <bool SEEDED>
 struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
+    static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         if (!ident) return load_rgeo<SEEDED>(P, e);
@@ -472,7 +486,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         const bool more = rhon < nr;
         if (!lastj) {
             if constexpr (AL)
-                load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt);
+                load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt, Src::kAlMid ? jfix : 0xffffffffu);
             else
                 load_rbatch<G>(q, nbw, j + 1, gl, nxt);
         } else {
