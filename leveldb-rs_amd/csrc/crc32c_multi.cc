@@ -14,7 +14,8 @@
 // range's payload (plus kPackSlack), the range's buffers are packed into a
 // contiguous host copy first, in index order, so the device receives its
 // payload and nothing else; the pack is one host memcpy of the payload,
-// the same work the pageable upload's staging copy does anyway.
+// the same work the pageable upload's staging copy does anyway, done in
+// chunks of kPackChunk bytes so the copy never holds a range's whole payload.
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -47,6 +48,43 @@ struct Shard {
 
 constexpr double kPackRatio = 1.5;
 constexpr uint64_t kPackSlack = 1ull << 20;
+constexpr uint64_t kPackChunk = 256ull << 20;
+
+// Ships a scattered range in sub-ranges of at most kPackChunk payload bytes
+// (a lone longer buffer is its own sub-range and ships from the arena as
+// is), each packed into one reused host buffer: host memory stays bounded
+// by the chunk however large the range's payload is.
+int packed_ranges(const uint8_t *arena, const uint64_t *off, const uint32_t *len, const uint32_t *seed,
+                  uint32_t *out, size_t cnt, uint32_t flags, int device) {
+    std::vector<uint8_t> packed;
+    std::vector<uint64_t> poff;
+    for (size_t lo = 0; lo < cnt;) {
+        if (len[lo] >= kPackChunk) {
+            const uint64_t zero = 0;
+            const int rc = lv_crc32c_batch_host(arena + off[lo], len[lo], &zero, len + lo, seed ? seed + lo : nullptr,
+                                                out + lo, 1, flags, device);
+            if (rc) return rc;
+            ++lo;
+            continue;
+        }
+        size_t hi = lo;
+        uint64_t bytes = 0;
+        while (hi < cnt && len[hi] < kPackChunk && bytes + len[hi] <= kPackChunk) bytes += len[hi++];
+        packed.resize(bytes ? bytes : 1);  // non-null even for all-empty buffers
+        poff.resize(hi - lo);
+        uint64_t pos = 0;
+        for (size_t k = lo; k < hi; ++k) {
+            std::memcpy(packed.data() + pos, arena + off[k], len[k]);
+            poff[k - lo] = pos;
+            pos += len[k];
+        }
+        const int rc = lv_crc32c_batch_host(packed.data(), bytes, poff.data(), len + lo, seed ? seed + lo : nullptr,
+                                            out + lo, hi - lo, flags, device);
+        if (rc) return rc;
+        lo = hi;
+    }
+    return LV_OK;
+}
 
 }  // namespace
 
@@ -75,25 +113,15 @@ int lv_crc32c_batch_multi_devices(const uint8_t *h_arena, size_t arena_bytes, co
                 last = std::max(last, h_off[i] + h_len[i]);
                 payload += h_len[i];
             }
-            std::vector<uint64_t> off(h_off + lo, h_off + lo + cnt);
-            const uint8_t *span = h_arena + first;
-            uint64_t span_bytes = last - first;
-            std::vector<uint8_t> packed;
-            if (static_cast<double>(span_bytes) > kPackRatio * static_cast<double>(payload) + kPackSlack) {
-                packed.resize(payload ? payload : 1);  // non-null even for all-empty buffers
-                uint64_t pos = 0;
-                for (size_t k = 0; k < cnt; ++k) {
-                    std::memcpy(packed.data() + pos, h_arena + h_off[lo + k], h_len[lo + k]);
-                    off[k] = pos;
-                    pos += h_len[lo + k];
-                }
-                span = packed.data();
-                span_bytes = payload;
-            } else {
+            const uint32_t *seed = h_seed ? h_seed + lo : nullptr;
+            if (static_cast<double>(last - first) <= kPackRatio * static_cast<double>(payload) + kPackSlack) {
+                std::vector<uint64_t> off(h_off + lo, h_off + lo + cnt);
                 for (auto &o : off) o -= first;  // this device's span starts at `first`
+                res[r].rc = lv_crc32c_batch_host(h_arena + first, last - first, off.data(), h_len + lo, seed,
+                                                 h_out + lo, cnt, flags, devices[r]);
+            } else {
+                res[r].rc = packed_ranges(h_arena, h_off + lo, h_len + lo, seed, h_out + lo, cnt, flags, devices[r]);
             }
-            res[r].rc = lv_crc32c_batch_host(span, span_bytes, off.data(), h_len + lo,
-                                             h_seed ? h_seed + lo : nullptr, h_out + lo, cnt, flags, devices[r]);
             if (res[r].rc) res[r].err = lv_last_error();
         });
     }

@@ -151,20 +151,42 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         // every hop's wait for its header load also wait for the previous
         // hop's store.
         uint64_t *const hl = hcl + t * (kHdrCache + 1);  // stride 65 words: lanes spread over the banks
+        // Software-pipelined hop: decode the header, issue the NEXT header's
+        // loads, and only then do this record's bookkeeping (sort key, header
+        // cache, histogram ballots and LDS atomic) while that load is in
+        // flight (+0.9 % on the 1 GiB scan, profiles/r03/wal/ab_pipe.txt).
+        uint64_t wlo = 0, whi = 0;
+        uint32_t wsh = 0;
+        auto issue = [&](uint32_t p, bool on) {
+            const uint64_t pa = start + p, a = pa & ~7ull;
+            const uint64_t *w = reinterpret_cast<const uint64_t *>(log + a);
+            wsh = static_cast<uint32_t>(pa & 7u) * 8u;
+            wlo = on && a < size ? w[0] : 0ull;
+            whi = on && wsh && a + 8 < size ? w[1] : 0ull;
+        };
+        issue(0, active);
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
                 touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
-            uint32_t key = 0;
             const bool rec = active;
+            WalRec r{};
+            uint32_t npos = pos;
+            bool nact = false;
             if (active) {
-                const WalRec r = wal_record(log, size, start, blen, pos);
+                r = wal_decode(wsh ? (wlo >> wsh) | (whi << (64u - wsh)) : wlo, blen, pos);
+                npos = pos + kWalHeader + r.len;
+                nact = r.status == LV_WAL_REC_OK && blen - npos >= kWalHeader;
+            }
+            issue(npos, nact);
+            uint32_t key = 0;
+            if (rec) {
                 key = sort_key(r.ulen);
                 if (cnt < kHdrCache) hl[cnt] = hdr_pack(pos, r.len, r.type);
                 ++cnt;
-                pos += kWalHeader + r.len;
-                active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
             }
             wave_count(h, key, rec, lane);
+            pos = npos;
+            active = nact;
         }
         for (uint32_t c = 0; c < cnt && c < kHdrCache; ++c) hcache[b * kHdrCache + c] = hl[c];
         if (b < hi) blkcnt[b] = cnt;

@@ -338,6 +338,34 @@ def test_batch_multi_ships_each_device_its_buffers(gpu):
     assert moved <= payload + 16 * n
 
 
+def test_batch_multi_packs_a_large_scatter_in_chunks(gpu):
+    """A scattered gather whose range payload (~0.55 GiB, under 2/3 of its
+    1 GiB span) exceeds the host pack chunk (256 MiB): the range ships in
+    packed sub-ranges, a lone 260 MiB buffer straight from the arena; CRCs equal the oracle and the
+    device still receives the payload, not the 1 GiB arena."""
+    import numpy as np
+    rng = np.random.default_rng(77)
+    arena_n = 1 << 30
+    arena = np.frombuffer(rng.bytes(arena_n), dtype=np.uint8)
+    big = 260 << 20
+    n_small = 150
+    lens = np.full(n_small + 1, 2 << 20, dtype=np.uint32)
+    lens[n_small // 2] = big
+    lens[:n_small // 2] -= rng.integers(0, 4096, size=n_small // 2).astype(np.uint32)
+    slots = rng.permutation((arena_n - big) // (2 << 20))[:n_small + 1].astype(np.uint64) * np.uint64(2 << 20)
+    offs = slots.copy()
+    offs[n_small // 2] = arena_n - big
+    offs[0] = 0
+    payload = int(lens.sum(dtype=np.uint64))
+    want = np.zeros(lens.size, dtype=np.uint32)
+    W.lib().oracle_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, want.ctypes.data, lens.size, 0)
+    before = lvgpu.device_counters(0)
+    got = lvgpu.batch_multi(arena, offs, lens, None, devices=[0])
+    moved = lvgpu.device_counters(0)["h2d"] - before["h2d"]
+    assert np.array_equal(got, want)
+    assert moved <= payload + 16 * lens.size + (4 << 20), (moved, payload)
+
+
 def test_sorted_walk_edges(torch_dev, arena):
     """Offsets API edge geometry for the wave-uniform walk: lengths at the
     class edges (256/257, 2048/2049, 32768/32769) and at batch-count edges of
