@@ -79,8 +79,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
             if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
             return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
         };
-        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), SortedList<SEEDED>{ident}, lane, L, pool(),
-                          pool);
+        SortedList<SEEDED> src{ident};
+        if (LVK_CLASS3_FIRST && cls[6] && cls[7]) {  // both classes: class 3 first (SortedList::r3)
+            src.n2 = cls[6];
+            src.r3 = cls[7];
+        }
+        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), src, lane, L, pool(), pool);
     }
 }
 

@@ -38,7 +38,10 @@
     defined(LVK_SST_ROWS) || \
     defined(LVK_LONG_TABS) || \
     defined(LVK_SORT_MIN_WGS) || \
-    defined(LVK_VERIFY_WIDE))
+    defined(LVK_VERIFY_WIDE) || \
+    defined(LVK_CLASS3_FIRST) || \
+    defined(LVK_EXP_WAL_MAXHOPS) || \
+    defined(LVK_EXP_WAL_NOBOOK))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -125,4 +128,13 @@
 #endif
 #ifndef LVK_VERIFY_WIDE  // experiment: the four-word verify staging even without crc_out
 #define LVK_VERIFY_WIDE 0
+#endif
+#ifndef LVK_CLASS3_FIRST  // class kernel: walk class 3 (> 32 KiB) before class 2 (SortedList::r3)
+#define LVK_CLASS3_FIRST 0
+#endif
+#ifndef LVK_EXP_WAL_MAXHOPS  // experiment (wrong framing): wal_hist stops every chain after this many hops (0: off)
+#define LVK_EXP_WAL_MAXHOPS 0
+#endif
+#ifndef LVK_EXP_WAL_NOBOOK  // experiment (wrong framing): wal_hist hops skip the histogram and header cache
+#define LVK_EXP_WAL_NOBOOK 0
 #endif

@@ -168,6 +168,7 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
                 touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
+            if (LVK_EXP_WAL_MAXHOPS && cnt >= LVK_EXP_WAL_MAXHOPS) active = false;  // timing only
             const bool rec = active;
             WalRec r{};
             uint32_t npos = pos;
@@ -179,6 +180,12 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
             }
             issue(npos, nact);
             uint32_t key = 0;
+            if (LVK_EXP_WAL_NOBOOK) {  // timing only
+                cnt += rec ? 1u : 0u;
+                pos = npos;
+                active = nact;
+                continue;
+            }
             if (rec) {
                 key = sort_key(r.ulen);
                 if (cnt < kHdrCache) hl[cnt] = hdr_pack(pos, r.len, r.type);
