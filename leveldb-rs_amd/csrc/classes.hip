@@ -74,17 +74,27 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         if (4ull * np >= 3ull * (n23 + np) && bytes >= (64ull << 10) * grid * kWaves)
             for (uint32_t k = 0; k < wave * LVK_STAGGER; ++k) __builtin_amdgcn_s_sleep(32);
 #endif
+        // Walk order of classes 2 + 3 (each sorted longest first): with both
+        // present, the full rounds are rotated to start at class 3's first
+        // round, so the pool ends on class 2's shortest buffers instead of a
+        // round of 32-64 KiB buffers (the persistent grid's ragged end).  The
+        // rotation is on the wave-uniform round index (scalar registers: an
+        // entry remap in SortedList::load cost the class kernel 5 VGPRs of
+        // spills and C3 via offsets 5 %).
+        const uint64_t rrot = (LVK_CLASS3_FIRST && cls[6] && cls[7]) ? n23 / 4u : 0u;  // K = 4 entries per round
+        const uint64_t s3 = cls[6] / 4u;
         auto pool = [&]() -> uint64_t {
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
-            return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+            uint64_t rho = blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+            if (rho < rrot) {
+                rho += s3;
+                if (rho >= rrot) rho -= rrot;
+            }
+            return rho;
         };
-        SortedList<SEEDED> src{ident};
-        if (LVK_CLASS3_FIRST && cls[6] && cls[7]) {  // both classes: class 3 first (SortedList::r3)
-            src.n2 = cls[6];
-            src.r3 = cls[7];
-        }
-        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), src, lane, L, pool(), pool);
+        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), SortedList<SEEDED>{ident}, lane, L, pool(),
+                          pool);
     }
 }
 

@@ -41,7 +41,11 @@
     defined(LVK_VERIFY_WIDE) || \
     defined(LVK_CLASS3_FIRST) || \
     defined(LVK_EXP_WAL_MAXHOPS) || \
-    defined(LVK_EXP_WAL_NOBOOK))
+    defined(LVK_EXP_WAL_NOBOOK) || \
+    defined(LVK_WAL_LANE_COUNT) || \
+    defined(LVK_EXP_WAL_NOCACHE) || \
+    defined(LVK_EXP_WAL_NOCOUNT) || \
+    defined(LVK_WAL_LEAN_HOP))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -130,11 +134,23 @@
 #define LVK_VERIFY_WIDE 0
 #endif
 #ifndef LVK_CLASS3_FIRST  // class kernel: walk class 3 (> 32 KiB) before class 2 (SortedList::r3)
-#define LVK_CLASS3_FIRST 0
+#define LVK_CLASS3_FIRST 1
 #endif
 #ifndef LVK_EXP_WAL_MAXHOPS  // experiment (wrong framing): wal_hist stops every chain after this many hops (0: off)
 #define LVK_EXP_WAL_MAXHOPS 0
 #endif
 #ifndef LVK_EXP_WAL_NOBOOK  // experiment (wrong framing): wal_hist hops skip the histogram and header cache
 #define LVK_EXP_WAL_NOBOOK 0
+#endif
+#ifndef LVK_WAL_LANE_COUNT  // wal_hist: per-lane LDS atomic per record instead of the wave-aggregated count
+#define LVK_WAL_LANE_COUNT 1
+#endif
+#ifndef LVK_EXP_WAL_NOCACHE  // experiment (wrong framing): wal_hist hops skip the header cache write
+#define LVK_EXP_WAL_NOCACHE 0
+#endif
+#ifndef LVK_EXP_WAL_NOCOUNT  // experiment (wrong framing): wal_hist hops skip the sort key and histogram
+#define LVK_EXP_WAL_NOCOUNT 0
+#endif
+#ifndef LVK_WAL_LEAN_HOP  // wal_hist: branch-free hop body (0: the branchy one with its timing knobs)
+#define LVK_WAL_LEAN_HOP 1
 #endif

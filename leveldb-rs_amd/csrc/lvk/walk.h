@@ -397,16 +397,8 @@ struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
-    // Walk order of the large-buffer list (classes 2 + 3, each sorted longest
-    // first): the r3 class-3 entries (> 32 KiB) before the n2 class-2 ones, so
-    // the pool ends on the shortest buffers instead of a round of 32-64 KiB
-    // buffers (the persistent grid's ragged end).  r3 = 0: the sorted order.
-    uint32_t n2 = 0, r3 = 0;
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
-        if (!ident) {
-            if (r3) e = e < r3 ? e + n2 : (e < static_cast<uint64_t>(n2) + r3 ? e - r3 : e);
-            return load_rgeo<SEEDED>(P, e);
-        }
+        if (!ident) return load_rgeo<SEEDED>(P, e);
         const bool valid = e < P.n;
         const uint64_t ec = valid ? e : P.n - 1;
         RGeo q;

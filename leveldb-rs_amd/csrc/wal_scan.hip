@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
                                                             uint32_t *__restrict__ blkcnt,
                                                             uint64_t *__restrict__ hcache) {
     constexpr uint32_t T = kWalHistThreads;
-    __shared__ uint32_t h[kKeys];
+    __shared__ uint32_t h[kKeys + 64];  // + a dummy bin per lane (LVK_WAL_LEAN_HOP)
     __shared__ uint64_t wsum[T / 64];
     __shared__ uint64_t hcl[T * (kHdrCache + 1)];  // per-thread header cache
     const uint32_t t = threadIdx.x, lane = t & 63u;
@@ -151,7 +151,53 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         // every hop's wait for its header load also wait for the previous
         // hop's store.
         uint64_t *const hl = hcl + t * (kHdrCache + 1);  // stride 65 words: lanes spread over the banks
-        // Software-pipelined hop: decode the header, issue the NEXT header's
+#if LVK_WAL_LEAN_HOP
+        // Branch-free hop: every lane runs every instruction of the loop body
+        // (no exec-mask branches) but the loads, the next header's loads are
+        // issued right after the decode, and this record's bookkeeping -- the
+        // header cache slot in LDS and a fire-and-forget LDS atomic on its sort
+        // key -- runs while they are in flight.  Finished lanes write their pad
+        // cache slot (64) and count into a per-lane dummy bin.  (Loads for
+        // every lane, finished ones rereading their last header from L2, made
+        // wal_hist 26.8 -> 41.8 us: a load instruction's cost grows with the
+        // lines its lanes touch.)  One wave per SIMD runs this loop alone, so the
+        // hop is bound by its instruction latency as much as by the load:
+        // timing variants put the header cache write and the key count at
+        // ~6.5 us each of a 26.8 us wal_hist with the branchy body (the
+        // wave-aggregated count before it: 31.8 us).
+        const uint64_t lastw = (size - 1) & ~7ull;  // the last aligned word holding a log byte
+        uint64_t wlo = 0, whi = 0;
+        uint32_t wsh = 0;
+        auto issue = [&](uint32_t p, bool on) {  // bytes of the log's end word past it are never used
+            const uint64_t pa = start + p, a = pa & ~7ull;
+            wsh = static_cast<uint32_t>(pa & 7u) * 8u;
+            if (on) {  // exec-masked: a load's cost grows with the lines its active lanes touch
+                wlo = *reinterpret_cast<const uint64_t *>(log + (a < lastw ? a : lastw));
+                whi = *reinterpret_cast<const uint64_t *>(log + (a + 8 < lastw ? a + 8 : lastw));
+            }
+        };
+        issue(0, active);
+        while (__any(active)) {  // wave-uniform: the longest chain of the wave
+            if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
+                touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
+            const uint64_t hw = (wlo >> wsh) | ((whi << 1) << (63u - wsh));  // bytes pos .. pos + 7
+            const uint32_t len = static_cast<uint32_t>(hw >> 32) & 0xffffu;
+            const uint32_t type = static_cast<uint32_t>(hw >> 48) & 0xffu;
+            // log_reader.rs:312-331: BAD_LENGTH past the block, ZERO at a 0/0 header
+            const bool ok = kWalHeader + len <= blen - pos && (type | len) != 0u;
+            const uint32_t npos = pos + kWalHeader + len;
+            const bool nact = active && ok && blen - npos >= kWalHeader;
+            issue(npos, nact);
+            const uint32_t slot = active && cnt < kHdrCache ? cnt : kHdrCache;
+            hl[slot] = hdr_pack(pos, len, type);
+            const uint32_t key = active ? sort_key(ok ? len + 1u : 0u) : kKeys + lane;
+            __hip_atomic_fetch_add(&h[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            cnt += active ? 1u : 0u;
+            pos = npos;
+            active = nact;
+        }
+#else
+        // (round 3 second pass) Software-pipelined hop: decode the header, issue the NEXT header's
         // loads, and only then do this record's bookkeeping (sort key, header
         // cache, histogram ballots and LDS atomic) while that load is in
         // flight (+0.9 % on the 1 GiB scan, profiles/r03/wal/ab_pipe.txt).
@@ -187,14 +233,27 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
                 continue;
             }
             if (rec) {
-                key = sort_key(r.ulen);
-                if (cnt < kHdrCache) hl[cnt] = hdr_pack(pos, r.len, r.type);
+                if (!LVK_EXP_WAL_NOCOUNT) key = sort_key(r.ulen);
+                if (!LVK_EXP_WAL_NOCACHE && cnt < kHdrCache) hl[cnt] = hdr_pack(pos, r.len, r.type);
                 ++cnt;
             }
+            if (LVK_EXP_WAL_NOCOUNT) {  // timing only
+                pos = npos;
+                active = nact;
+                continue;
+            }
+#if LVK_WAL_LANE_COUNT
+            // one fire-and-forget LDS atomic per record (no return, no wait):
+            // the wave-aggregated count (ballots, a lane broadcast through
+            // LDS and its wait, branches) sat on every hop of the chain
+            if (rec) __hip_atomic_fetch_add(&h[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
             wave_count(h, key, rec, lane);
+#endif
             pos = npos;
             active = nact;
         }
+#endif
         for (uint32_t c = 0; c < cnt && c < kHdrCache; ++c) hcache[b * kHdrCache + c] = hl[c];
         if (b < hi) blkcnt[b] = cnt;
         mine += cnt;
