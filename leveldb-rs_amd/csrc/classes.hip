@@ -17,6 +17,7 @@ namespace lvk {
 // per CU as on 16 (it is bound by per-buffer VALU work and random line
 // reads, not latency), and classes 2+3 run FASTER on 12 waves than on 16.
 constexpr uint32_t kSmallWaves = LVK_SMALL_WAVES;
+constexpr uint32_t kSmallRounds = LVK_SMALL_ROUNDS;  // small-class rounds per wave (LVK_SMALL_ADAPT)
 
 // The offsets API in ONE persistent launch over the length-sorted list, on
 // the G = 16 table image (staged once).  Waves [0, kSmallWaves) of every
@@ -48,10 +49,25 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     // pieces)
     const uint32_t np = P.part ? min(ws[kWsPieces], kPieceBudget) : 0u;
     // With no large buffers at all, every wave walks the small classes.
+    // Otherwise (round 3) as few waves per workgroup as keep each one at <=
+    // kSmallRounds rounds of the small classes (64 class-0 or 16 class-1
+    // buffers a round), at most kSmallWaves: a small-class round is latency-
+    // bound, a wave taken from the large pool costs bandwidth.  Measured
+    // (profiles/r03/small_waves/): the 1 GiB WAL scan (12 rounds on one wave)
+    // 61.0 -> 63.2 % with 1 wave instead of 4, C2 (24 rounds on 3) 73.8 ->
+    // 74.2-75.4 %, C4 (23 on 4) best with 4 (-1.2 % with 2, -1.8 % with 1).
 #if LVK_SMALL_ALL
-    const uint32_t nsmall = n23 ? kSmallWaves : kWaves;
+    uint32_t nsmall = n23 ? kSmallWaves : kWaves;
 #else
-    constexpr uint32_t nsmall = kSmallWaves;
+    uint32_t nsmall = kSmallWaves;
+#endif
+#if LVK_SMALL_ADAPT
+    if (n23) {
+        const uint64_t rounds = (cls[4] + 63ull) / 64u + (cls[5] + 15ull) / 16u;
+        const uint64_t per = static_cast<uint64_t>(kSmallRounds) * gridDim.x;
+        const uint64_t ns = (rounds + per - 1) / per;
+        nsmall = static_cast<uint32_t>(ns < 1 ? 1 : (ns > kSmallWaves ? kSmallWaves : ns));
+    }
 #endif
     if (wave < nsmall) {
         const uint64_t sw = blockIdx.x * nsmall + wave, nsw = grid * nsmall;

@@ -45,7 +45,10 @@
     defined(LVK_WAL_LANE_COUNT) || \
     defined(LVK_EXP_WAL_NOCACHE) || \
     defined(LVK_EXP_WAL_NOCOUNT) || \
-    defined(LVK_WAL_LEAN_HOP))
+    defined(LVK_WAL_LEAN_HOP) || \
+    defined(LVK_SMALL_ADAPT) || \
+    defined(LVK_SMALL_ROUNDS) || \
+    defined(LVK_WAL_ALIGNBYTE))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -153,4 +156,13 @@
 #endif
 #ifndef LVK_WAL_LEAN_HOP  // wal_hist: branch-free hop body (0: the branchy one with its timing knobs)
 #define LVK_WAL_LEAN_HOP 1
+#endif
+#ifndef LVK_SMALL_ADAPT  // class kernel: small-class waves per workgroup from the class counts (<= LVK_SMALL_WAVES)
+#define LVK_SMALL_ADAPT 1
+#endif
+#ifndef LVK_SMALL_ROUNDS
+#define LVK_SMALL_ROUNDS 26
+#endif
+#ifndef LVK_WAL_ALIGNBYTE  // wal_hist: header length/type from two dwords and v_alignbyte_b32
+#define LVK_WAL_ALIGNBYTE 1
 #endif

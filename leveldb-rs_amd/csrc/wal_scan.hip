@@ -165,6 +165,22 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         // timing variants put the header cache write and the key count at
         // ~6.5 us each of a 26.8 us wal_hist with the branchy body (the
         // wave-aggregated count before it: 31.8 us).
+#if LVK_WAL_ALIGNBYTE
+        // The framing needs header bytes 4..6 (length, type): the two aligned
+        // dwords around them and one v_alignbyte_b32.  The second dword holds
+        // one of those bytes only when they straddle; otherwise it is clamped
+        // to the log's last dword.
+        const uint64_t lastd = (size - 1) & ~3ull;  // the last aligned dword holding a log byte
+        uint32_t wlo = 0, whi = 0, wsh = 0;
+        auto issue = [&](uint32_t p, bool on) {
+            const uint64_t pa = start + p + 4u, a = pa & ~3ull;
+            wsh = static_cast<uint32_t>(pa & 3u);
+            if (on) {  // exec-masked: a load's cost grows with the lines its active lanes touch
+                wlo = *reinterpret_cast<const uint32_t *>(log + a);
+                whi = *reinterpret_cast<const uint32_t *>(log + (a + 4 < lastd ? a + 4 : lastd));
+            }
+        };
+#else
         const uint64_t lastw = (size - 1) & ~7ull;  // the last aligned word holding a log byte
         uint64_t wlo = 0, whi = 0;
         uint32_t wsh = 0;
@@ -176,13 +192,20 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
                 whi = *reinterpret_cast<const uint64_t *>(log + (a + 8 < lastw ? a + 8 : lastw));
             }
         };
+#endif
         issue(0, active);
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
                 touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
+#if LVK_WAL_ALIGNBYTE
+            const uint32_t hw = __builtin_amdgcn_alignbyte(whi, wlo, wsh);  // bytes pos + 4 .. pos + 7
+            const uint32_t len = hw & 0xffffu;
+            const uint32_t type = (hw >> 16) & 0xffu;
+#else
             const uint64_t hw = (wlo >> wsh) | ((whi << 1) << (63u - wsh));  // bytes pos .. pos + 7
             const uint32_t len = static_cast<uint32_t>(hw >> 32) & 0xffffu;
             const uint32_t type = static_cast<uint32_t>(hw >> 48) & 0xffu;
+#endif
             // log_reader.rs:312-331: BAD_LENGTH past the block, ZERO at a 0/0 header
             const bool ok = kWalHeader + len <= blen - pos && (type | len) != 0u;
             const uint32_t npos = pos + kWalHeader + len;
