@@ -84,20 +84,37 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t *h, uint32_t k, bool val
     return valid ? atomicAdd(&h[k], 1u) : 0u;
 }
 
+// Inclusive scan of v over a workgroup of W waves: wave scans (lane shuffles),
+// then the earlier waves' totals from `wt` (W LDS words); one barrier
+// (the caller's next write to `wt` must follow a barrier).  (Round 3: the
+// Hillis-Steele scans in LDS, two barriers per step, cost the sort and WAL
+// scatter passes ~1 us each.)
+template <uint32_t W>
+__device__ __forceinline__ uint32_t wg_incl_scan(uint32_t v, uint32_t *wt) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(inc, d);
+        if (lane >= d) inc += x;
+    }
+    if (lane == 63) wt[w] = inc;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < W; ++k) inc += k < w ? wt[k] : 0u;
+    return inc;
+}
+
 // Exclusive scan of the 256 key totals (one per thread of a 256-thread
-// workgroup) into sc[]; returns this thread's key start.
+// workgroup); sc[] gets the inclusive prefix; returns this thread's key start.
 __device__ __forceinline__ uint32_t key_starts(const uint32_t *ws, uint32_t *sc) {
+    __shared__ uint32_t wt[kKeys / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t mine = ws[kWsTot + t];
-    sc[t] = mine;
+    const uint32_t inc = wg_incl_scan<kKeys / 64>(mine, wt);
+    sc[t] = inc;
     __syncthreads();
-    for (uint32_t d = 1; d < kKeys; d <<= 1) {
-        const uint32_t x = t >= d ? sc[t - d] : 0u;
-        __syncthreads();
-        sc[t] += x;
-        __syncthreads();
-    }
-    return sc[t] - mine;
+    return inc - mine;
 }
 
 // Long-buffer split of the offsets API (verdict r01: a batch of a few long

@@ -327,30 +327,26 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
         *o.count = total;
         ws[kWsIdent] = 0u;  // the class kernel reads the sorted entries
     }
-    // this workgroup's first record in log order: the records of the ones before
+    // this workgroup's first record in log order: the records of the ones
+    // before (a wave reduction per wave, then the four wave sums)
     uint64_t pre = 0;
     for (uint32_t v = t; v < blockIdx.x; v += kSortThreads) pre += wgrec[v];
-    red[t] = pre;
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) pre += __shfl_xor(pre, k);
+    if (lane == 0) red[t >> 6] = pre;
     __syncthreads();
-    for (uint32_t d = kSortThreads / 2; d >= 1; d >>= 1) {
-        if (t < d) red[t] += red[t + d];
-        __syncthreads();
-    }
-    uint64_t run = red[0];
+    uint64_t run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSortThreads / 64; ++k) run += red[k];
     __syncthreads();
     if (over) return;  // block-uniform
+    __shared__ uint32_t wt[kSortThreads / 64];
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
     for (uint64_t b0 = lo; b0 < hi; b0 += kSortThreads) {  // block-uniform
         const uint64_t b = b0 + t;
         const uint32_t c = b < hi ? blkcnt[b] : 0u;
-        red[t] = c;  // inclusive scan of the block counts (Hillis-Steele in LDS)
+        red[t] = wg_incl_scan<kSortThreads / 64>(c, wt);  // inclusive prefix of the block counts
         __syncthreads();
-        for (uint32_t d = 1; d < kSortThreads; d <<= 1) {
-            const uint64_t x = t >= d ? red[t - d] : 0u;
-            __syncthreads();
-            red[t] += x;
-            __syncthreads();
-        }
         const uint32_t tot = static_cast<uint32_t>(red[kSortThreads - 1]);  // records of these blocks
         // The chunk's cached records, thread-parallel in log order: record q
         // belongs to the block j whose inclusive prefix first exceeds q (a
@@ -489,8 +485,12 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     uint64_t chunk = 0;
     const uint64_t wgs = wal_wgs(nblocks, &chunk);
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
-    hipLaunchKernelGGL(lvk::wal_hist, g, dim3(lvk::kWalHistThreads), 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk,
-                       hc);
+    hipLaunchKernelGGL(lvk::wal_hist, g, dim3(lvk::kWalHistThreads), 0, s, d_log, static_cast<uint64_t>(bytes), nblocks,
+                       chunk, M, wgrec, blk, hc);
+    // (Round 3: claiming each workgroup's key runs with device atomics in
+    // wal_hist instead of this column scan -- a memset of the totals first --
+    // measured 0.6 % slower: the memset launch and wal_hist's returning
+    // atomics cost more than sort_scan, profiles/r03/wal2/atomic_totals/.)
     launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgrec, s);
     lvk::WalOut o{d_hdr_off, d_info, d_count, cap};
     hipLaunchKernelGGL(lvk::wal_scatter, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws, M, wgrec,

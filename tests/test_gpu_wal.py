@@ -122,15 +122,19 @@ def _check_scan_device(log, cap=None, shift=0):
     cap = len(o) if cap is None else cap
     t = torch.frombuffer(bytes(shift) + bytes(log) + b"\0", dtype=torch.uint8).to("cuda:0")[shift:shift + len(log)]
     assert len(log) == 0 or t.data_ptr() % 16 == shift
-    hdr, crc, info, count = LW.scan_device(t, cap)
-    torch.cuda.synchronize()
-    assert lvgpu.last_kernel() == SORTED or len(log) == 0
-    n = int(count.item())
-    assert n == len(o)
-    if n <= cap:
-        assert hdr[:n].cpu().numpy().tolist() == o
-        assert info[:n].cpu().numpy().view(np.uint32).tolist() == i
-        assert crc[:n].cpu().numpy().view(np.uint32).tolist() == c
+    # twice: a fresh workspace, then one left dirty (0xff): the scan reads
+    # nothing of the workspace it did not write first
+    dirty = torch.full((LW.scan_workspace_bytes(len(log), cap),), 0xff, dtype=torch.uint8, device="cuda:0")
+    for ws in (None, dirty):
+        hdr, crc, info, count = LW.scan_device(t, cap, workspace=ws)
+        torch.cuda.synchronize()
+        assert lvgpu.last_kernel() == SORTED or len(log) == 0
+        n = int(count.item())
+        assert n == len(o)
+        if n <= cap:
+            assert hdr[:n].cpu().numpy().tolist() == o
+            assert info[:n].cpu().numpy().view(np.uint32).tolist() == i
+            assert crc[:n].cpu().numpy().view(np.uint32).tolist() == c
 
 
 @pytest.mark.parametrize("shift", [0, 8])
