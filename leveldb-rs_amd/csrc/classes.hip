@@ -337,6 +337,7 @@ template <bool SEEDED>
 struct FusedUnits {
     static constexpr uint32_t kFlush = 16;
     static constexpr bool kAlMid = true;
+    static constexpr bool kOneRound = LVK_FUSED_ONE_ROUND;  // sorted_stream: a one-round wave loads all batches at once
     uint32_t nbuf;  // buffers (<= kFusedMax); P.n = units
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;

@@ -48,7 +48,8 @@
     defined(LVK_WAL_LEAN_HOP) || \
     defined(LVK_SMALL_ADAPT) || \
     defined(LVK_SMALL_ROUNDS) || \
-    defined(LVK_WAL_ALIGNBYTE))
+    defined(LVK_WAL_ALIGNBYTE) || \
+    defined(LVK_FUSED_ONE_ROUND))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -165,4 +166,7 @@
 #endif
 #ifndef LVK_WAL_ALIGNBYTE  // wal_hist: header length/type from two dwords and v_alignbyte_b32
 #define LVK_WAL_ALIGNBYTE 1
+#endif
+#ifndef LVK_FUSED_ONE_ROUND  // fused small-batch walk: a wave's only round requests all its batches at once
+#define LVK_FUSED_ONE_ROUND 1
 #endif

@@ -396,6 +396,7 @@ template <bool SEEDED>
 struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
+    static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         if (!ident) return load_rgeo<SEEDED>(P, e);
@@ -480,6 +481,40 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     uint32_t a3p = 0;  // (AL) the last row's accumulator before the last batch
     uint32_t c = 0;  // rounds finished (output staging slot)
     uint32_t j = 0;
+    if constexpr (AL && Src::kOneRound && NU == 4) {
+        // The wave's only round, <= 4 batches (a batch of <= 1,024 one-round
+        // units: the pieces of a few long buffers): every batch's loads are
+        // requested at once -- one memory round trip for the walk instead of
+        // one per batch (the strided API's FUSE path does the same).  Missing
+        // batches reload batch 0 (branch-free: guarded loads made the
+        // compiler wait for each).
+        if (rhon >= nr && nbw <= 4u) {  // wave-uniform
+            uint4 v1[NU], v2[NU], v3[NU];
+            load_rbatch_al<NU>(q, nbw, nbw > 1u ? 1u : 0u, gl, v1, jfix);
+            load_rbatch_al<NU>(q, nbw, nbw > 2u ? 2u : 0u, gl, v2, jfix);
+            load_rbatch_al<NU>(q, nbw, nbw > 3u ? 3u : 0u, gl, v3, jfix);
+            tail = load_rtail(q, gl);
+            tr = src.trailer(q, gl);
+            auto fold_j = [&](uint4(&v)[NU], uint32_t jj) {
+                if (!LVK_EXP_NOFIX && jj <= jfix) fix_rbatch_al<NU>(q, nbw, jj, gl, v);
+                if (jj + 1u == nbw) a3p = jj == 0 ? 0u : A[NU - 1];
+                if (jj == 0)
+                    fold_first<W4K, NU, W4OFF>(v, A, L, pad);
+                else
+                    fold_batch<false, W4K, NU, W4OFF>(v, A, L);
+            };
+            fold_j(slot0, 0);
+            if (nbw > 1u) fold_j(v1, 1);
+            if (nbw > 2u) fold_j(v2, 2);
+            if (nbw > 3u) fold_j(v3, 3);
+            uint32_t X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
+            X = finish_raw(q, X, tail, gl, L);
+            if (gl == 0) src.stage(P, wave, grp, q, X, tr);
+            __builtin_amdgcn_wave_barrier();
+            src.flush(P, wave, lane, K);
+            return;
+        }
+    }
 
     auto step = [&](uint4(&cur)[NU], uint4(&nxt)[NU]) -> bool {
         const bool lastj = j + 1 == nbw;

@@ -45,6 +45,7 @@ struct TableUnits {
     // crc_out 32 slots of four words
     static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
+    static constexpr bool kOneRound = false;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
