@@ -432,27 +432,96 @@ __global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, 
     const uint32_t units = t < nbuf ? (m ? m : 1u) : 0u;
     uint32_t nunits = 0, nlong = 0;
     const uint32_t pre = block_exscan(units, sc + 32, &nunits);
-    const uint32_t lpre = block_exscan(m ? 1u : 0u, sc + 32, &nlong);
+    nunits = __builtin_amdgcn_readfirstlane(nunits);  // block-uniform (scalar registers)
+    const uint64_t grid = gridDim.x;
+    // One pass (every wave <= 1 round): workgroup b walks the contiguous units
+    // [b S, (b + 1) S), S = whole rounds, as many rounds per workgroup as the
+    // round-robin pool gave it; a split buffer whose pieces all fall in one
+    // workgroup's units is joined there, after the walk (no long record).
+    const bool onepass = LVK_FUSED_LOCAL_JOIN && nunits <= 4ull * kWaves * grid;
+    const uint32_t S = onepass ? 4u * static_cast<uint32_t>((nunits + 4ull * grid - 1) / (4ull * grid)) : 1u;
+    const bool local = onepass && m && pre / S == (pre + m - 1u) / S;
+    const uint32_t lpre = block_exscan(m && !local ? 1u : 0u, sc + 32, &nlong);
     if (t < nbuf) g_lds[kUnitPre + t] = pre | (p << 24);
     if (blockIdx.x == 0) {
-        if (m) longs[lpre] = make_uint4(t, pre, m, p);
+        if (m && !local) longs[lpre] = make_uint4(t, pre, m, p);
         if (t == 0) {
             ws[kWsLongs] = nlong;
             ws[kWsPieces] = nunits;
         }
     }
-    if (t == 0) g_lds[kPoolWord] = 0;
+    uint32_t *const lflag = g_lds + kFusedScratch + 48;  // a local buffer in the batch / in this workgroup
+    const uint32_t b0 = static_cast<uint32_t>(blockIdx.x) * S;
+    uint32_t pb = ceil_log2(total / 16384u);  // the batch's piece length (split_rule), for the join
+    pb = pb > kFusedPieceLog2 ? pb : kFusedPieceLog2;
+    pb = __builtin_amdgcn_readfirstlane(pb < 31u ? pb : 31u);
+    if (t == 0) {
+        g_lds[kPoolWord] = 0;
+        lflag[0] = 0;
+        lflag[1] = 0;
+    }
+    __syncthreads();
+    if (local) lflag[0] = 1u;
+    if (local && pre >= b0 && pre < b0 + S) lflag[1] = 1u;
     __syncthreads();
     const Lut L = make_lut(lane);
-    const uint64_t grid = gridDim.x;
-    auto pool = [&]() -> uint64_t {
+    Params Q = P;
+    Q.n = nunits;
+    // Without a local buffer, the round-robin pool (every workgroup busy);
+    // with one, workgroup b's static rounds.  (One instantiation of the walk
+    // for both: two spilled 33 VGPRs.)
+    const bool lmode = __builtin_amdgcn_readfirstlane(lflag[0]) != 0u;
+    constexpr uint64_t kNone = ~0ull >> 2;  // a round index past any list
+    const uint32_t rw = S / 4u;             // local mode: rounds of this workgroup
+    auto next = [&]() -> uint64_t {
+        if (lmode) return kNone;
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
         return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
     };
-    Params Q = P;
-    Q.n = nunits;
-    sorted_stream<16, FusedUnits<SEEDED>>(Q, FusedUnits<SEEDED>{nbuf}, lane, L, pool(), pool);
+    const uint64_t rho0 = lmode ? (w < rw ? blockIdx.x * static_cast<uint64_t>(rw) + w : kNone) : next();
+    sorted_stream<16, FusedUnits<SEEDED>>(Q, FusedUnits<SEEDED>{nbuf}, lane, L, rho0, next);
+    if (!lmode) return;
+    // ---- the in-workgroup join of this workgroup's local split buffers ----
+    __syncthreads();  // the walk is done: its piece registers are in g_ocrc
+    if (lflag[1] == 0) return;  // block-uniform
+    // Local buffers have m <= S <= 64 pieces, so their piece length is the
+    // batch's, 2^pb (a larger one comes from L > 4,096 x 2^pb, m > 2,048):
+    // stage Shift_{2^v P}, v < 6, over the image's region A (no longer read).
+    const uint32_t n4 = nunits;
+    stage_words(g_lds, P.tabs + pb * 1024u, 6u * 256u);
+    __syncthreads();
+    if (w != 0 || lane >= S) return;
+    // lane l: unit b0 + l (walked by wave l / 4 as group l % 4 of its one round)
+    const uint32_t u = b0 + lane;
+    if (u >= n4) return;
+    uint32_t i = 0;  // the last buffer whose first unit is <= u
+#pragma unroll
+    for (uint32_t step = kFusedMax / 2; step >= 1; step >>= 1)
+        if (i + step < nbuf && (g_lds[kUnitPre + i + step] & 0xffffffu) <= u) i += step;
+    const uint32_t wi = g_lds[kUnitPre + i];
+    const uint32_t pi = wi & 0xffffffu;
+    const uint32_t mi = (i + 1 < nbuf ? g_lds[kUnitPre + i + 1] & 0xffffffu : n4) - pi;
+    const bool mine = (wi >> 24) != 0 && pi / S == (pi + mi - 1u) / S;  // a local split buffer
+    const uint32_t k = u - pi;
+    // R_k (piece k > 0 was walked from ~0: remove Shift_P(~0)), shifted by
+    // (m - 1 - k) P bit by bit, then a segmented xor over the buffer's lanes
+    uint32_t R = g_ocrc[lane >> 2][lane & 3u] ^ (k ? tab_shift(g_lds, 0xffffffffu) : 0u);
+    const uint32_t j = mi - 1u - k;
+#pragma unroll
+    for (uint32_t v = 0; v < 6; ++v) {
+        const uint32_t sh = tab_shift(g_lds + v * 1024u, R);
+        R = (j >> v) & 1u ? sh : R;
+    }
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_down(R, d);
+        if (k % (2u * d) == 0 && k + d < mi) R ^= o;
+    }
+    if (mine && k == 0) {
+        const uint32_t crc = ~R;
+        P.out[i] = (P.flags & LV_CRC_MASK) ? mask_crc(crc) : crc;
+    }
 }
 
 }  // namespace lvk
@@ -490,6 +559,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
         const WsLayout lay = ws_layout(n);
         longs = reinterpret_cast<uint4 *>(ws_bytes + lay.longs);
         P.part = reinterpret_cast<uint32_t *>(ws_bytes + lay.part);
+        P.tabs = c.base_tabs;
         g_kernel = "crc32c_fused_small_kernel+combine_long_kernel";
         if (seed)
             hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<true>, dim3(static_cast<uint32_t>(c.cus)),
@@ -507,6 +577,9 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     // acquire around a per-buffer counter -- measured 64 x 16 MiB 200 -> 345
     // us and 1,024 x 64 KiB 41 -> 177 us: every fence writes back or
     // invalidates the XCD's whole L2; and C3 via offsets -2 % from spills.)
+    // (An empty launch -- C2 / C4, or a batch whose split buffers were all
+    // joined in the fused kernel -- takes 4-5 us in the trace, with 64
+    // workgroups as with one per CU: profiles/r03/fused_small/local_join/.)
     if (longs)
         hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(1024), 0, s, ws, longs,
                            P.part, c.base_mats, c.base_tabs, out, flags);

@@ -323,6 +323,7 @@ struct Params {
     uint64_t nplain;        // sorted walk: entries [nplain, n) are long-buffer pieces
     uint32_t *part;         // piece registers (long-buffer split of the offsets API)
     const uint32_t *mats;   // blocks kernel, FUSE: Shift_{j plen}, j < 2^pshift (32 column words each)
+    const uint32_t *tabs;   // fused small-batch kernel: the byte tables Shift_{2^i}, 1,024 words each
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of

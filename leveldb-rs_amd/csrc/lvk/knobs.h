@@ -49,7 +49,8 @@
     defined(LVK_SMALL_ADAPT) || \
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_WAL_ALIGNBYTE) || \
-    defined(LVK_FUSED_ONE_ROUND))
+    defined(LVK_FUSED_ONE_ROUND) || \
+    defined(LVK_FUSED_LOCAL_JOIN))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -169,4 +170,7 @@
 #endif
 #ifndef LVK_FUSED_ONE_ROUND  // fused small-batch walk: a wave's only round requests all its batches at once
 #define LVK_FUSED_ONE_ROUND 1
+#endif
+#ifndef LVK_FUSED_LOCAL_JOIN  // fused small-batch kernel: one-pass batches join workgroup-local split buffers in place
+#define LVK_FUSED_LOCAL_JOIN 1
 #endif

@@ -618,6 +618,15 @@ LONG_CASES = {
     "small_sort_2": [3 << 20, 17],
     "small_sort_1024": [(40000 + 977 * k) if k % 7 == 0 else (k * 37) % 3000 for k in range(1024)],
     "small_sort_1025": [(40000 + 977 * k) if k % 7 == 0 else (k * 37) % 3000 for k in range(1025)],
+    # round 3: one-pass batches of the fused small-batch kernel -- 256-B-aligned
+    # pieces take the one-round walk (all batches in flight), split buffers
+    # whose pieces fall in one workgroup are joined there (mixed: some do, some
+    # straddle two workgroups and go to combine_long_kernel)
+    "1024x64KiB_aligned": [65536] * 1024,
+    "16MiB_aligned": [16 << 20],
+    "local_mixed": [65536, 1000] * 512,
+    "local_mixed_aligned": [65536, 1000] * 512,
+    "local_ragged_aligned": [40000 + 4096 * (k % 5) for k in range(700)],
 }
 
 
@@ -632,10 +641,13 @@ def test_offsets_api_long_buffers(torch_dev, case, seeded):
     or not, masked."""
     torch, dev = torch_dev
     sizes = LONG_CASES[case]
-    offs, pos = [], 3
+    aligned = case.endswith("_aligned")
+    offs, pos = [], 0 if aligned else 3
     for sz in sizes:
         offs.append(pos)
         pos += sz + 5
+        if aligned:
+            pos = (pos + 255) & ~255
     arena = torch.empty(pos + 64, dtype=torch.uint8, device=dev)
     lvgpu.fill_splitmix(arena, 0, 0xB16 + len(sizes))
     rng = np.random.default_rng(len(sizes))
