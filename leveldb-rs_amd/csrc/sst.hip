@@ -97,6 +97,10 @@ struct TableUnits {
             if (lane >= nslots) return;
             const uint32_t bi = g_oidx[wave][lane];
             if (bi == 0xffffffffu || LVK_EXP_NOSEALWRITE) return;
+            if (LVK_EXP_SEAL_COMPACT) {  // timing only: the masked crc to a per-block word, no trailer
+                reinterpret_cast<uint32_t *>(P.base)[bi] = g_ocrc[wave][lane];  // overwrites the file's head
+                return;
+            }
             const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
             const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
             uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
