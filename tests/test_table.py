@@ -206,3 +206,25 @@ def test_gpu_table_one_launch_any_order(gpu):
     st = LT.verify_blocks(d, h)  # status only: the two-word staging
     assert lvgpu.last_kernel() == "sst_blocks_kernel<verify>"
     assert st.cpu().numpy().tolist() == [0] * len(handles)
+
+
+@pytest.mark.gpu
+def test_gpu_seal_without_types(gpu):
+    """Seal with no per-block types (all 0, the bench's case): the walk parks
+    each trailer's file offset instead of its block index, so the flush stores
+    without re-reading the handle.  Shuffled handles, sizes 0-70,000 B, a
+    count that is not a multiple of 4, and out-of-range handles (skipped)."""
+    import torch
+    from lvgpu import table as LT
+    rng = np.random.default_rng(74)
+    sizes = np.concatenate([rng.integers(0, 70000, size=120), rng.integers(4000, 4400, size=201), [0, 1, 2, 3, 4]])
+    file, handles = _make_table(rng, sizes.size, sizes=sizes)
+    perm = rng.permutation(len(handles))
+    handles = [handles[i] for i in perm]
+    want = _oracle_seal(file, handles, [0] * len(handles))
+    extra = [(len(file) - 4, 0), (2**63, 10), (0, 2**40)]
+    d = torch.frombuffer(bytearray(file), dtype=torch.uint8).to(gpu)
+    h = torch.tensor(np.array(handles + extra, dtype=np.uint64).view(np.int64), device=gpu)
+    LT.seal_blocks(d, h)
+    assert d.cpu().numpy().tobytes() == want
+    assert LT.verify_blocks(d, h).cpu().numpy().tolist() == [0] * len(handles) + [2, 2, 2]
