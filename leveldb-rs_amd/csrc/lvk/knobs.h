@@ -40,15 +40,8 @@
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_VERIFY_WIDE) || \
     defined(LVK_CLASS3_FIRST) || \
-    defined(LVK_EXP_WAL_MAXHOPS) || \
-    defined(LVK_EXP_WAL_NOBOOK) || \
-    defined(LVK_WAL_LANE_COUNT) || \
-    defined(LVK_EXP_WAL_NOCACHE) || \
-    defined(LVK_EXP_WAL_NOCOUNT) || \
-    defined(LVK_WAL_LEAN_HOP) || \
     defined(LVK_SMALL_ADAPT) || \
     defined(LVK_SMALL_ROUNDS) || \
-    defined(LVK_WAL_ALIGNBYTE) || \
     defined(LVK_FUSED_ONE_ROUND) || \
     defined(LVK_FUSED_LOCAL_JOIN) || \
     defined(LVK_EXP_SEAL_COMPACT))
@@ -142,32 +135,11 @@
 #ifndef LVK_CLASS3_FIRST  // class kernel: walk class 3 (> 32 KiB) before class 2 (SortedList::r3)
 #define LVK_CLASS3_FIRST 1
 #endif
-#ifndef LVK_EXP_WAL_MAXHOPS  // experiment (wrong framing): wal_hist stops every chain after this many hops (0: off)
-#define LVK_EXP_WAL_MAXHOPS 0
-#endif
-#ifndef LVK_EXP_WAL_NOBOOK  // experiment (wrong framing): wal_hist hops skip the histogram and header cache
-#define LVK_EXP_WAL_NOBOOK 0
-#endif
-#ifndef LVK_WAL_LANE_COUNT  // wal_hist: per-lane LDS atomic per record instead of the wave-aggregated count
-#define LVK_WAL_LANE_COUNT 1
-#endif
-#ifndef LVK_EXP_WAL_NOCACHE  // experiment (wrong framing): wal_hist hops skip the header cache write
-#define LVK_EXP_WAL_NOCACHE 0
-#endif
-#ifndef LVK_EXP_WAL_NOCOUNT  // experiment (wrong framing): wal_hist hops skip the sort key and histogram
-#define LVK_EXP_WAL_NOCOUNT 0
-#endif
-#ifndef LVK_WAL_LEAN_HOP  // wal_hist: branch-free hop body (0: the branchy one with its timing knobs)
-#define LVK_WAL_LEAN_HOP 1
-#endif
 #ifndef LVK_SMALL_ADAPT  // class kernel: small-class waves per workgroup from the class counts (<= LVK_SMALL_WAVES)
 #define LVK_SMALL_ADAPT 1
 #endif
 #ifndef LVK_SMALL_ROUNDS
 #define LVK_SMALL_ROUNDS 26
-#endif
-#ifndef LVK_WAL_ALIGNBYTE  // wal_hist: header length/type from two dwords and v_alignbyte_b32
-#define LVK_WAL_ALIGNBYTE 1
 #endif
 #ifndef LVK_FUSED_ONE_ROUND  // fused small-batch walk: a wave's only round requests all its batches at once
 #define LVK_FUSED_ONE_ROUND 1

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
                                                             uint32_t *__restrict__ blkcnt,
                                                             uint64_t *__restrict__ hcache) {
     constexpr uint32_t T = kWalHistThreads;
-    __shared__ uint32_t h[kKeys + 64];  // + a dummy bin per lane (LVK_WAL_LEAN_HOP)
+    __shared__ uint32_t h[kKeys + 64];  // + a dummy bin per lane (finished lanes)
     __shared__ uint64_t wsum[T / 64];
     __shared__ uint64_t hcl[T * (kHdrCache + 1)];  // per-thread header cache
     const uint32_t t = threadIdx.x, lane = t & 63u;
@@ -151,61 +151,42 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         // every hop's wait for its header load also wait for the previous
         // hop's store.
         uint64_t *const hl = hcl + t * (kHdrCache + 1);  // stride 65 words: lanes spread over the banks
-#if LVK_WAL_LEAN_HOP
-        // Branch-free hop: every lane runs every instruction of the loop body
-        // (no exec-mask branches) but the loads, the next header's loads are
-        // issued right after the decode, and this record's bookkeeping -- the
-        // header cache slot in LDS and a fire-and-forget LDS atomic on its sort
-        // key -- runs while they are in flight.  Finished lanes write their pad
-        // cache slot (64) and count into a per-lane dummy bin.  (Loads for
-        // every lane, finished ones rereading their last header from L2, made
-        // wal_hist 26.8 -> 41.8 us: a load instruction's cost grows with the
-        // lines its lanes touch.)  One wave per SIMD runs this loop alone, so the
+        // Branch-free hop (round 3): every lane runs every instruction of the
+        // loop body (no exec-mask branches) but the loads; the next header's
+        // loads are issued right after the decode, and this record's
+        // bookkeeping -- the header cache slot in LDS and a fire-and-forget
+        // LDS atomic on its sort key -- runs while they are in flight.
+        // Finished lanes write their pad cache slot (64) and count into a
+        // per-lane dummy bin.  One wave per SIMD runs this loop alone, so the
         // hop is bound by its instruction latency as much as by the load:
-        // timing variants put the header cache write and the key count at
-        // ~6.5 us each of a 26.8 us wal_hist with the branchy body (the
-        // wave-aggregated count before it: 31.8 us).
-#if LVK_WAL_ALIGNBYTE
+        // timing variants (profiles/r03/wal2/) put a chain walk with no
+        // bookkeeping at 16.4 us of the round-2 body's 31.4; the wave-
+        // aggregated count (ballots, a lane broadcast through LDS and its
+        // wait) -> one atomic per record took 31.8 -> 26.9 us, the branch-free
+        // body -> 22.8.  Loads for every lane (finished ones rereading their
+        // last header from L2) made it 41.8 us: a load instruction's cost
+        // grows with the lines its lanes touch, so the loads stay exec-masked.
         // The framing needs header bytes 4..6 (length, type): the two aligned
-        // dwords around them and one v_alignbyte_b32.  The second dword holds
-        // one of those bytes only when they straddle; otherwise it is clamped
-        // to the log's last dword.
+        // dwords around them and one v_alignbyte_b32 (+0.4 % over a 64-bit
+        // funnel shift).  The second dword holds one of those bytes only when
+        // they straddle; otherwise it is clamped to the log's last dword.
         const uint64_t lastd = (size - 1) & ~3ull;  // the last aligned dword holding a log byte
         uint32_t wlo = 0, whi = 0, wsh = 0;
         auto issue = [&](uint32_t p, bool on) {
             const uint64_t pa = start + p + 4u, a = pa & ~3ull;
             wsh = static_cast<uint32_t>(pa & 3u);
-            if (on) {  // exec-masked: a load's cost grows with the lines its active lanes touch
+            if (on) {
                 wlo = *reinterpret_cast<const uint32_t *>(log + a);
                 whi = *reinterpret_cast<const uint32_t *>(log + (a + 4 < lastd ? a + 4 : lastd));
             }
         };
-#else
-        const uint64_t lastw = (size - 1) & ~7ull;  // the last aligned word holding a log byte
-        uint64_t wlo = 0, whi = 0;
-        uint32_t wsh = 0;
-        auto issue = [&](uint32_t p, bool on) {  // bytes of the log's end word past it are never used
-            const uint64_t pa = start + p, a = pa & ~7ull;
-            wsh = static_cast<uint32_t>(pa & 7u) * 8u;
-            if (on) {  // exec-masked: a load's cost grows with the lines its active lanes touch
-                wlo = *reinterpret_cast<const uint64_t *>(log + (a < lastw ? a : lastw));
-                whi = *reinterpret_cast<const uint64_t *>(log + (a + 8 < lastw ? a + 8 : lastw));
-            }
-        };
-#endif
         issue(0, active);
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
                 touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
-#if LVK_WAL_ALIGNBYTE
             const uint32_t hw = __builtin_amdgcn_alignbyte(whi, wlo, wsh);  // bytes pos + 4 .. pos + 7
             const uint32_t len = hw & 0xffffu;
             const uint32_t type = (hw >> 16) & 0xffu;
-#else
-            const uint64_t hw = (wlo >> wsh) | ((whi << 1) << (63u - wsh));  // bytes pos .. pos + 7
-            const uint32_t len = static_cast<uint32_t>(hw >> 32) & 0xffffu;
-            const uint32_t type = static_cast<uint32_t>(hw >> 48) & 0xffu;
-#endif
             // log_reader.rs:312-331: BAD_LENGTH past the block, ZERO at a 0/0 header
             const bool ok = kWalHeader + len <= blen - pos && (type | len) != 0u;
             const uint32_t npos = pos + kWalHeader + len;
@@ -219,64 +200,6 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
             pos = npos;
             active = nact;
         }
-#else
-        // (round 3 second pass) Software-pipelined hop: decode the header, issue the NEXT header's
-        // loads, and only then do this record's bookkeeping (sort key, header
-        // cache, histogram ballots and LDS atomic) while that load is in
-        // flight (+0.9 % on the 1 GiB scan, profiles/r03/wal/ab_pipe.txt).
-        uint64_t wlo = 0, whi = 0;
-        uint32_t wsh = 0;
-        auto issue = [&](uint32_t p, bool on) {
-            const uint64_t pa = start + p, a = pa & ~7ull;
-            const uint64_t *w = reinterpret_cast<const uint64_t *>(log + a);
-            wsh = static_cast<uint32_t>(pa & 7u) * 8u;
-            wlo = on && a < size ? w[0] : 0ull;
-            whi = on && wsh && a + 8 < size ? w[1] : 0ull;
-        };
-        issue(0, active);
-        while (__any(active)) {  // wave-uniform: the longest chain of the wave
-            if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
-                touched ^= wal_touch(log, b0 + (t & ~63u), pos, blen, active, lane);
-            if (LVK_EXP_WAL_MAXHOPS && cnt >= LVK_EXP_WAL_MAXHOPS) active = false;  // timing only
-            const bool rec = active;
-            WalRec r{};
-            uint32_t npos = pos;
-            bool nact = false;
-            if (active) {
-                r = wal_decode(wsh ? (wlo >> wsh) | (whi << (64u - wsh)) : wlo, blen, pos);
-                npos = pos + kWalHeader + r.len;
-                nact = r.status == LV_WAL_REC_OK && blen - npos >= kWalHeader;
-            }
-            issue(npos, nact);
-            uint32_t key = 0;
-            if (LVK_EXP_WAL_NOBOOK) {  // timing only
-                cnt += rec ? 1u : 0u;
-                pos = npos;
-                active = nact;
-                continue;
-            }
-            if (rec) {
-                if (!LVK_EXP_WAL_NOCOUNT) key = sort_key(r.ulen);
-                if (!LVK_EXP_WAL_NOCACHE && cnt < kHdrCache) hl[cnt] = hdr_pack(pos, r.len, r.type);
-                ++cnt;
-            }
-            if (LVK_EXP_WAL_NOCOUNT) {  // timing only
-                pos = npos;
-                active = nact;
-                continue;
-            }
-#if LVK_WAL_LANE_COUNT
-            // one fire-and-forget LDS atomic per record (no return, no wait):
-            // the wave-aggregated count (ballots, a lane broadcast through
-            // LDS and its wait, branches) sat on every hop of the chain
-            if (rec) __hip_atomic_fetch_add(&h[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-            wave_count(h, key, rec, lane);
-#endif
-            pos = npos;
-            active = nact;
-        }
-#endif
         for (uint32_t c = 0; c < cnt && c < kHdrCache; ++c) hcache[b * kHdrCache + c] = hl[c];
         if (b < hi) blkcnt[b] = cnt;
         mine += cnt;
