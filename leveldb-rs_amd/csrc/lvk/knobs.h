@@ -27,6 +27,7 @@
     defined(LVK_MAX_PIECES) || \
     defined(LVK_SMALL_SORT) || \
     defined(LVK_WAL_TOUCH_HOPS) || \
+    defined(LVK_WAL_ADDR32) || \
     defined(LVK_PERMLANE) || \
     defined(LVK_AL_RT_LAST) || \
     defined(LVK_ZERO_PAGE) || \
@@ -149,4 +150,7 @@
 #endif
 #ifndef LVK_EXP_SEAL_COMPACT  // experiment (no trailers): the seal stores its masked crcs to a per-block array
 #define LVK_EXP_SEAL_COMPACT 0
+#endif
+#ifndef LVK_WAL_ADDR32  // wal_hist: header addresses as in-block 32-bit offsets
+#define LVK_WAL_ADDR32 1
 #endif
