@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         if constexpr (FUSE) fuse_pieces(P, fm, g_ocrc, lane, wave);  // the barrier is workgroup-wide
         return;
     }
-    if constexpr (PIECES && LVK_FUSE_INFLIGHT) {
+    if constexpr (PIECES) {
         // One round of <= 4 batches per group (pieces of <= 4 KiB): every
         // batch's loads in flight at once -- one memory round trip for the
         // whole walk, where the one-ahead prefetch of the loop below pays one

@@ -138,16 +138,11 @@ __global__ __launch_bounds__(1024) void combine_long_kernel(const uint32_t *__re
     // the counter counts every claim; records exist only below the budget
     const uint32_t nl = min(ws[kWsLongs], kPieceBudget / 2);
     if (blockIdx.x >= nl) return;  // block-uniform (every workgroup below nl has a wave or a record)
-#if !LVK_LONG_TABS
-    __shared__ uint32_t M[kBaseMats * 32];
-    for (uint32_t i = threadIdx.x; i < kBaseMats * 32; i += blockDim.x) M[i] = base[i];
-    __syncthreads();
-    auto shift = [&](uint32_t i, uint32_t v) { return gf2_apply(M + i * 32, v); };
-#else
     // Shift_{2^i}(v) by four byte-table lookups (tables in HBM, L2-resident:
     // 192 KiB for every i) instead of a staged 32-column matrix product
+    // (round 2: 1,024 x 64 KiB 36.8 -> 32.7 us, profiles/r02/long/ab_long_tables.txt)
+    (void)base;
     auto shift = [&](uint32_t i, uint32_t v) { return tab_shift(tabs + i * 1024u, v); };
-#endif
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
     for (uint32_t w = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); w < nl; w += nw) {

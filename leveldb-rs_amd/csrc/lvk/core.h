@@ -104,11 +104,7 @@ __device__ __forceinline__ uint32_t lds_word(uint32_t byte_addr) {
 // trees are most of the kernel's VALU work, and VALU issue (4 cycles per
 // wave64 instruction per SIMD) is one of the resources that bound it.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-#if LVK_XOR3
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-#else
-    return a ^ b ^ c;
-#endif
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // (round 1: 78.6 % with plain xors -> 80.5 %)
 }
 
 // XOR of the four Latin tables at byte offset OFF indexed by the bytes of s.

@@ -11,7 +11,6 @@
 #pragma once
 
 #if !defined(LVK_EXPERIMENT_BUILD) && ( \
-    defined(LVK_XOR3) || \
     defined(LVK_EXP_NOSHIFT) || \
     defined(LVK_EXP_NOFOLD) || \
     defined(LVK_STAGGER) || \
@@ -20,26 +19,18 @@
     defined(LVK_EXP_NOFIX) || \
     defined(LVK_EXP_NOMERGE) || \
     defined(LVK_EXP_NOSEALWRITE) || \
-    defined(LVK_FUSE_INFLIGHT) || \
     defined(LVK_AL_ROWS) || \
     defined(LVK_ALIGNED_ROWS) || \
     defined(LVK_IDENT) || \
     defined(LVK_MAX_PIECES) || \
     defined(LVK_SMALL_SORT) || \
     defined(LVK_WAL_TOUCH_HOPS) || \
-    defined(LVK_WAL_ADDR32) || \
-    defined(LVK_PERMLANE) || \
-    defined(LVK_AL_RT_LAST) || \
-    defined(LVK_ZERO_PAGE) || \
-    defined(LVK_SKIP_PAD) || \
     defined(LVK_SMALL_WAVES) || \
     defined(LVK_SMALL_ALL) || \
     defined(LVK_CLASS_STAGGER) || \
     defined(LVK_SEAL_FLUSH) || \
     defined(LVK_SST_ROWS) || \
-    defined(LVK_LONG_TABS) || \
     defined(LVK_SORT_MIN_WGS) || \
-    defined(LVK_VERIFY_WIDE) || \
     defined(LVK_CLASS3_FIRST) || \
     defined(LVK_SMALL_ADAPT) || \
     defined(LVK_SMALL_ROUNDS) || \
@@ -49,9 +40,6 @@
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
-#ifndef LVK_XOR3
-#define LVK_XOR3 1
-#endif
 #ifndef LVK_EXP_NOSHIFT
 #define LVK_EXP_NOSHIFT 0
 #endif
@@ -76,9 +64,6 @@
 #ifndef LVK_EXP_NOSEALWRITE  // the seal computes its trailers but stores none
 #define LVK_EXP_NOSEALWRITE 0
 #endif
-#ifndef LVK_FUSE_INFLIGHT
-#define LVK_FUSE_INFLIGHT 1
-#endif
 #ifndef LVK_AL_ROWS
 #define LVK_AL_ROWS 4
 #endif
@@ -97,18 +82,6 @@
 #ifndef LVK_WAL_TOUCH_HOPS
 #define LVK_WAL_TOUCH_HOPS 16
 #endif
-#ifndef LVK_PERMLANE
-#define LVK_PERMLANE 1
-#endif
-#ifndef LVK_AL_RT_LAST
-#define LVK_AL_RT_LAST 0
-#endif
-#ifndef LVK_ZERO_PAGE
-#define LVK_ZERO_PAGE 1
-#endif
-#ifndef LVK_SKIP_PAD
-#define LVK_SKIP_PAD 1
-#endif
 #ifndef LVK_SMALL_WAVES
 #define LVK_SMALL_WAVES 4
 #endif
@@ -124,14 +97,8 @@
 #ifndef LVK_SST_ROWS
 #define LVK_SST_ROWS 3
 #endif
-#ifndef LVK_LONG_TABS
-#define LVK_LONG_TABS 1
-#endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024
-#endif
-#ifndef LVK_VERIFY_WIDE  // experiment: the four-word verify staging even without crc_out
-#define LVK_VERIFY_WIDE 0
 #endif
 #ifndef LVK_CLASS3_FIRST  // class kernel: walk class 3 (> 32 KiB) before class 2 (SortedList::r3)
 #define LVK_CLASS3_FIRST 1
@@ -150,7 +117,4 @@
 #endif
 #ifndef LVK_EXP_SEAL_COMPACT  // experiment (no trailers): the seal stores its masked crcs to a per-block array
 #define LVK_EXP_SEAL_COMPACT 0
-#endif
-#ifndef LVK_WAL_ADDR32  // wal_hist: header addresses as in-block 32-bit offsets
-#define LVK_WAL_ADDR32 1
 #endif

@@ -33,16 +33,13 @@ struct RGeo {
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int from) {
     for (int m = from; m < 64; m <<= 1) {
         uint32_t o;
-#if LVK_PERMLANE
         if (m == 16) {
             const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
             o = r[0] > r[1] ? r[0] : r[1];
         } else if (m == 32) {
             const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
             o = r[0] > r[1] ? r[0] : r[1];
-        } else
-#endif
-        {
+        } else {
             o = __shfl_xor(v, m);
         }
         v = o > v ? o : v;
@@ -254,21 +251,15 @@ __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint
     const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) {
-        int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
-#if LVK_ZERO_PAGE
+        const int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
         const uint64_t ad = (d < 0 || d > dmax) ? reinterpret_cast<uint64_t>(&g_zero_granules[gl])
                                                 : ab + (static_cast<uint32_t>(d) << 4);
-#else
-        d = d > dmax ? dmax : d;  // upper clamp first: a buffer with no whole granule has dmax = -1
-        d = d < 0 ? 0 : d;
-        const uint64_t ad = ab + (static_cast<uint32_t>(d) << 4);
-#endif
-        v[i] = (LVK_AL_RT_LAST && i == NU - 1) ? load16_rt(ad) : load16(ad);
+        v[i] = load16(ad);
     }
 }
 
-// Head fix-up (as fix_rbatch) plus, without the zero block, the zero
-// granules outside the buffer.
+// Head fix-up (as fix_rbatch); granules outside [0, dmax] were loaded from
+// the zero block.
 template <uint32_t NU>
 __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
                                               uint4 (&v)[NU]) {
@@ -279,13 +270,7 @@ __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint3
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) {
         const int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
-#if LVK_ZERO_PAGE  // granules outside [0, dmax] were loaded from the zero block
         if ((d == 0 || (d == 1 && alow > 12)) && d <= dmax) {
-#else
-        if (d < 0 || d > dmax) {
-            v[i] = make_uint4(0, 0, 0, 0);
-        } else if (d == 0 || (d == 1 && alow > 12)) {
-#endif
             const int32_t rel = d * 16 - alow;
             v[i].x = fix_word(v[i].x, rel, s0);
             v[i].y = fix_word(v[i].y, rel + 4, s0);
@@ -353,7 +338,6 @@ __device__ __forceinline__ uint32_t round_pad(const RGeo &q, uint32_t nbw) {
 
 template <int W4K, uint32_t NU, uint32_t W4OFF>
 __device__ __forceinline__ void fold_first(const uint4 (&v)[NU], uint32_t (&A)[NU], const Lut &L, uint32_t pad) {
-#if LVK_SKIP_PAD
     if constexpr (NU >= 3) {
         if constexpr (NU == 4) {
             if (pad == 3) {
@@ -370,7 +354,6 @@ __device__ __forceinline__ void fold_first(const uint4 (&v)[NU], uint32_t (&A)[N
             return;
         }
     }
-#endif
     fold_batch<true, W4K, NU, W4OFF>(v, A, L);
 }
 
@@ -538,7 +521,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             }
         }
         if constexpr (AL) {
-            if (!LVK_EXP_NOFIX && (j <= jfix || (!LVK_ZERO_PAGE && lastj && rot))) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
+            if (!LVK_EXP_NOFIX && j <= jfix) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
         } else if (j <= jfix) {
             fix_rbatch<G>(q, nbw, j, gl, cur);
         }

@@ -165,7 +165,7 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
         lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
         g_kernel = "sst_blocks_kernel<seal>";
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P, c->image[kTableImage], u);
-    } else if (d_crc || LVK_VERIFY_WIDE) {
+    } else if (d_crc) {
         lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
         g_kernel = "sst_blocks_kernel<verify,crc>";
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, true>), grid, block, 0, s, P, c->image[kTableImage], u);

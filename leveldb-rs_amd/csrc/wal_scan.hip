@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         // dwords around them and one v_alignbyte_b32 (+0.4 % over a 64-bit
         // funnel shift).  The second dword holds one of those bytes only when
         // they straddle; otherwise it is clamped to the log's last dword.
-#if LVK_WAL_ADDR32  // in-block 32-bit offsets (blocks start 32 KiB-aligned in the 8-B-aligned log)
+        // in-block 32-bit offsets (blocks start 32 KiB-aligned in the 8-B-aligned log; +0.4 %)
         const uint8_t *const blk = log + start;
         const uint32_t lastd = (blen - 1u) & ~3u;  // the block's last aligned dword
         uint32_t wlo = 0, whi = 0, wsh = 0;
@@ -182,18 +182,6 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
                 whi = *reinterpret_cast<const uint32_t *>(blk + (ar + 4u < lastd ? ar + 4u : lastd));
             }
         };
-#else
-        const uint64_t lastd = (size - 1) & ~3ull;  // the last aligned dword holding a log byte
-        uint32_t wlo = 0, whi = 0, wsh = 0;
-        auto issue = [&](uint32_t p, bool on) {
-            const uint64_t pa = start + p + 4u, a = pa & ~3ull;
-            wsh = static_cast<uint32_t>(pa & 3u);
-            if (on) {
-                wlo = *reinterpret_cast<const uint32_t *>(log + a);
-                whi = *reinterpret_cast<const uint32_t *>(log + (a + 4 < lastd ? a + 4 : lastd));
-            }
-        };
-#endif
         issue(0, active);
         while (__any(active)) {  // wave-uniform: the longest chain of the wave
             if (LVK_WAL_TOUCH_HOPS && hops++ == LVK_WAL_TOUCH_HOPS)
