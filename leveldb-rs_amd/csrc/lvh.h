@@ -132,8 +132,8 @@ int piece_mats(DevCtx &c, uint64_t plen, const uint32_t **out);
 int piece_tabs(DevCtx &c, uint64_t plen, const uint32_t **out);
 
 // ---- launchers ----
-// The length sort of the offsets API (sort.hip): one launch for n <=
-// lvk::kSmallSort, else histogram + column scan + scatter.  Fills P.ent,
+// The length sort of the offsets API (sort.hip) for n > 1,024 buffers:
+// histogram + column scan + scatter.  Fills P.ent,
 // P.sseed and P.part (the long-buffer split's piece registers, or null when
 // splitting is off) and returns the long-buffer records (or null).
 uint4 *launch_sort(uint8_t *ws_bytes, const uint64_t *off, const uint32_t *len, const uint32_t *seed, uint64_t n,

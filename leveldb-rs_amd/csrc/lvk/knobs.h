@@ -23,7 +23,6 @@
     defined(LVK_ALIGNED_ROWS) || \
     defined(LVK_IDENT) || \
     defined(LVK_MAX_PIECES) || \
-    defined(LVK_SMALL_SORT) || \
     defined(LVK_WAL_TOUCH_HOPS) || \
     defined(LVK_SMALL_WAVES) || \
     defined(LVK_SMALL_ALL) || \
@@ -75,9 +74,6 @@
 #endif
 #ifndef LVK_MAX_PIECES  // pieces per split buffer (a lone 16 MiB buffer: 4,096 of 4 KiB, as the strided API cuts it)
 #define LVK_MAX_PIECES 4096
-#endif
-#ifndef LVK_SMALL_SORT
-#define LVK_SMALL_SORT 1
 #endif
 #ifndef LVK_WAL_TOUCH_HOPS
 #define LVK_WAL_TOUCH_HOPS 16

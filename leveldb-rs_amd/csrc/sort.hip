@@ -1,8 +1,9 @@
 // Length sort of the offsets API (lv_crc32c_batch_device): a counting sort
 // by (length class, batch count) into 16-B entries, with the long-buffer
-// split (pieces after the sorted entries), in one launch for small batches
-// (sort_small) or three (sort_hist, sort_scan, sort_scatter).  No host sync,
-// no device-scope fences.  Keys and workspace layout: lvk/sort.h.
+// split (pieces after the sorted entries), in three launches (sort_hist,
+// sort_scan, sort_scatter) for batches of > 1,024 buffers (smaller ones:
+// crc32c_fused_small_kernel, classes.hip).  No host sync, no device-scope
+// fences.  Keys and workspace layout: lvk/sort.h.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -265,164 +266,6 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
     }
 }
 
-// Small batches (n <= kSmallSort): the three passes in ONE launch.  Every
-// workgroup reads all n lengths (<= 4 KiB), so it knows the whole key
-// histogram, the histogram of the buffers before its chunk, the batch's
-// payload bytes and every buffer's split (pieces m_i, log2 piece length p_i);
-// piece slots and long-record indices are index-order prefix sums instead of
-// device-atomic claims, so no pass waits for another and no counter needs
-// zeroing.  (By construction every split fits: P >= batch bytes / 16,384,
-// so sum m <= 16,384 + n pieces and <= n long records, below the budgets.)  Each workgroup then claims its
-// chunk's sorted slots, and writes an equal share of ALL the piece slots (a
-// binary search over the LDS prefix finds a slot's buffer): a lone 16 MiB
-// buffer is 4,096 pieces, 16 dependent rounds for the one workgroup of its
-// chunk.  The chunks are the three-pass sort's; the grid is at least
-// kSmallSortWgs workgroups (the extra ones write pieces only).
-constexpr uint32_t kSmallSort = 4 * kSortThreads;  // buffers
-constexpr uint32_t kSmallSortWgs = 64;
-__global__ __launch_bounds__(kSortThreads) void sort_small(const uint64_t *__restrict__ off,
-                                                           const uint32_t *__restrict__ len, uint64_t n,
-                                                           uint64_t chunk, uint32_t *__restrict__ ws,
-                                                           uint4 *__restrict__ ent, const uint32_t *__restrict__ seed,
-                                                           uint32_t *__restrict__ sseed, uint4 *__restrict__ longs) {
-    __shared__ uint32_t hall[kKeys], hpre[kKeys], sc[kKeys];
-    __shared__ uint32_t mpre[kSmallSort + 1];  // exclusive prefix of m over buffer index (+ total)
-    __shared__ uint32_t lpre[kSmallSort + 1];  // exclusive prefix of split buffers
-    __shared__ uint32_t pp[kSmallSort];        // log2 piece length of a split buffer
-    __shared__ uint64_t red[kSortThreads / 64];
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    hall[t] = 0;
-    hpre[t] = 0;
-    uint32_t l[4];
-    uint64_t mine = 0;
-#pragma unroll
-    for (uint32_t e = 0; e < 4; ++e) {
-        const uint64_t i = e * kSortThreads + t;
-        l[e] = i < n ? len[i] : 0u;
-        mine += l[e];
-    }
-#pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) mine += __shfl_xor(mine, k);
-    if (lane == 0) red[w] = mine;
-    __syncthreads();
-    const uint64_t total = red[0] + red[1] + red[2] + red[3];
-    // histograms, splits and their index-order prefixes
-    uint32_t run_m = 0, run_l = 0;
-#pragma unroll
-    for (uint32_t e = 0; e < 4; ++e) {
-        const uint64_t i = e * kSortThreads + t;
-        const bool valid = i < n;
-        const uint32_t k = sort_key(l[e]);
-        wave_count(hall, k, valid, lane);
-        wave_count(hpre, k, valid && i < lo, lane);
-        uint32_t p = 0;
-        const uint32_t m = longs && valid ? split_rule(l[e], total, &p) : 0u;
-        // exclusive scans over t of m and (m > 0), plus the running totals of rows e' < e
-        uint32_t im = m, il = m > 0 ? 1u : 0u;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t xm = __shfl_up(im, d), xl = __shfl_up(il, d);
-            if (lane >= d) {
-                im += xm;
-                il += xl;
-            }
-        }
-        __syncthreads();  // red / sc reuse
-        if (lane == 63) {
-            sc[w] = im;
-            sc[4 + w] = il;
-        }
-        __syncthreads();
-        uint32_t bm = run_m, bl = run_l;
-        for (uint32_t v = 0; v < w; ++v) {
-            bm += sc[v];
-            bl += sc[4 + v];
-        }
-        pp[i] = p;  // i < kSmallSort: e < 4, t < kSortThreads
-        mpre[i] = bm + im - m;
-        lpre[i] = bl + il - (m > 0 ? 1u : 0u);
-        run_m += sc[0] + sc[1] + sc[2] + sc[3];
-        run_l += sc[4] + sc[5] + sc[6] + sc[7];
-    }
-    __syncthreads();
-    if (t == 0) {
-        mpre[kSmallSort] = run_m;
-        lpre[kSmallSort] = run_l;
-    }
-    // key starts (exclusive scan of the whole histogram) and this chunk's
-    // slots: a wave scan, then the earlier waves' totals (2 barriers, where a
-    // Hillis-Steele scan over LDS took 16)
-    static_assert(kKeys == kSortThreads, "one key per thread");
-    __shared__ uint32_t wtot[kSortThreads / 64];
-    const uint32_t mineh = hall[t];
-    uint32_t inc = mineh;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t x = __shfl_up(inc, d);
-        if (lane >= d) inc += x;
-    }
-    if (lane == 63) wtot[w] = inc;
-    __syncthreads();
-    for (uint32_t v = 0; v < w; ++v) inc += wtot[v];
-    sc[t] = inc;  // inclusive (block 0 reads other keys' entries below)
-    __syncthreads();
-    const uint32_t ks = inc - mineh;
-    const uint32_t kc = t / kBuckets, knb = kBuckets - 1 - t % kBuckets;
-    const bool ident_ok = mineh == static_cast<uint32_t>(n) && (kc <= 1 || (kc == 2 && (knb <= 16 || n >= 16384)));
-    const bool ident = __syncthreads_or(LVK_IDENT && ident_ok && run_l == 0);
-    if (blockIdx.x == 0) {
-        ws[kWsTot + t] = mineh;
-        if (t % kBuckets == 0) {  // per-class [start, count) for the CRC kernel
-            ws[kWsCls + kc] = ks;
-            ws[kWsCls + 4 + kc] = sc[t + kBuckets - 1] - ks;
-        }
-        if (t == 0) {
-            ws[kWsIdent] = ident ? 1u : 0u;
-            ws[kWsBytes] = static_cast<uint32_t>(total);
-            ws[kWsBytes + 1] = static_cast<uint32_t>(total >> 32);
-            ws[kWsPieces] = run_m;
-            ws[kWsLongs] = run_l;
-        }
-    }
-    if (ident) return;  // block-uniform
-    __syncthreads();  // sc (inclusive) is read above; hpre becomes the claim cursor
-    hpre[t] += ks;
-    __syncthreads();
-    // this chunk's buffers: sorted slots, entries, long records
-    const uint64_t i = lo + t;
-    const bool valid = i < hi;  // chunk <= 16 <= kSortThreads for n <= kSmallSort
-    const uint32_t L = valid ? len[i] : 0u;
-    const uint64_t o = valid ? off[i] : 0u;
-    const uint32_t sd = (seed && valid) ? seed[i] : 0u;
-    const uint32_t pos = wave_claim(hpre, sort_key(L), valid, lane);
-    const uint32_t m = valid ? mpre[i + 1] - mpre[i] : 0u;
-    if (valid) {
-        ent[pos] = make_uint4(static_cast<uint32_t>(o), static_cast<uint32_t>(o >> 32), m ? 0u : L,
-                              m ? 0xffffffffu : static_cast<uint32_t>(i));
-        if (seed) sseed[pos] = sd;
-        if (m) longs[lpre[i]] = make_uint4(static_cast<uint32_t>(i), mpre[i], m, pp[i]);
-    }
-    // this workgroup's share of the piece slots [0, run_m), one per thread
-    const uint32_t per = (run_m + gridDim.x - 1) / gridDim.x;
-    const uint32_t s0 = min(blockIdx.x * per, run_m), s1 = min(s0 + per, run_m);
-    for (uint32_t u = s0 + t; u < s1; u += kSortThreads) {
-        uint32_t j = 0, jh = static_cast<uint32_t>(n);  // the buffer holding slot u: the last j with mpre[j] <= u
-        while (jh - j > 1) {
-            const uint32_t mid = (j + jh) >> 1;
-            if (mpre[mid] <= u) j = mid; else jh = mid;
-        }
-        const uint32_t mj = mpre[j + 1] - mpre[j], k = u - mpre[j];
-        const uint32_t Lj = len[j];
-        const uint64_t P = 1ull << pp[j];
-        const uint64_t first = Lj - (static_cast<uint64_t>(mj) - 1) * P;  // piece 0: [0, first)
-        const uint64_t a = off[j] + (k ? first + (k - 1) * P : 0);
-        ent[n + u] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
-                                static_cast<uint32_t>(k ? P : first), u | kPieceFlag);
-        if (seed) sseed[n + u] = k ? 0u : seed[j];
-    }
-}
-
 }  // namespace lvk
 
 namespace lvh {
@@ -481,14 +324,11 @@ uint4 *launch_sort(uint8_t *ws_bytes, const uint64_t *off, const uint32_t *len, 
     // whose buffer indices reach the piece flag bit
     uint4 *longs = n < lvk::kPieceFlag ? reinterpret_cast<uint4 *>(ws_bytes + lay.longs) : nullptr;
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
-    if (n <= lvk::kSmallSort && LVK_SMALL_SORT) {  // one launch (sort_small)
-        const dim3 gs(static_cast<uint32_t>(std::max<uint64_t>(wgs, lvk::kSmallSortWgs)));
-        hipLaunchKernelGGL(lvk::sort_small, gs, b, 0, s, off, len, n, chunk, ws, ent, seed, sseed, longs);
-    } else {
-        hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M, ws, wgb);
-        launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgb, s);
-        hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed, longs);
-    }
+    // (n > 1,024: smaller batches take crc32c_fused_small_kernel, which
+    // retired round 2's one-launch sort_small in round 3)
+    hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M, ws, wgb);
+    launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgb, s);
+    hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed, longs);
     P->ent = ent;
     P->sseed = seed ? sseed : nullptr;
     P->part = longs ? part : nullptr;

@@ -614,7 +614,7 @@ LONG_CASES = {
     "1024x64KiB": [65536] * 1024,
     "300_ragged": [(1 << 20) + 13 * k for k in range(300)] + [100] * 50,
     "few_long_many_short": [9 << 20, 3 << 20] + [200 + k % 3000 for k in range(20000)],
-    # the one-launch sort (sort_small, n <= 1,024) and the three-pass sort just past it
+    # the fused small-batch kernel (n <= 1,024, no sort) and the three-pass sort just past it
     "small_sort_2": [3 << 20, 17],
     "small_sort_1024": [(40000 + 977 * k) if k % 7 == 0 else (k * 37) % 3000 for k in range(1024)],
     "small_sort_1025": [(40000 + 977 * k) if k % 7 == 0 else (k * 37) % 3000 for k in range(1025)],
@@ -690,7 +690,7 @@ def test_offsets_api_one_key_batches(torch_dev, n, size, seeded):
 
 @pytest.mark.parametrize("trial", range(6))
 def test_offsets_api_small_batches_random(torch_dev, trial):
-    """Random batches of 1-1,024 buffers (the one-launch sort, sort_small):
+    """Random batches of 1-1,024 buffers (the fused small-batch kernel, no sort):
     lengths 0 to 3 MiB with a few long ones split into pieces, overlapping
     and unaligned offsets, seeded or not, masked or not -- every CRC against
     the oracle."""
