@@ -132,7 +132,6 @@ constexpr uint32_t kWgJoinMin = 65;  // pieces: one workgroup per buffer from he
 __global__ __launch_bounds__(1024) void combine_long_kernel(const uint32_t *__restrict__ ws,
                                                            const uint4 *__restrict__ longs,
                                                            const uint32_t *__restrict__ part,
-                                                           const uint32_t *__restrict__ base,
                                                            const uint32_t *__restrict__ tabs,
                                                            uint32_t *__restrict__ out, uint32_t flags) {
     // the counter counts every claim; records exist only below the budget
@@ -141,7 +140,6 @@ __global__ __launch_bounds__(1024) void combine_long_kernel(const uint32_t *__re
     // Shift_{2^i}(v) by four byte-table lookups (tables in HBM, L2-resident:
     // 192 KiB for every i) instead of a staged 32-column matrix product
     // (round 2: 1,024 x 64 KiB 36.8 -> 32.7 us, profiles/r02/long/ab_long_tables.txt)
-    (void)base;
     auto shift = [&](uint32_t i, uint32_t v) { return tab_shift(tabs + i * 1024u, v); };
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
@@ -577,7 +575,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     // workgroups as with one per CU: profiles/r03/fused_small/local_join/.)
     if (longs)
         hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(1024), 0, s, ws, longs,
-                           P.part, c.base_mats, c.base_tabs, out, flags);
+                           P.part, c.base_tabs, out, flags);
     return 0;
 }
 

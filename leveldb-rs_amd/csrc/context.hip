@@ -169,15 +169,6 @@ int current_ctx(DevCtx **out) {
             LV_HIP(hipMemcpy(c.image[i], im.data(), im.size() * 4, hipMemcpyHostToDevice));
         }
         {
-            std::vector<uint32_t> bm(lvk::kBaseMats * 32);
-            lvgpu::Gf2Mat m = lvgpu::shift_matrix(1);
-            for (uint32_t i = 0; i < lvk::kBaseMats; ++i) {
-                for (int j = 0; j < 32; ++j) bm[i * 32 + j] = m.col[j];
-                m = m.then(m);  // Shift_{2^(i+1)}
-            }
-            LV_HIP(hipMalloc(&c.base_mats, bm.size() * 4));
-            counters().allocs++;
-            LV_HIP(hipMemcpy(c.base_mats, bm.data(), bm.size() * 4, hipMemcpyHostToDevice));
             std::vector<uint32_t> bt(lvk::kBaseMats * 1024);
             for (uint32_t i = 0; i < lvk::kBaseMats; ++i) {
                 uint32_t S[4][256];

@@ -61,8 +61,7 @@ struct DevCtx {
     bool ready = false;
     int cus = 0;
     uint4 *image[kImages] = {};  // per G (kGs), then the table image
-    uint32_t *base_mats = nullptr;  // Shift_{2^i}, i < lvk::kBaseMats (combine_long_kernel)
-    uint32_t *base_tabs = nullptr;  // the same shifts as byte tables (4 x 256 words each)
+    uint32_t *base_tabs = nullptr;  // Shift_{2^i}, i < lvk::kBaseMats, as byte tables (4 x 256 words each)
     std::mutex ws_m;  // guards the map (entries are never erased)
     std::map<hipStream_t, std::unique_ptr<StreamWs>> ws;
     // long-block split: Shift matrices per piece length (immutable once built)

@@ -653,7 +653,7 @@ __device__ __forceinline__ void stage_words(uint32_t *dst, const uint32_t *src, 
     for (; i < n4; i += b) d4[i] = s4[i];
 }
 
-// base: Shift_{2^i} bytes, i < kBaseMats, as GF(2) matrices (32 columns).
+// The base shifts Shift_{2^i} bytes, i < kBaseMats, as byte tables (DevCtx::base_tabs).
 constexpr uint32_t kBaseMats = 48;
 
 // Rows per batch of the table walk.  A 4,097-4,352-B unit at a byte-packed
