@@ -72,8 +72,9 @@ def main():
     lg = load(os.path.join(out, "long.json"))
     if lg:
         for r in lg["results"]:
-            rows.append(f"| {r['blocks']} x {r['block_bytes']} B | strided {r['strided']['us_avg']} us, offsets "
-                        f"{r['offsets']['us_avg']} us | - | {r['offsets']['kernels']} |")
+            med = lambda a: f" (median {r[a]['us_p50']})" if "us_p50" in r[a] else ""
+            rows.append(f"| {r['blocks']} x {r['block_bytes']} B | strided {r['strided']['us_avg']} us{med('strided')}, "
+                        f"offsets {r['offsets']['us_avg']} us{med('offsets')} | - | {r['offsets']['kernels']} |")
     g = load(os.path.join(out, "gloo2.json"))
     if g:
         rows.append(f"| N=2 launcher (gloo, 1 GPU) | {g['value']} GiB/s | - | n_gpus {g['n_gpus']}, world {g['world_size']}, "
