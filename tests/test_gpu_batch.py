@@ -716,6 +716,41 @@ def test_offsets_api_small_batches_random(torch_dev, trial):
     assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:10]]
 
 
+@pytest.mark.parametrize("trial", range(8))
+def test_offsets_api_one_pass_local_joins_random(torch_dev, trial):
+    """Random one-pass batches of the fused small-batch kernel built so that
+    split buffers of 3-64 pieces mix with short ones: some buffers' pieces
+    fall in one workgroup's units (joined in the kernel), some straddle two
+    (combine_long_kernel), at 256-B-aligned or odd offsets, seeded or not,
+    masked or not -- every CRC against the oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(2000 + trial)
+    n = int(rng.integers(2, 1025))
+    lens = rng.integers(0, 4000, size=n)
+    split = rng.random(n) < 0.3
+    lens[split] = rng.integers(16385, 64 * 4096, size=int(split.sum()))  # 4 KiB pieces: 5-64 each
+    aligned = trial % 2 == 0
+    offs, pos = [], 0
+    for sz in lens:
+        offs.append(pos)
+        pos += int(sz) + int(rng.integers(0, 9))
+        if aligned:
+            pos = (pos + 255) & ~255
+    arena = torch.empty(pos + 64, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, 0x10CA1 + trial)
+    seeded, masked = trial % 4 < 2, trial % 3 == 0
+    seeds = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    o = torch.tensor(offs, dtype=torch.int64, device=dev)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out = lvgpu.batch(arena, o, ln, sd, masked=masked)
+    assert lvgpu.last_kernel() == "crc32c_fused_small_kernel+combine_long_kernel"
+    got = out.cpu().numpy().view(np.uint32)
+    want = oracle_batch(arena.cpu().numpy().tobytes(), np.array(offs, dtype=np.int64), lens, seeds, masked)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:10]]
+
+
 @pytest.mark.parametrize("n,L,distinct", [(300, 1 << 30, 5), (2000, 256 << 20, 7), (40000, (8 << 20) + 1, 3)])
 def test_offsets_api_huge_batch_piece_budget(torch_dev, n, L, distinct):
     """Batches of 300-500 GiB of heavily overlapping buffers: the
