@@ -227,39 +227,46 @@ __global__ __launch_bounds__(1024) void combine_long_kernel(const uint32_t *__re
         }
         const uint32_t lq = lc < 2u ? lc : 2u, Q = 1u << lq, ld = lc - lq, d = 1u << ld;
         const uint32_t pad = nt * c - m;
-        const uint32_t corr = tab_shift(tabs + p * 1024u, 0xffffffffu);  // Shift_P(~0): pieces k > 0 started from ~0
         __syncthreads();  // the previous record's readers of TW / PW are done
-        // padded piece x at PW[x + x / 64]: coalesced loads, conflict-free
-        // stores, and thread t's run t c + i reads 64 distinct banks for any
-        // power of two c <= 64.  (Named registers, not an array: arrays in
-        // these copy loops were placed in LDS by the compiler.)
+        // One memory round trip: the pieces' loads, then the tables' (staged
+        // in LDS), then the pieces' LDS stores; Shift_P(~0) from the staged
+        // table afterwards (loading it first cost a round trip of its own).
+        // Padded piece x at PW[x + x / 64], raw (the seed correction is
+        // applied on reading): coalesced loads, conflict-free stores, and
+        // thread t's run t c + i reads 64 distinct banks for any power of two
+        // c <= 64.  (Named registers, not an array: arrays in these copy
+        // loops were placed in LDS by the compiler.)
         auto ldp = [&](uint32_t x) {
-            const uint32_t kp = x - pad;
             const bool on = x < nt * c && x >= pad;
-            const uint32_t v = part[r.y + (on ? kp : 0u)];
-            return on ? v ^ (kp ? corr : 0u) : 0u;
+            const uint32_t v = part[r.y + (on ? x - pad : 0u)];
+            return on ? v : 0u;
         };
         auto st = [&](uint32_t x, uint32_t v) {
             if (x < nt * c) PW[x + (x >> 6)] = v;
         };
-        for (uint32_t x0 = t; x0 < nt * c; x0 += 8u * nt) {  // block-uniform
-            const uint32_t v0 = ldp(x0), v1 = ldp(x0 + nt), v2 = ldp(x0 + 2u * nt), v3 = ldp(x0 + 3u * nt);
-            const uint32_t v4 = ldp(x0 + 4u * nt), v5 = ldp(x0 + 5u * nt), v6 = ldp(x0 + 6u * nt), v7 = ldp(x0 + 7u * nt);
-            st(x0, v0);
-            st(x0 + nt, v1);
-            st(x0 + 2u * nt, v2);
-            st(x0 + 3u * nt, v3);
-            st(x0 + 4u * nt, v4);
-            st(x0 + 5u * nt, v5);
-            st(x0 + 6u * nt, v6);
-            st(x0 + 7u * nt, v7);
+        if (c == 4u) {  // block-uniform: m > 2,048, four pieces per thread
+            const uint32_t v0 = ldp(t), v1 = ldp(t + nt), v2 = ldp(t + 2u * nt), v3 = ldp(t + 3u * nt);
+            stage_words(TW, tabs + p * 1024u, (lc + 10u) * 256u);
+            st(t, v0);
+            st(t + nt, v1);
+            st(t + 2u * nt, v2);
+            st(t + 3u * nt, v3);
+        } else if (c == 2u) {
+            const uint32_t v0 = ldp(t), v1 = ldp(t + nt);
+            stage_words(TW, tabs + p * 1024u, (lc + 10u) * 256u);
+            st(t, v0);
+            st(t + nt, v1);
+        } else {
+            const uint32_t v0 = ldp(t);
+            stage_words(TW, tabs + p * 1024u, (lc + 10u) * 256u);
+            st(t, v0);
         }
-        stage_words(TW, tabs + p * 1024u, (lc + 10u) * 256u);
         __syncthreads();
+        const uint32_t corr = tab_shift(TW, 0xffffffffu);  // Shift_P(~0): pieces k > 0 started from ~0
         auto sh = [&](uint32_t v, uint32_t a) { return tab_shift(TW + v * 1024u, a); };
-        auto pw = [&](uint32_t i) {  // thread t's padded piece t c + i
+        auto pw = [&](uint32_t i) {  // thread t's padded piece t c + i (piece x - pad > 0: remove Shift_P(~0))
             const uint32_t x = t * c + i;
-            return PW[x + (x >> 6)];
+            return PW[x + (x >> 6)] ^ (x > pad ? corr : 0u);
         };
         uint32_t ch[4];
 #pragma unroll

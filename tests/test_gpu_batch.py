@@ -751,6 +751,73 @@ def test_offsets_api_one_pass_local_joins_random(torch_dev, trial):
     assert bad.size == 0, [(int(i), int(lens[i])) for i in bad[:10]]
 
 
+# Split buffers of the fused small-batch kernel that straddle workgroups
+# (joined by combine_long_kernel): one-pass batches (static per-workgroup
+# rounds) and the round-robin pool (> 16,384 units)
+STRADDLE_CASES = {
+    "static_16x1MiB": [1 << 20] * 16,  # 256 pieces each over 16 workgroups
+    "static_16MiB": [16 << 20],  # 4,096 pieces over every workgroup
+    "static_mixed": [3 << 20, 70000, 17, 0, 5 << 20] + [300] * 200,
+    "pool_1000x65KiB": [66560] * 1000,  # 17 pieces each: 17,000 units
+    "pool_big_and_small": [32 << 20] + [98305] * 1023,  # 4,096 + 1,023 x 13 pieces
+}
+
+
+@pytest.mark.parametrize("api", ["library_ws", "caller_ws"])
+@pytest.mark.parametrize("case", sorted(STRADDLE_CASES))
+def test_offsets_api_straddling_joins_repeat(torch_dev, case, api):
+    """Split buffers whose pieces straddle workgroups of the fused small-batch
+    kernel, joined by combine_long_kernel from the long records the fused
+    kernel wrote.  Three calls in a row on one stream -- seeded, unseeded
+    masked, seeded again, with a sorted-path call (n > 1,024) on the same
+    workspace in between -- through the library's workspace and a dirty
+    caller workspace, every CRC against the oracle each time (no state may
+    leak from one call into the next)."""
+    torch, dev = torch_dev
+    sizes = STRADDLE_CASES[case]
+    offs, pos = [], 3
+    for sz in sizes:
+        offs.append(pos)
+        pos += sz + 5
+    arena = torch.empty(pos + 64, dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, 0, 0xC0DE + len(sizes))
+    host = arena.cpu().numpy().tobytes()
+    rng = np.random.default_rng(len(sizes))
+    seeds = rng.integers(0, 2**32, size=len(sizes), dtype=np.uint64).astype(np.uint32)
+    o = torch.tensor(offs, dtype=torch.int64, device=dev)
+    ln = torch.tensor(sizes, dtype=torch.int32, device=dev)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    want_s = oracle_batch(host, offs, sizes, seeds, False)
+    want_m = oracle_batch(host, offs, sizes, None, True)
+    ws = None
+    if api == "caller_ws":  # a dirty workspace
+        nb = max(lvgpu.workspace_bytes(len(sizes)), lvgpu.workspace_bytes(1100))
+        ws = torch.full((nb,), 0xff, dtype=torch.uint8, device=dev)
+
+    def run(seed, masked):
+        if ws is None:
+            out = lvgpu.batch(arena, o, ln, seed, masked=masked)
+        else:
+            out = lvgpu.batch_ws(arena, o, ln, ws, seed, masked=masked)
+        assert lvgpu.last_kernel() == "crc32c_fused_small_kernel+combine_long_kernel"
+        return out.cpu().numpy().view(np.uint32)
+
+    for k, (seed, masked, want) in enumerate([(sd, False, want_s), (None, True, want_m), (sd, False, want_s)]):
+        got = run(seed, masked)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (k, [(int(i), sizes[i]) for i in bad[:10]])
+        if k == 0:  # the sorted path on the same stream / workspace in between
+            o2 = torch.arange(1100, dtype=torch.int64, device=dev) * 50
+            l2 = torch.full((1100,), 40000, dtype=torch.int32, device=dev)
+            a2 = torch.empty(1100 * 50 + 40064, dtype=torch.uint8, device=dev)
+            lvgpu.fill_splitmix(a2, 0, 7)
+            if ws is None:
+                lvgpu.batch(a2, o2, l2)
+            else:
+                lvgpu.batch_ws(a2, o2, l2, ws)
+            assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel"
+
+
 @pytest.mark.parametrize("n,L,distinct", [(300, 1 << 30, 5), (2000, 256 << 20, 7), (40000, (8 << 20) + 1, 3)])
 def test_offsets_api_huge_batch_piece_budget(torch_dev, n, L, distinct):
     """Batches of 300-500 GiB of heavily overlapping buffers: the

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Few long buffers through the offsets API (sort split + class kernel +
 combine_long_kernel), for a kernel trace:
-    rocprofv3 --kernel-trace --stats -- python3 tools/long_offsets_probe.py [n] [bytes]
+    rocprofv3 --kernel-trace --stats -- python3 tools/long_offsets_probe.py [n] [bytes] [ws|lib]
+(ws: a caller workspace, lv_crc32c_batch_device_ws; lib: the library's).
 """
 import os
 import sys
@@ -24,13 +25,21 @@ def main():
     ln = torch.full((n,), bl, dtype=torch.int32, device=dev)
     ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
+    lib = len(sys.argv) > 3 and sys.argv[3] == "lib"
+
+    def call():
+        if lib:
+            lvgpu.batch(arena, o, ln, out=out)
+        else:
+            lvgpu.batch_ws(arena, o, ln, ws, out=out)
+
     for _ in range(400):
-        lvgpu.batch_ws(arena, o, ln, ws, out=out)
+        call()
     torch.cuda.synchronize()
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     st.record()
     for _ in range(50):
-        lvgpu.batch_ws(arena, o, ln, ws, out=out)
+        call()
     en.record()
     torch.cuda.synchronize()
     us = st.elapsed_time(en) * 1e3 / 50
