@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__rest
 // writes back the L2 and cost more than this whole pass).
 __global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__ M, uint32_t wgs,
                                                           uint32_t *__restrict__ ws, const uint64_t *__restrict__ wgb) {
-    __shared__ uint32_t part[64][16];
+    __shared__ uint32_t part[64][17];  // padded: the transposed scan reads a column
     __shared__ uint64_t bsum[kScanThreads / 64];
     if (blockIdx.x == 0) {  // the batch's payload bytes (sizes the long-buffer split's pieces)
         uint64_t b = threadIdx.x < wgs ? wgb[threadIdx.x] : 0u;
@@ -90,12 +90,18 @@ __global__ __launch_bounds__(kScanThreads) void sort_scan(uint32_t *__restrict__
     }
     part[sub][kl] = sum;
     __syncthreads();
-    for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive scan over sub
-        const uint32_t x = sub >= d ? part[sub - d][kl] : 0u;
-        __syncthreads();
-        part[sub][kl] += x;
-        __syncthreads();
+    {  // inclusive scan over sub: wave w scans key w's 64 row ranges, one per lane (two barriers
+       // instead of a 6-level Hillis-Steele over LDS with two barriers per level)
+        const uint32_t lane = t & 63u, w = t >> 6;
+        uint32_t x = part[lane][w];
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        part[lane][w] = x;
     }
+    __syncthreads();
     if (sub == 63) ws[kWsTot + k] = part[63][kl];
     uint32_t run = part[sub][kl] - sum;  // exclusive
 #pragma unroll
