@@ -97,6 +97,9 @@ def parse():
                         "the GPU; one JSON line with a roofline")
     p.add_argument("--as-rank", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--as-world", type=int, default=1, help=argparse.SUPPRESS)
+    p.add_argument("--c5-strong", default="auto", choices=["auto", "off"],
+                   help="auto: the default C3 line also times BASELINE configs[4] (64 GiB of 4 KiB blocks split "
+                        "across the ranks) as its `c5_strong` sub-record")
     p.add_argument("--traffic", default="auto", choices=["auto", "off"],
                    help="auto: measure roofline.traffic in a child rocprofv3 --pmc FETCH_SIZE pass")
     return p.parse_args()
@@ -219,7 +222,7 @@ def measure_traffic(args, shard_rank=0, shard_world=1):
     out = tempfile.mkdtemp(prefix="lvgpu_pmc_", dir="/tmp")
     cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
            sys.executable, os.path.abspath(__file__), "--steps", "10", "--warmup", "60", "--cpu-seconds", "0",
-           "--traffic", "off", "--no-settle", "--workload", args.workload, "--api", args.api,
+           "--traffic", "off", "--no-settle", "--c5-strong", "off", "--workload", args.workload, "--api", args.api,
            "--scaling", args.scaling,  # bytes per launch do not depend on the clock state: no settle
            "--as-rank", str(shard_rank), "--as-world", str(shard_world)]
     if args.group:
@@ -313,6 +316,67 @@ def cpu_baseline(torch, arena, off, ln, seconds, sample_bytes=64 << 20):
             "all_cores": {"value": round(agg_rate, 2), "unit": "GiB/s", "threads": len(th),
                           "note": "same sample split over the box's 16-thread CPU share, for context"},
             "host_cpu": _cpu_model(), "host_nproc": os.cpu_count()}, crcs, k
+
+
+def cpu_loop_baseline(pass_fn, n, seconds, sample, unit_scale=2**30, unit="GiB/s", threads=16):
+    """A CPU baseline for the SURVEY 8f lines: `pass_fn(lo, hi)` runs the
+    oracle's restatement of the reference loop over items [lo, hi) of the
+    same workload once and returns the bytes (or keys) it covered.  One
+    thread for `seconds` (the reference callers are single-threaded), then
+    the box's 16-thread CPU share over equal slices for seconds / 4, for
+    context (ctypes drops the GIL inside the C calls)."""
+    import threading
+
+    def run(lo, hi, secs, out):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            done += pass_fn(lo, hi)
+            el = time.perf_counter() - t0
+            if el >= secs:
+                break
+        out.append((done, el))
+    single = []
+    run(0, n, seconds, single)
+    bounds = [n * t // threads for t in range(threads + 1)]
+    agg, th = [], []
+    for t in range(threads):
+        if bounds[t + 1] > bounds[t]:
+            th.append(threading.Thread(target=run, args=(bounds[t], bounds[t + 1], max(1.0, seconds / 4), agg)))
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    d1, e1 = single[0]
+    return {"value": round(d1 / unit_scale / e1, 3), "unit": unit, "cores": 1, "kind": "port",
+            "sample": f"{sample}; {e1:.1f} s on 1 thread",
+            "all_cores": {"value": round(sum(d / e for d, e in agg) / unit_scale, 2), "unit": unit,
+                          "threads": len(th), "note": "same work split over the box's 16-thread CPU share"},
+            "host_cpu": _cpu_model(), "host_nproc": os.cpu_count()}
+
+
+def wal_cpu_baseline(log, seconds, expect_records):
+    """The reference reader's verify (log_reader.rs:271-364: 32 KiB reads,
+    header framing, unmask(header) == value([type || payload]) per record)
+    restated in C (oracle_wal_verify) over the same log, in GB/s of log.
+    Blocks are independent, so the 16-thread figure splits at block bounds."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    L = W.lib()
+    size = int(log.size)
+    base = log.ctypes.data
+    nblk = (size + 32767) // 32768
+    mm = ctypes.c_uint64()
+    ok = L.oracle_wal_verify(base, size, ctypes.byref(mm), None)
+    if ok != expect_records or mm.value:
+        raise SystemExit(f"WAL cpu baseline: oracle verify found {ok} good / {mm.value} bad records, "
+                         f"expected {expect_records}")
+
+    def one(lo, hi):
+        b0, b1 = lo * 32768, min(size, hi * 32768)
+        L.oracle_wal_verify(base + b0, b1 - b0, None, None)
+        return b1 - b0
+    return cpu_loop_baseline(one, nblk, seconds, f"the whole {size / 2**30:.2f} GiB log, oracle_wal_verify "
+                             f"(framing + CRC of log_reader.rs:271-364)", unit_scale=1e9, unit="GB/s")
 
 
 def e2e(args):
@@ -613,6 +677,8 @@ def wal_device_bench(args):
             if st == 0 and int(h_crc[k]) != W.value(raw[int(h_hdr[k]) + 6:int(h_hdr[k]) + 7 + ln]):
                 raise SystemExit("WAL device scan parity check failed")
         parity = "first 2000 records' CRCs vs oracle value()"
+    variant = os.environ.get("LVGPU_EXPERIMENT") == "1"
+    cpu = wal_cpu_baseline(log, args.cpu_seconds, cap) if args.cpu_seconds > 0 and not variant else None
     gbs = log.size / (avg * 1e-3) / 1e9
     res = {"metric": "device-resident WAL verify scan (framing + CRC of every record), HBM", "unit": "GB/s",
            "log_bytes": int(log.size), "records": int(sizes.size), "physical_records": cap,
@@ -620,7 +686,7 @@ def wal_device_bench(args):
                         "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_avg": round(avg, 4), "ms_p50": round(p50, 4),
                         "bytes_per_call": int(log.size),
                         "kernels": lvgpu.last_kernel()},
-           "api": "lv_wal_scan_device", "parity": parity,
+           "api": "lv_wal_scan_device", "parity": parity, "cpu_baseline": cpu,
            "timing": "HIP events around each call (all of its kernels), mean after settle + warmup",
            "data": "synthetic: Random(301).skewed(17) record sizes, random payload, encoded by lv_wal_encode_host"}
     print(json.dumps(res), flush=True)
@@ -668,6 +734,7 @@ def table_bench(args):
         if W.value(host[o:o + sz + 1]) != int(got[k]):
             raise SystemExit("table bench parity check failed")
     unit = int(sizes.sum()) + n  # contents + type byte per block
+    cpu = table_cpu_baseline(f, offs, sizes, unit, args.cpu_seconds) if args.cpu_seconds > 0 and not variant else None
     res = {"metric": "SSTable block trailer seal / verify, device-resident", "unit": "GiB/s",
            "blocks": n, "bytes_per_call": unit, "table_bytes": total,
            "seal": {"GiB_per_s": round(unit / 2**30 / (seal_avg * 1e-3), 1), "ms_avg": round(seal_avg, 4),
@@ -675,9 +742,68 @@ def table_bench(args):
            "verify": {"GiB_per_s": round(unit / 2**30 / (ver_avg * 1e-3), 1), "ms_avg": round(ver_avg, 4),
                       "ms_p50": round(ver_p50, 4), "frac_of_8TBps": round(unit / (ver_avg * 1e-3) / 8e12, 4)},
            "timing": "HIP events around each call (CRC batch + trailer kernels)", "parity": "first 2000 blocks vs oracle",
+           "cpu_baseline": cpu,
            "data": "synthetic splitmix64 contents in HBM"}
     print(json.dumps(res), flush=True)
     return res
+
+
+def table_cpu_baseline(f, offs, sizes, unit_bytes, seconds):
+    """Per-block trailer verify and seal on one host core over the same
+    (sealed) table copied to host memory: value(contents || type) against
+    unmask(LE32 after it) / mask(extend(value(contents), [type])) written
+    after the type (oracle_units_verify / oracle_units_seal), in GiB/s of
+    contents + type, like the GPU line."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    L = W.lib()
+    host = f.cpu().numpy().copy()
+    uo = offs.astype(np.uint64)
+    ul = (sizes + 1).astype(np.uint32)
+    co = (offs + sizes + 1).astype(np.uint64)
+    sz = sizes.astype(np.uint32)
+    n = int(offs.size)
+    if L.oracle_units_verify(host.ctypes.data, uo.ctypes.data, ul.ctypes.data, co.ctypes.data, n):
+        raise SystemExit("table cpu baseline: the oracle rejects a trailer the GPU sealed")
+    per_block = ul.astype(np.uint64)
+    csum = np.concatenate([[0], np.cumsum(per_block)])
+
+    def verify(lo, hi):
+        L.oracle_units_verify(host.ctypes.data, uo[lo:].ctypes.data, ul[lo:].ctypes.data, co[lo:].ctypes.data, hi - lo)
+        return int(csum[hi] - csum[lo])
+
+    def seal(lo, hi):
+        L.oracle_units_seal(host.ctypes.data, uo[lo:].ctypes.data, sz[lo:].ctypes.data, hi - lo)
+        return int(csum[hi] - csum[lo])
+    samp = f"the whole table ({unit_bytes / 2**30:.2f} GiB of contents + type, {n} blocks) in host memory"
+    v = cpu_loop_baseline(verify, n, seconds, samp + ", oracle_units_verify: unmask(trailer) == value(contents||type)")
+    s = cpu_loop_baseline(seal, n, seconds / 2, samp + ", oracle_units_seal: mask(extend(value(contents), type))")
+    if L.oracle_units_verify(host.ctypes.data, uo.ctypes.data, ul.ctypes.data, co.ctypes.data, n):
+        raise SystemExit("table cpu baseline: the oracle seal differs from the GPU seal")
+    return {"verify": v, "seal": s}
+
+
+def hash_cpu_baseline(arena, offs, lens, seconds):
+    """hash.rs:20-51 per key on one host core (oracle_hash_batch) over the
+    same byte-packed keys copied to host memory, in G keys/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import wal_oracle as W
+    L = W.lib()
+    host = arena.cpu().numpy()
+    n = int(offs.size)
+    outb = np.zeros(n, dtype=np.uint32)
+    keyb = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)])
+
+    def one(lo, hi):
+        L.oracle_hash_batch(host.ctypes.data, offs[lo:].ctypes.data, lens[lo:].ctypes.data, None,
+                            outb[lo:].ctypes.data, hi - lo)
+        return hi - lo
+    r = cpu_loop_baseline(one, n, seconds, f"all {n} keys ({int(keyb[-1]) / 1e9:.3f} GB) in host memory, "
+                          f"oracle_hash_batch (hash.rs:20-51, seed 0 as cache.rs:182/:395)", unit_scale=1e9, unit="Gkeys/s")
+    r["key_GB_per_s"] = round(r["value"] * float(keyb[-1]) / n, 3)
+    return r
 
 
 def hash_bench(args):
@@ -717,13 +843,20 @@ def hash_bench(args):
     L.oracle_hash_batch(host.ctypes.data, offs[:k].ctypes.data, lens[:k].ctypes.data, None, want.ctypes.data, k)
     if not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
         raise SystemExit("hash bench parity check failed")
+    cpu = hash_cpu_baseline(arena, offs, lens, args.cpu_seconds) if args.cpu_seconds > 0 else None
     moved = total + 16 * n  # key bytes + off/len + out
+    key_gbs = total / (avg * 1e-3) / 1e9
     res = {"metric": "batched leveldb hash() + cache shard, device-resident", "unit": "Gkeys/s",
            "keys": n, "key_bytes": total, "value": round(n / (avg * 1e-3) / 1e9, 3), "ms_avg": round(avg, 4),
-           "ms_p50": round(p50, 4), "hbm_GB_per_s": round(moved / (avg * 1e-3) / 1e9, 1),
-           "frac_of_8TBps": round(moved / (avg * 1e-3) / 8e12, 4),
-           "note": "hbm bytes = key bytes + 8 B offset + 4 B length + 4 B output per key",
-           "parity": "first 100000 keys vs oracle", "data": "synthetic splitmix64 keys in HBM"}
+           "ms_p50": round(p50, 4),
+           "roofline": {"bound": "hbm", "achieved": round(key_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(key_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": total,
+                        "algorithmic_bytes": "key bytes only (SURVEY 8d: metadata reported alongside, not counted)"},
+           "with_metadata": {"bytes_per_launch": moved, "GB_per_s": round(moved / (avg * 1e-3) / 1e9, 1),
+                             "frac_of_8TBps": round(moved / (avg * 1e-3) / 8e12, 4),
+                             "note": "key bytes + 8 B offset + 4 B length read + 4 B output written per key"},
+           "parity": "first 100000 keys vs oracle", "cpu_baseline": cpu,
+           "data": "synthetic splitmix64 keys in HBM"}
     print(json.dumps(res), flush=True)
     return res
 
@@ -795,6 +928,7 @@ def wal_bench(args):
         nrec += 1
     t_read = time.perf_counter() - t0
     assert nrec == sizes.size, (nrec, sizes.size)
+    cpu = wal_cpu_baseline(out, args.cpu_seconds, int(o.size)) if args.cpu_seconds > 0 else None
     gib = out.size / 2**30
     print(json.dumps({"metric": "WAL group-commit encode and whole-log verify, host memory end to end",
                       "unit": "GiB/s of log", "log_bytes": int(out.size), "records": int(sizes.size),
@@ -805,6 +939,7 @@ def wal_bench(args):
                                "api": "lv_wal_scan_host (H2D + framing + CRC batch + D2H)"},
                       "reader_ms": round(t_read * 1e3, 1),
                       "reader_note": "host Reader replay via ctypes, one call per record (not a GPU figure)",
+                      "cpu_baseline": cpu,
                       "data": "synthetic: Random(301).skewed(17) record sizes, random payload"}), flush=True)
 
 
@@ -999,52 +1134,40 @@ def main():
         def step():
             lvgpu.batch(arena, off, ln, out=out, stream=stream, group=args.group)
 
-    settle_info = settle(torch, step, stream) if args.settle and n else None
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
     # Timed region (value): K steps between barrier + synchronize, nothing
-    # else on the stream, max over ranks (lvgpu.shard.timed_steps, the code
-    # the gloo test drives).  A timestamp event between launches costs ~3 %
-    # of the step time on MI355X, so the per-launch HIP events for
-    # roofline.achieved are taken in a second pass of the same K steps, right
-    # after, on the launch stream.
-    el_own, el = shard.timed_steps(
-        step, args.steps, torch.cuda.synchronize, dist,
-        lambda x: torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu"))
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    for s, e in evs:
-        s.record(stream)
-        step()
-        e.record(stream)
-    torch.cuda.synchronize()
-    kern_seq = [s.elapsed_time(e) for s, e in evs]
-    kern_ms = sorted(kern_seq)
-    if os.environ.get("LVGPU_BENCH_TRACE"):
-        print("per-launch ms:", " ".join(f"{x:.4f}" for x in kern_seq), file=sys.stderr)
+    # else on the stream, max over ranks of each rank's own time
+    # (lvgpu.shard.timed_steps, the code the gloo test drives).  A timestamp
+    # event between launches costs ~3 % of the step time on MI355X, so the
+    # per-launch HIP events for roofline.achieved are taken in a second pass
+    # of the same K steps, right after, on the launch stream.
+    head = timed_line(torch, step, stream, args, dist, backend, dev, chunk=20, active=n > 0)
+    kern_ms = head["kern_ms"]
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
-    # per-GPU figures: each rank's own timed-pass rate and kernel rate
-    props = torch.cuda.get_device_properties(dev)
-    own = {"rank": rank, "device": local,
-           "pci_bus_id": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
-           "gpu_uuid": str(getattr(props, "uuid", "")), "hostname": socket.gethostname(),
-           "payload_bytes": nbytes,
-           "GiB_per_s": round(nbytes * args.steps / 2**30 / el_own, 2),
-           "kernel_GB_per_s": round(nbytes / (kern_avg_ms * 1e-3) / 1e9, 1),
-           "frac_of_8TBps": round(nbytes / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    own = rank_record(torch, dev, rank, local, nbytes, args.steps, head["timing"], kern_avg_ms)
     per_rank = shard.gather_ranks(own, dist, world)
-    agg = shard.aggregate(per_rank, args.steps, el)
+    agg = shard.aggregate(per_rank, args.steps, head["timing"].own_max)
+    agg_b = shard.aggregate(per_rank, args.steps, head["timing"].barrier_max)
     value = agg["GiB_per_s"]
     achieved_gbs = nbytes / (kern_avg_ms * 1e-3) / 1e9
     kernel = lvgpu.last_kernel()
 
+    # BASELINE configs[4]: one global batch of 64 GiB of
+    # 4 KiB blocks split into contiguous rank ranges, timed the same way.  It
+    # rides in every default line (N = 1 and the driver's N > 1 lines) as the
+    # `c5_strong` sub-record; `value` stays C3 so SCALE N=1 equals BENCH.
+    c5 = None
+    if c5_wanted(args):
+        c5 = c5_strong_record(torch, lvgpu, args, dist, backend, dev, rank, local, world, shard_rank, shard_world)
+
+    # Everything after this point is rank 0's alone and outside every timed
+    # region: the other ranks leave the group first, so a slow CPU baseline or
+    # PMC pass can never hold them in a collective.
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
     result = None
     if rank == 0:
         cpu = None
-        # after the timed region: on rank 0 at every N (the other ranks wait
-        # at the closing barrier), over rank 0's own shard
         if args.cpu_seconds > 0:
             cpu, crcs, k = cpu_baseline(torch, arena, off, ln, args.cpu_seconds)
             got = out[:k].cpu().numpy().view("uint32")
@@ -1055,11 +1178,14 @@ def main():
             traffic, tsrc = measure_traffic(args, shard_rank, shard_world)
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
-            "world_size": dist.get_world_size() if dist else 1,
+            "world_size": world,
             "launcher": os.environ.get("LVGPU_LAUNCHER", "torch.distributed.run" if world > 1 else "single process"),
             "backend": backend if world > 1 else None,
             "distinct_devices": len({(r["hostname"], r["pci_bus_id"]) for r in per_rank}),
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(agg["ms_per_step"], 4),
+            "timing": TIMING_NOTE,
+            "value_barrier_inclusive": round(agg_b["GiB_per_s"], 2),
+            "ms_per_step_barrier_inclusive": round(agg_b["ms_per_step"], 4),
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 payload generated in HBM)",
             "config": {"workload": desc, "buffers_per_gpu": n, "bytes_per_gpu": nbytes,
@@ -1069,7 +1195,7 @@ def main():
                                        else f"dp{world} (one global batch split into contiguous rank ranges, "
                                             f"no collective)")},
             "hbm_peak_frac": round(value * 2**30 / world / 1e9 / HBM_PEAK_GBS, 4),
-            "settle": settle_info,
+            "settle": head["settle"],
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic), "traffic_source": tsrc,
@@ -1085,12 +1211,137 @@ def main():
             "cpu_baseline": cpu,
             "per_gpu": per_rank,
             "load_imbalance": round(agg["imbalance"], 4),
+            "c5_strong": c5,
         }
         print(json.dumps(result), flush=True)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
     return result
+
+
+TIMING_NOTE = ("value = bytes of all ranks x steps / max over ranks of each rank's own time (opening barrier + "
+               "sync -> K steps -> sync); *_barrier_inclusive: the same up to the end of the closing barrier")
+
+
+def timed_line(torch, step, stream, args, dist, backend, dev, chunk, active=True):
+    """settle -> warmup -> the K timed steps (shard.timed_steps) -> a second
+    pass of K steps with a HIP event pair around each launch on `stream`."""
+    from lvgpu import shard
+    settle_info = settle(torch, step, stream, chunk=chunk) if args.settle and active else None
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    tm = shard.timed_steps(
+        step, args.steps, torch.cuda.synchronize, dist,
+        lambda x: torch.tensor(x, dtype=torch.float64, device=dev if backend == "nccl" else "cpu"))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    for s, e in evs:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize()
+    kern_seq = [s.elapsed_time(e) for s, e in evs]
+    if os.environ.get("LVGPU_BENCH_TRACE"):
+        print("per-launch ms:", " ".join(f"{x:.4f}" for x in kern_seq), file=sys.stderr)
+    return {"settle": settle_info, "timing": tm, "kern_ms": sorted(kern_seq)}
+
+
+def rank_record(torch, dev, rank, local, nbytes, steps, tm, kern_avg_ms):
+    """This rank's entry of `per_gpu` (SURVEY 8e per-GPU figures)."""
+    props = torch.cuda.get_device_properties(dev)
+    return {"rank": rank, "device": local,
+            "pci_bus_id": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}",
+            "gpu_uuid": str(getattr(props, "uuid", "")), "hostname": socket.gethostname(),
+            "payload_bytes": nbytes,
+            "own_ms_per_step": round(tm.own / steps * 1e3, 4),
+            "GiB_per_s": round(nbytes * steps / 2**30 / tm.own, 2),
+            "kernel_GB_per_s": round(nbytes / (kern_avg_ms * 1e-3) / 1e9, 1),
+            "frac_of_8TBps": round(nbytes / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+C5_BLOCKS = 16777216  # BASELINE configs[4]: 64 GiB of 4 KiB blocks
+
+
+def c5_wanted(args):
+    """The C5 sub-record rides in the default line: the C3 weak headline over
+    the strided API, not a --as-rank replay (the PMC child) and not asked off."""
+    return (args.c5_strong == "auto" and args.workload == "c3" and args.scaling == "weak"
+            and args.api == "strided" and args.as_world == 1 and not args.blocks and not args.group)
+
+
+def c5_strong_record(torch, lvgpu, args, dist, backend, dev, rank, local, world, shard_rank, shard_world):
+    """BASELINE configs[4] at this world size: the global batch of C5_BLOCKS x
+    4 KiB split by RankShard.uniform, this rank's range generated at its
+    byte_lo of the one global splitmix arena, K steps timed like the headline.
+    A sample of every rank's blocks (its first and last 8) is checked against
+    the oracle over host bytes generated at the same global offsets."""
+    from lvgpu import shard
+    n_total = C5_BLOCKS
+    bl = 4096
+    sh = shard.RankShard.uniform(n_total, bl, shard_rank, shard_world)
+    arena = torch.empty(max(sh.byte_hi - sh.byte_lo, 1), dtype=torch.uint8, device=dev)
+    lvgpu.fill_splitmix(arena, sh.byte_lo, PAYLOAD_SEED)
+    out = torch.empty(max(sh.n, 1), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        if sh.n:
+            lvgpu.batch_strided(arena, bl, bl, sh.n, out=out, stream=stream)
+    # one launch is 10.6 ms at N = 1 (1.3 ms at N = 8): settle chunks of ~3 ms
+    chunk = max(1, min(20, round(0.003 / max(sh.payload_bytes / 6.5e12, 1e-6))))
+    line = timed_line(torch, step, stream, args, dist, backend, dev, chunk=chunk, active=sh.n > 0)
+    kern_ms = line["kern_ms"]
+    kern_avg = sum(kern_ms) / len(kern_ms)
+    rec = rank_record(torch, dev, rank, local, sh.payload_bytes, args.steps, line["timing"], kern_avg)
+    rec.update(blocks=[sh.lo, sh.hi], byte_lo=sh.byte_lo, parity_sample=c5_sample_check(arena, out, sh))
+    del arena
+    per = shard.gather_ranks(rec, dist, world)
+    agg = shard.aggregate(per, args.steps, line["timing"].own_max)
+    agg_b = shard.aggregate(per, args.steps, line["timing"].barrier_max)
+    if not all(r["parity_sample"] for r in per):
+        raise SystemExit("c5_strong parity sample failed on rank(s) "
+                         + str([r["rank"] for r in per if not r["parity_sample"]]))
+    return {"metric": "GiB/s device-resident batched CRC32C, BASELINE configs[4]: 64 GiB of 4 KiB blocks "
+                      "sharded across the GPUs (strong scaling)",
+            "value": round(agg["GiB_per_s"], 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(agg["ms_per_step"], 4),
+            "value_barrier_inclusive": round(agg_b["GiB_per_s"], 2),
+            "ms_per_step_barrier_inclusive": round(agg_b["ms_per_step"], 4),
+            "scaling": "strong", "timing": TIMING_NOTE,
+            "hbm_peak_frac": round(agg["GiB_per_s"] * 2**30 / world / 1e9 / HBM_PEAK_GBS, 4),
+            "config": {"workload": f"c5: global batch {n_total} x {bl} B ({n_total * bl / 2**30:.0f} GiB), "
+                                   f"RankShard.uniform contiguous rank ranges", "global_buffers": n_total,
+                       "global_bytes": n_total * bl, "api": "lv_crc32c_batch_strided",
+                       "parallelism": f"dp{world} (one global batch split into contiguous rank ranges, "
+                                      f"no collective)"},
+            "settle": line["settle"], "rank0_kernel_ms_avg": round(kern_avg, 4),
+            "per_gpu": per, "load_imbalance": round(agg["imbalance"], 4),
+            "parity": "every rank's first and last 8 blocks vs the oracle over host bytes generated at the "
+                      "same global offsets"}
+
+
+def c5_sample_check(arena, out, sh, k=8):
+    """The rank's first and last k blocks vs the oracle: the host bytes come
+    from the oracle's generator at the blocks' GLOBAL byte offsets, so this
+    also checks that the range was generated where it belongs in the arena."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    L = W.lib()
+    if sh.n == 0:
+        return True
+    got = out[:sh.n].cpu().numpy().view(np.uint32)
+    for lo in sorted({0, max(0, sh.n - k)}):
+        m = min(k, sh.n - lo)
+        bl = int(sh.lens[0])
+        buf = np.empty(m * bl, dtype=np.uint8)
+        L.oracle_fill_splitmix(buf.ctypes.data, sh.byte_lo + lo * bl, buf.size, PAYLOAD_SEED)
+        want = np.zeros(m, dtype=np.uint32)
+        ho = np.arange(m, dtype=np.uint64) * np.uint64(bl)  # named: the C call reads them
+        hl = np.full(m, bl, dtype=np.uint32)
+        L.oracle_batch(buf.ctypes.data, ho.ctypes.data, hl.ctypes.data, None, want.ctypes.data, m, 0)
+        if not np.array_equal(got[lo:lo + m], want):
+            return False
+    return True
 
 
 if __name__ == "__main__":

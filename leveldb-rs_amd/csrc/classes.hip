@@ -329,6 +329,7 @@ constexpr uint32_t kFusedMax = 1024;                   // buffers: one per threa
 // join of 16,384 pieces cost 9.2 us against ~5 for 4,096.
 constexpr uint32_t kFusedPieceLog2 = 12;
 constexpr uint32_t kFusedMaxPieces = kMaxPieces;
+static_assert(kFusedMaxPieces / 2 >= 64, "a local split buffer (<= 64 pieces) must be split at the batch's 2^pb");
 constexpr uint32_t kUnitPre = (kComb + 4 * 4096) / 4;  // LDS word: unit prefix | log2 piece << 24
 constexpr uint32_t kFusedScratch = kPoolWord + 1;      // LDS words: per-wave payload sums, scan totals
 static_assert(kFusedMax <= 1024 && kUnitPre + kFusedMax <= kPoolWord, "prefix fits combine table 4");
@@ -440,7 +441,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, 
     // workgroup's units is joined there, after the walk (no long record).
     const bool onepass = LVK_FUSED_LOCAL_JOIN && nunits <= 4ull * kWaves * grid;
     const uint32_t S = onepass ? 4u * static_cast<uint32_t>((nunits + 4ull * grid - 1) / (4ull * grid)) : 1u;
-    const bool local = onepass && m && pre / S == (pre + m - 1u) / S;
+    uint32_t pb = ceil_log2(total / 16384u);  // the batch's piece length (split_rule), for the join
+    pb = pb > kFusedPieceLog2 ? pb : kFusedPieceLog2;
+    pb = __builtin_amdgcn_readfirstlane(pb < 31u ? pb : 31u);
+    // The in-workgroup join stages only Shift_{2^v 2^pb}, v < 6: a buffer is
+    // local only if it was split at the batch's piece length 2^pb (split_rule's
+    // L / kMaxPieces term gives a larger one only to buffers of > kMaxPieces / 2
+    // pieces, which never fit one workgroup's <= 64 units; checked, not assumed).
+    const bool local = onepass && m && p == pb && pre / S == (pre + m - 1u) / S;
     const uint32_t lpre = block_exscan(m && !local ? 1u : 0u, sc + 32, &nlong);
     if (t < nbuf) g_lds[kUnitPre + t] = pre | (p << 24);
     if (blockIdx.x == 0) {
@@ -452,9 +460,6 @@ __global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, 
     }
     uint32_t *const lflag = g_lds + kFusedScratch + 48;  // a local buffer in the batch / in this workgroup
     const uint32_t b0 = static_cast<uint32_t>(blockIdx.x) * S;
-    uint32_t pb = ceil_log2(total / 16384u);  // the batch's piece length (split_rule), for the join
-    pb = pb > kFusedPieceLog2 ? pb : kFusedPieceLog2;
-    pb = __builtin_amdgcn_readfirstlane(pb < 31u ? pb : 31u);
     if (t == 0) {
         g_lds[kPoolWord] = 0;
         lflag[0] = 0;

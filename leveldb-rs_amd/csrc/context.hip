@@ -374,6 +374,16 @@ int host_upload(int device, const uint8_t *h, size_t bytes, size_t pad, HostPath
     return LV_OK;
 }
 
+int pinned_alloc(size_t bytes, uint8_t **p) {
+    *p = nullptr;
+    LV_HIP(hipHostMalloc(reinterpret_cast<void **>(p), bytes ? bytes : 1, hipHostMallocDefault));
+    return LV_OK;
+}
+
+void pinned_free(uint8_t *p) {
+    if (p) (void)hipHostFree(p);
+}
+
 void count_h2d(uint64_t bytes) { counters().h2d += bytes; }
 void count_d2h(uint64_t bytes) { counters().d2h += bytes; }
 

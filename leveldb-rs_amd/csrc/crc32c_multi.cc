@@ -13,9 +13,12 @@
 // every device ~the whole arena.  When the span exceeds kPackRatio x the
 // range's payload (plus kPackSlack), the range's buffers are packed into a
 // contiguous host copy first, in index order, so the device receives its
-// payload and nothing else; the pack is one host memcpy of the payload,
-// the same work the pageable upload's staging copy does anyway, done in
-// chunks of kPackChunk bytes so the copy never holds a range's whole payload.
+// payload and nothing else.  The pack goes straight into page-locked memory,
+// which the host upload DMAs as is: one host copy of the payload, the copy
+// the pageable upload's staging pass would have made (round 3 packed into
+// pageable memory, which the upload then staged again: two copies).  It is
+// done in chunks of kPackChunk bytes so the copy never holds a range's whole
+// payload; a chunk's pack is not overlapped with the previous chunk's upload.
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -50,13 +53,29 @@ constexpr double kPackRatio = 1.5;
 constexpr uint64_t kPackSlack = 1ull << 20;
 constexpr uint64_t kPackChunk = 256ull << 20;
 
+// Page-locked pack buffer, freed on every return path.
+struct Pinned {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    ~Pinned() { lvgpu_internal::pinned_free(p); }
+    int reserve(size_t bytes) {
+        if (cap >= bytes) return LV_OK;
+        lvgpu_internal::pinned_free(p);
+        p = nullptr;
+        cap = 0;
+        if (int rc = lvgpu_internal::pinned_alloc(bytes, &p)) return rc;
+        cap = bytes;
+        return LV_OK;
+    }
+};
+
 // Ships a scattered range in sub-ranges of at most kPackChunk payload bytes
 // (a lone longer buffer is its own sub-range and ships from the arena as
-// is), each packed into one reused host buffer: host memory stays bounded
-// by the chunk however large the range's payload is.
+// is), each packed into one reused page-locked buffer: host memory stays
+// bounded by the chunk however large the range's payload is.
 int packed_ranges(const uint8_t *arena, const uint64_t *off, const uint32_t *len, const uint32_t *seed,
                   uint32_t *out, size_t cnt, uint32_t flags, int device) {
-    std::vector<uint8_t> packed;
+    Pinned packed;
     std::vector<uint64_t> poff;
     for (size_t lo = 0; lo < cnt;) {
         if (len[lo] >= kPackChunk) {
@@ -70,15 +89,15 @@ int packed_ranges(const uint8_t *arena, const uint64_t *off, const uint32_t *len
         size_t hi = lo;
         uint64_t bytes = 0;
         while (hi < cnt && len[hi] < kPackChunk && bytes + len[hi] <= kPackChunk) bytes += len[hi++];
-        packed.resize(bytes ? bytes : 1);  // non-null even for all-empty buffers
+        if (int rc = packed.reserve(bytes ? bytes : 1)) return rc;  // non-null even for all-empty buffers
         poff.resize(hi - lo);
         uint64_t pos = 0;
         for (size_t k = lo; k < hi; ++k) {
-            std::memcpy(packed.data() + pos, arena + off[k], len[k]);
+            std::memcpy(packed.p + pos, arena + off[k], len[k]);
             poff[k - lo] = pos;
             pos += len[k];
         }
-        const int rc = lv_crc32c_batch_host(packed.data(), bytes, poff.data(), len + lo, seed ? seed + lo : nullptr,
+        const int rc = lv_crc32c_batch_host(packed.p, bytes, poff.data(), len + lo, seed ? seed + lo : nullptr,
                                             out + lo, hi - lo, flags, device);
         if (rc) return rc;
         lo = hi;

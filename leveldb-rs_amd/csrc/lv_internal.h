@@ -47,6 +47,10 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
                       const uint8_t *d_types, size_t n, uint32_t *d_status, uint32_t *d_crc, void *stream);
 // Cached device scratch buffer `slot` (0..1) of the HostPath's device, >= bytes.
 int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d);
+// Page-locked host memory (hipHostMalloc): a buffer host_upload DMAs in one
+// copy, with no staging pass.
+int pinned_alloc(size_t bytes, uint8_t **p);
+void pinned_free(uint8_t *p);
 // lv_device_counters bookkeeping for host copies made outside
 // context.hip (current device).
 void count_h2d(uint64_t bytes);

@@ -479,11 +479,11 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
         if (hip_err(hipMemcpyAsync(&count, d_count, 8, hipMemcpyDeviceToHost, s), "D2H") ||
             hip_err(hipStreamSynchronize(s), "sync"))
             break;
+        lvgpu_internal::count_d2h(8);  // counted once it has arrived, on every attempt
         if (count > cap) {  // more records than the guess: once more at the exact count
             cap = count;
             continue;
         }
-        lvgpu_internal::count_d2h(8 + count * 16);
         scan->off.resize(count);
         scan->crc.resize(count);
         scan->info.resize(count);
@@ -493,6 +493,7 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
              hip_err(hipMemcpyAsync(scan->info.data(), d_info, count * 4, hipMemcpyDeviceToHost, s), "D2H") ||
              hip_err(hipStreamSynchronize(s), "sync")))
             break;
+        lvgpu_internal::count_d2h(count * 16);  // after the copies succeeded
         return scan;
     }
     (void)hipStreamSynchronize(s);

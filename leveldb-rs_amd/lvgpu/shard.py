@@ -54,11 +54,30 @@ def world_from_env(requested: int, env=None):
 
 
 def free_port(host: str = "127.0.0.1") -> int:
+    """A port that was free a moment ago (tests that start their own groups).
+    `launch` does not use it: between the probe and rank 0 binding it another
+    process could take the port, so the launcher hosts the store itself."""
     s = socket.socket()
     s.bind((host, 0))
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+def host_store(master_addr: str = "127.0.0.1", nprocs: int = 1):
+    """A TCPStore server owned by the launching process, bound to a port the OS
+    picks (port 0) and kept open while the ranks run, so no other process can
+    take the port between its choice and the rendezvous.  The ranks reach it
+    as clients: `TORCHELASTIC_USE_AGENT_STORE=True` makes env:// rendezvous
+    connect every rank, rank 0 included, instead of rank 0 hosting
+    (torch/distributed/rendezvous.py `_create_c10d_store`), which is how
+    torchrun's agent runs it.  Only torch.distributed's store is imported:
+    nothing here touches a GPU."""
+    from datetime import timedelta
+
+    from torch.distributed import TCPStore
+    return TCPStore(master_addr, 0, nprocs, is_master=True, wait_for_workers=False,
+                    timeout=timedelta(seconds=900))
 
 
 def launch(argv, nprocs: int, env=None, master_addr: str = "127.0.0.1", master_port: int = None,
@@ -71,9 +90,14 @@ def launch(argv, nprocs: int, env=None, master_addr: str = "127.0.0.1", master_p
     over env:// exactly as under `python -m torch.distributed.run`.  The
     children inherit stdout/stderr: rank 0's JSON line is the job's output.
 
-    The parent never initialises a GPU (it imports neither torch nor the
-    library): the children are started as new processes, not forked from a
-    process holding a device context, and not exec'd over it.  If any child
+    Unless `master_port` is given, the parent hosts the rendezvous store on
+    an OS-chosen port for the life of the job (`host_store`), so the port
+    cannot be taken between its choice and rank 0's bind.
+
+    The parent never initialises a GPU (it imports torch.distributed's store,
+    never the library or a device): the children are started as new
+    processes, not forked from a process holding a device context, and not
+    exec'd over it.  If any child
     fails the others are terminated (by their own pid, never by pattern) and
     the first non-zero exit status is returned; 0 when all succeed."""
     if nprocs < 1:
@@ -81,7 +105,13 @@ def launch(argv, nprocs: int, env=None, master_addr: str = "127.0.0.1", master_p
     base = dict(os.environ if env is None else env)
     for k in RANK_ENV:
         base.pop(k, None)
-    port = master_port or free_port(master_addr)
+    store = None
+    if master_port:
+        port = master_port
+    else:
+        store = host_store(master_addr, nprocs)
+        port = store.port
+        base["TORCHELASTIC_USE_AGENT_STORE"] = "True"
     procs = []
     try:
         for r in range(nprocs):
@@ -119,6 +149,8 @@ def launch(argv, nprocs: int, env=None, master_addr: str = "127.0.0.1", master_p
             if p.poll() is None:
                 p.kill()
         raise
+    finally:
+        del store  # the ranks are gone: release the port
 
 
 def self_launch(script: str, args, nprocs: int) -> int:
@@ -200,11 +232,24 @@ class RankShard:
         return RankShard(rank, world, lo, hi, blo, bhi, start[lo:hi] - np.uint64(blo), ln[lo:hi].copy())
 
 
-def timed_steps(step, steps: int, sync, dist=None, max_tensor=None):
+@dataclass
+class Timing:
+    """One rank's timed region (seconds).  `own`: this rank's K steps, from
+    the opening barrier + sync to its closing sync; `own_max`: the max of
+    `own` over ranks -- the job's wall time (SURVEY 8e "wall time (max over
+    GPUs)"), which `value` divides by; `barrier_max`: the max over ranks of
+    the time to the end of the closing barrier (includes the barrier's
+    latency and the ranks' skew; reported beside it)."""
+    own: float
+    own_max: float
+    barrier_max: float
+
+
+def timed_steps(step, steps: int, sync, dist=None, max_tensor=None) -> Timing:
     """The timed region of the bench contract: barrier + sync, exactly `steps`
     calls of `step`, sync (this rank's own time), barrier, then the max over
-    ranks.  `max_tensor(x)` wraps a float for the all-reduce (a device tensor
-    under RCCL, a CPU one under gloo).  Returns (own_seconds, max_seconds)."""
+    ranks of both times in one all-reduce.  `max_tensor(list)` wraps floats
+    for the all-reduce (a device tensor under RCCL, a CPU one under gloo)."""
     if dist is not None:
         dist.barrier()
     sync()
@@ -216,11 +261,12 @@ def timed_steps(step, steps: int, sync, dist=None, max_tensor=None):
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
+    own_max = own
     if dist is not None:
-        t = max_tensor(el)
+        t = max_tensor([own, el])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    return own, el
+        own_max, el = (float(x) for x in t.tolist())
+    return Timing(own, own_max, el)
 
 
 def gather_ranks(own: dict, dist=None, world: int = 1):
@@ -235,7 +281,8 @@ def gather_ranks(own: dict, dist=None, world: int = 1):
 def aggregate(per_rank, steps: int, el_max: float) -> dict:
     """Whole-job figures from the gathered per-rank records (each carries
     'payload_bytes' per step): total bytes over all ranks / the max-over-ranks
-    time (the contract's `value`), plus the load balance."""
+    time (the contract's `value`; bench.py passes `Timing.own_max`), plus the
+    load balance."""
     total = sum(int(r["payload_bytes"]) for r in per_rank)
     shares = [int(r["payload_bytes"]) for r in per_rank]
     return {"total_bytes_per_step": total,

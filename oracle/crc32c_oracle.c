@@ -185,9 +185,14 @@ static inline uint64_t orc_splitmix64(uint64_t x) {
 void oracle_fill_splitmix(uint8_t *dst, uint64_t byte_begin, uint64_t nbytes, uint64_t seed) {
     uint64_t k = byte_begin;
     uint64_t end = byte_begin + nbytes;
-    while (k < end) {
-        uint64_t w = orc_splitmix64(seed ^ (k >> 3));
-        unsigned b = (unsigned)(k & 7);
-        for (; b < 8 && k < end; ++b, ++k) *dst++ = (uint8_t)(w >> (8 * b));
+    while (k < end && (k & 7)) {  /* head up to the next word boundary */
+        *dst++ = (uint8_t)(orc_splitmix64(seed ^ (k >> 3)) >> (8 * (k & 7)));
+        ++k;
     }
+    for (; k + 8 <= end; k += 8, dst += 8) {  /* whole words, little-endian */
+        uint64_t w = orc_splitmix64(seed ^ (k >> 3));
+        memcpy(dst, &w, 8);  /* x86-64 hosts only: little-endian */
+    }
+    for (; k < end; ++k)  /* tail */
+        *dst++ = (uint8_t)(orc_splitmix64(seed ^ (k >> 3)) >> (8 * (k & 7)));
 }

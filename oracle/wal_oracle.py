@@ -57,6 +57,14 @@ def lib():
         L.oracle_fill_splitmix.argtypes = [p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         L.oracle_table16.restype = None
         L.oracle_table16.argtypes = [p]
+        L.oracle_wal_verify.restype = ctypes.c_uint64  # verify_oracle.c
+        L.oracle_wal_verify.argtypes = [p, ctypes.c_uint64, p, p]
+        L.oracle_units_verify.restype = ctypes.c_uint64
+        L.oracle_units_verify.argtypes = [p, p, p, p, sz]
+        L.oracle_units_seal.restype = None
+        L.oracle_units_seal.argtypes = [p, p, p, sz]
+        L.oracle_hash_batch.restype = None  # hash_oracle.c
+        L.oracle_hash_batch.argtypes = [p] * 5 + [sz]
         _lib = L
     return _lib
 

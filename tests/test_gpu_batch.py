@@ -455,6 +455,62 @@ def test_full_size_c5_shard(torch_dev):
     assert np.array_equal(got, want)
 
 
+def _oracle_uniform_range(byte_lo, n, bl, seed, chunk_blocks=16384, threads=16):
+    """Oracle CRCs of n blocks of bl bytes whose bytes are the global splitmix
+    arena from byte_lo on, generated on the host chunk by chunk (16 threads:
+    the box's CPU share; ctypes drops the GIL inside the C calls)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import threading
+    L = W.lib()
+    want = np.zeros(n, dtype=np.uint32)
+    local = threading.local()
+    offs = np.arange(chunk_blocks, dtype=np.uint64) * bl
+    lens = np.full(chunk_blocks, bl, dtype=np.uint32)
+
+    def one(c0):
+        m = min(chunk_blocks, n - c0)
+        buf = getattr(local, "buf", None)
+        if buf is None:
+            buf = local.buf = np.empty(chunk_blocks * bl, dtype=np.uint8)
+        L.oracle_fill_splitmix(buf.ctypes.data, byte_lo + c0 * bl, m * bl, seed)
+        L.oracle_batch(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, want[c0:].ctypes.data, m, 0)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(one, range(0, n, chunk_blocks)))
+    return want
+
+
+def test_full_size_c5_strong_world8(torch_dev):
+    """BASELINE configs[4] at full size, as the driver's N = 8 line shards it:
+    the global batch of 16,777,216 x 4 KiB = 64 GiB split by RankShard.uniform
+    into 8 rank ranges, each generated at its byte_lo of the one global
+    splitmix arena (bench.build_shard / c5_strong_record) and checksummed by
+    the strided kernel, the ranges run one after another on this GPU.  Every
+    one of the 16,777,216 CRCs equals the oracle's over host bytes generated
+    at the same global offsets (so the ranges tile the arena where they
+    belong, and no rank checksums another's bytes)."""
+    torch, dev = torch_dev
+    import bench
+    from lvgpu.shard import RankShard
+    world, bl = 8, 4096
+    n_total = bench.C5_BLOCKS
+    got_all = np.zeros(n_total, dtype=np.uint32)
+    covered = 0
+    for r in range(world):
+        sh = RankShard.uniform(n_total, bl, r, world)
+        assert sh.lo == covered and sh.byte_lo == sh.lo * bl
+        arena = torch.empty(sh.byte_hi - sh.byte_lo, dtype=torch.uint8, device=dev)
+        lvgpu.fill_splitmix(arena, sh.byte_lo, bench.PAYLOAD_SEED)
+        out = lvgpu.batch_strided(arena, bl, bl, sh.n)
+        torch.cuda.synchronize()
+        got_all[sh.lo:sh.hi] = out.cpu().numpy().view(np.uint32)
+        covered = sh.hi
+        del arena, out
+    assert covered == n_total
+    want = _oracle_uniform_range(0, n_total, bl, bench.PAYLOAD_SEED)
+    bad = np.nonzero(got_all != want)[0]
+    assert bad.size == 0, f"{bad.size} CRCs differ, first blocks {bad[:8].tolist()}"
+
+
 def test_many_buffers_chunked_sort(torch_dev):
     """n above one sort pass's 1024 x 4096 buffers (4,194,304): 5,000,000
     byte-packed buffers of 0-300 B (every small class, chunked length sort),

@@ -119,3 +119,84 @@ def test_splitmix_fill_is_prefix_consistent(n):
     part = ctypes.create_string_buffer(n)
     L.oracle_fill_splitmix(part, 13, n, 99)
     assert part.raw[:n] == full.raw[13:13 + n]
+
+
+def _reader_counts(log: bytes):
+    """(passed, mismatched, bad length) physical records per the Python
+    restatement of log_reader.rs:271-364: scan_log walks every header; the
+    reference drops the rest of a block after a mismatch and counts an
+    overrun as "bad record length" only before EOF."""
+    offs, crcs, info = W.scan_log(log)
+    ok = mm = bl = 0
+    dropped = set()
+    last_block = (len(log) - 1) // W.BLOCK_SIZE if log else -1
+    short_tail = len(log) % W.BLOCK_SIZE != 0
+    for o, c, i in zip(offs, crcs, info):
+        blk = o // W.BLOCK_SIZE
+        if blk in dropped:
+            continue
+        status = (i >> 8) & 0xFF
+        if status == 1:
+            if not (blk == last_block and short_tail):
+                bl += 1
+            continue
+        if status == 2:
+            continue
+        if W.unmask(W.decode_fixed_32(log[o:o + 4])) == c:
+            ok += 1
+        else:
+            mm += 1
+            dropped.add(blk)
+    return ok, mm, bl
+
+
+def test_wal_verify_oracle_matches_reader_restatement():
+    """oracle_wal_verify (verify_oracle.c, the bench's WAL cpu_baseline) counts
+    what the Python reader restatement counts, on intact, corrupted and
+    truncated logs written by the oracle Writer."""
+    L = W.lib()
+    rnd = W.Random(301)
+    rng = random.Random(17)
+    seen_bl = seen_mm = False
+    for trial in range(12):
+        dest = bytearray()
+        w = W.Writer(dest)
+        for i in range(60):
+            w.add_record(W.random_skewed_string(i, rnd).encode())
+        log = bytearray(dest)
+        for _ in range(trial % 4):  # corrupt payload / header bytes
+            k = rng.randrange(len(log))
+            log[k] ^= 1 << rng.randrange(8)
+        if trial % 3 == 2:
+            log = log[:rng.randrange(len(log))]
+        if trial % 4 == 1 and len(log) > 3 * W.BLOCK_SIZE:  # a length that overruns block 1
+            log[W.BLOCK_SIZE + 5] = 0x7F
+        buf = (ctypes.c_uint8 * max(len(log), 1)).from_buffer_copy(bytes(log) or b"\0")
+        mm, bl = ctypes.c_uint64(), ctypes.c_uint64()
+        ok = L.oracle_wal_verify(ctypes.addressof(buf), len(log), ctypes.byref(mm), ctypes.byref(bl))
+        assert (ok, mm.value, bl.value) == _reader_counts(bytes(log)), trial
+        seen_bl = seen_bl or bl.value > 0
+        seen_mm = seen_mm or mm.value > 0
+    assert seen_bl and seen_mm
+
+
+def test_units_seal_and_verify_oracle():
+    """oracle_units_seal writes type || LE32(mask(crc32c(contents || type)))
+    and oracle_units_verify finds exactly the trailers that were damaged."""
+    import numpy as np
+    L = W.lib()
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(0, 5000, 200).astype(np.uint32)
+    offs = np.zeros(200, dtype=np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 5)
+    f = rng.integers(0, 256, int(offs[-1] + sizes[-1] + 5), dtype=np.uint8)
+    L.oracle_units_seal(f.ctypes.data, offs.ctypes.data, sizes.ctypes.data, 200)
+    for i in (0, 57, 199):
+        o, s = int(offs[i]), int(sizes[i])
+        assert W.decode_fixed_32(f[o + s + 1:o + s + 5].tobytes()) == W.mask(W.value(f[o:o + s + 1].tobytes()))
+    uo, ul, co = offs.copy(), sizes + 1, offs + sizes + 1
+    assert L.oracle_units_verify(f.ctypes.data, uo.ctypes.data, ul.ctypes.data, co.ctypes.data, 200) == 0
+    f[int(co[9])] ^= 4
+    f[int(uo[100])] ^= 1 if sizes[100] else 0
+    bad = 1 + (1 if sizes[100] else 0)
+    assert L.oracle_units_verify(f.ctypes.data, uo.ctypes.data, ul.ctypes.data, co.ctypes.data, 200) == bad

@@ -20,7 +20,7 @@ export TMPDIR=/tmp
 b() { local name=$1; shift; timeout -k 10 400 python3 bench.py "$@" > "$out/$name.json" 2> "$out/$name.err"; }
 p() { local name=$1; shift
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_$name" -o "$name" -- \
-         python3 "$root/bench.py" --steps 50 --warmup 100 --cpu-seconds 0 --traffic off "$@") > "$out/prof_$name.log" 2>&1 &&
+         python3 "$root/bench.py" --steps 50 --warmup 100 --cpu-seconds 0 --traffic off --c5-strong off "$@") > "$out/prof_$name.log" 2>&1 &&
       python3 tools/kstats_steady.py "$(ls "$out/prof_$name"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_${name}_steady.json" > /dev/null; }
 b default_driver --steps 20 --warmup 5 &&
 b default &&
@@ -41,7 +41,7 @@ p c3 &&
 p c2 --workload c2 --api offsets &&
 p c4 --workload c4 --api offsets &&
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_wal" -o wal -- \
-   python3 "$root/bench.py" --wal-device --steps 50 --warmup 20) > "$out/prof_wal.log" 2>&1 &&
+   python3 "$root/bench.py" --wal-device --steps 50 --warmup 20 --cpu-seconds 0) > "$out/prof_wal.log" 2>&1 &&
 python3 tools/kstats_steady.py "$(ls "$out/prof_wal"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_wal_steady.json" > /dev/null &&
 bash tools/prof_8f.sh "$out/prof8f" table hash &&
 bash tools/prof_long.sh "$out/prof_long" &&

@@ -15,12 +15,12 @@ export TMPDIR=/tmp
 declare -A ARGS=([table]="--table" [hash]="--hash" [wal]="--wal-device")
 k() { local name=$1; shift
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/k_$name" -o "$name" -- \
-          python3 "$root/bench.py" "$@" --steps 50 --warmup 20) > "$out/k_$name.log" 2>&1 &&
+          python3 "$root/bench.py" "$@" --steps 50 --warmup 20 --cpu-seconds 0) > "$out/k_$name.log" 2>&1 &&
       python3 tools/kstats_steady.py "$(ls "$out/k_$name"/*kernel_trace.csv | head -n 1)" 50 "$out/${name}_steady.json" > /dev/null &&
       cp "$(ls "$out/k_$name"/*kernel_stats.csv | head -n 1)" "$out/${name}_kernel_stats.csv"; }
 m() { local name=$1 ctr=$2; shift 2
       (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc "$ctr" --output-format csv -d "$root/$out/m_$name/$ctr" -o pmc -- \
-          python3 "$root/bench.py" "$@" --steps 5 --warmup 1 --no-settle) > "$out/m_${name}_$ctr.log" 2>&1; }
+          python3 "$root/bench.py" "$@" --steps 5 --warmup 1 --no-settle --cpu-seconds 0) > "$out/m_${name}_$ctr.log" 2>&1; }
 for w in $what; do
   a=${ARGS[$w]}
   k "$w" $a && m "$w" FETCH_SIZE $a && m "$w" WRITE_SIZE $a &&
