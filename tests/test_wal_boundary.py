@@ -62,3 +62,25 @@ def test_reader_checksum_off_ignores_crcs():
     rep2 = W.ReportCollector()
     r2 = LW.Reader(log, LW.Scan.from_arrays(o, [x ^ 1 for x in c], i), rep2, checksum=True)
     assert r2.read_record() is None and "checksum mismatch" in rep2.message
+
+
+def test_native_reader_replay_helper():
+    """tools/host_replay.c (bench.py --wal's native Reader loop) reads every
+    logical record of a log through the C ABI, from a scan built from the
+    oracle's CRCs (no GPU needed)."""
+    import ctypes
+    import os
+    import lvgpu.wal as LW
+    from conftest import ROOT
+    rnd = W.Random(301)
+    msgs = [W.random_skewed_string(i, rnd).encode() for i in range(200)]
+    log = _log(msgs)
+    o, c, i = W.scan_log(log)
+    s = LW.Scan.from_arrays(o, c, i)
+    R = ctypes.CDLL(os.path.join(ROOT, "leveldb-rs_amd", "lib", "libhostreplay.so"))
+    R.lv_replay_reader.restype = ctypes.c_double
+    R.lv_replay_reader.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    nr, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    t = R.lv_replay_reader(log, len(log), s._h, 2, ctypes.byref(nr), ctypes.byref(nb))
+    assert t >= 0 and nr.value == len(msgs) and nb.value == sum(len(m) for m in msgs)
