@@ -81,6 +81,27 @@ int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, con
                               const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
                               void *d_workspace, size_t workspace_bytes, void *stream);
 
+/* Host-side facts about a batch whose lengths live on the device.  The WAL
+ * group-commit writer and the SST sealer know their fragment / block lengths
+ * on the host; with them the library can leave out launches that the facts
+ * prove empty -- the long-buffer join when no buffer can be split, or when
+ * every split buffer of a uniform batch of <= 1,024 buffers is joined inside
+ * the walk -- which the device-only call cannot know without a host sync.
+ * The facts must be exact (max_len may be any upper bound of the lengths): a
+ * hint that understates them gives wrong CRCs. */
+typedef struct lv_batch_hint {
+    uint64_t total_bytes; /* sum of d_len[i] */
+    uint32_t max_len;     /* an upper bound of every d_len[i] */
+    uint32_t uniform;     /* nonzero: every d_len[i] == max_len (then total_bytes == n * max_len) */
+} lv_batch_hint;
+
+/* lv_crc32c_batch_device(_ws) with an optional hint (NULL = no hint) and an
+ * optional caller workspace (NULL = the library's per-stream workspace). */
+int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                                const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
+                                const lv_batch_hint *hint, void *d_workspace, size_t workspace_bytes,
+                                void *stream);
+
 /* Fixed-stride form for table blocks: buffer i is
  * d_base[i*stride .. i*stride + block_len).  Same semantics as above. */
 int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t block_len, size_t n,

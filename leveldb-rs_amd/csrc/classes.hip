@@ -542,10 +542,54 @@ void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const ui
                            0, s, P, c.image[2], ws);
 }
 
+// ---- the batch hint (lv_crc32c_batch_device_hint) ----
+// Host replica of lvk::split_rule (lvk/sort.h) for the offsets API's split,
+// pmin = 12 (4 KiB) and maxp = kMaxPieces in both the sort and the fused
+// small-batch path.  Whether a buffer splits is monotone in its length L:
+// with q_b = max(ceil_log2(total / 16,384), 12), L splits iff L > 16 KiB and
+// L > 2^(q_b + 1) (the L / kMaxPieces term only raises q where L / 2^q is
+// far above 2).
+static uint32_t host_ceil_log2(uint64_t x) { return x <= 1 ? 0u : 64u - static_cast<uint32_t>(__builtin_clzll(x - 1)); }
+
+static uint32_t host_split_rule(uint32_t L, uint64_t total, uint32_t *p) {
+    *p = 0;
+    if (L <= 16384u) return 0u;
+    uint32_t q = host_ceil_log2(total / 16384u);
+    const uint32_t pl = host_ceil_log2((static_cast<uint64_t>(L) + lvk::kMaxPieces - 1) / lvk::kMaxPieces);
+    q = std::max(q, pl);
+    q = std::max(q, 12u);
+    q = std::min(q, 31u);
+    if (L <= (2ull << q)) return 0u;
+    *p = q;
+    return static_cast<uint32_t>((L + (1ull << q) - 1) >> q);
+}
+
+// Does the batch need combine_long_kernel?  No when no buffer of at most
+// max_len bytes can split in a batch of `total` bytes; for a uniform batch of
+// <= kFusedMax buffers also when every split buffer's pieces fall in one
+// workgroup's static rounds of the fused kernel, which joins those itself
+// (the same unit layout crc32c_fused_small_kernel computes on the device).
+static bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
+    uint32_t p = 0;
+    if (host_split_rule(h.max_len, h.total_bytes, &p) == 0) return false;  // monotone: nothing splits
+    if (!h.uniform || n > lvk::kFusedMax || !LVK_FUSED_LOCAL_JOIN) return true;
+    const uint32_t m = host_split_rule(h.max_len, h.total_bytes, &p);
+    const uint64_t nunits = n * m;
+    const uint64_t grid = cus;
+    if (nunits > 4ull * lvk::kWaves * grid) return true;  // not one pass: the pool, no local joins
+    const uint64_t S = 4ull * ((nunits + 4ull * grid - 1) / (4ull * grid));
+    uint32_t pb = host_ceil_log2(h.total_bytes / 16384u);
+    pb = std::min(std::max(pb, lvk::kFusedPieceLog2), 31u);
+    if (p != pb) return true;
+    for (uint64_t t = 0; t < n; ++t)
+        if ((t * m) / S != (t * m + m - 1) / S) return true;  // straddles two workgroups
+    return false;
+}
+
 // Length-sorted launch of the offsets API, no host sync: the sort (one or
 // three launches), the persistent class kernel, the long-buffer join.
 int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s) {
+                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join = true) {
     uint32_t *ws = reinterpret_cast<uint32_t *>(ws_bytes);
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(arena);
@@ -565,7 +609,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
         longs = reinterpret_cast<uint4 *>(ws_bytes + lay.longs);
         P.part = reinterpret_cast<uint32_t *>(ws_bytes + lay.part);
         P.tabs = c.base_tabs;
-        g_kernel = "crc32c_fused_small_kernel+combine_long_kernel";
+        g_kernel = join ? "crc32c_fused_small_kernel+combine_long_kernel" : "crc32c_fused_small_kernel";
         if (seed)
             hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<true>, dim3(static_cast<uint32_t>(c.cus)),
                                dim3(lvk::kThreads), 0, s, P, c.image[2], ws, longs);
@@ -574,7 +618,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
                                dim3(lvk::kThreads), 0, s, P, c.image[2], ws, longs);
     } else {
         longs = launch_sort(ws_bytes, off, len, seed, n, s, &P);
-        g_kernel = "sort+crc32c_classes_kernel";
+        g_kernel = join ? "sort+crc32c_classes_kernel+combine_long_kernel" : "sort+crc32c_classes_kernel";
         launch_classes(c, seed != nullptr, P, ws, s);
     }
     // joins split long buffers (exits at once when the sort split none).  (A
@@ -585,7 +629,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     // (An empty launch -- C2 / C4, or a batch whose split buffers were all
     // joined in the fused kernel -- takes 4-5 us in the trace, with 64
     // workgroups as with one per CU: profiles/r03/fused_small/local_join/.)
-    if (longs)
+    if (longs && join)
         hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(1024), 0, s, ws, longs,
                            P.part, c.base_tabs, out, flags);
     return 0;
@@ -600,7 +644,7 @@ extern "C" {
 
 static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
                              const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
-                             void *stream, uint8_t *d_ws, size_t ws_bytes) {
+                             void *stream, uint8_t *d_ws, size_t ws_bytes, const lv_batch_hint *hint = nullptr) {
     g_err.clear();
     if (n == 0) return LV_OK;
     if (!d_arena || !d_off || !d_len || !d_out) return set_err(LV_ERR_INVALID, "null device pointer");
@@ -621,7 +665,8 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
     } else if (int rc = stream_ws(*c, s, n, &d_ws, &ws_lk)) {
         return rc;
     }
-    if (int rc = launch_binned(*c, d_ws, d_arena, d_off, d_len, d_seed, d_out, n, flags, s)) return rc;
+    const bool join = hint ? hint_needs_join(*hint, n, static_cast<uint32_t>(c->cus)) : true;
+    if (int rc = launch_binned(*c, d_ws, d_arena, d_off, d_len, d_seed, d_out, n, flags, s, join)) return rc;
     return check_launch();
 }
 
@@ -632,6 +677,19 @@ int lv_crc32c_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const 
 }
 
 size_t lv_crc32c_workspace_bytes(size_t n) { return sort_ws_bytes(n); }
+
+int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
+                                const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
+                                const lv_batch_hint *hint, void *d_workspace, size_t workspace_bytes, void *stream) {
+    if (hint) {
+        if (hint->uniform && hint->total_bytes != static_cast<uint64_t>(n) * hint->max_len)
+            return set_err(LV_ERR_INVALID, "uniform hint: total_bytes != n * max_len");
+        if (n && hint->max_len == 0 && hint->total_bytes != 0)
+            return set_err(LV_ERR_INVALID, "hint: max_len 0 with nonzero total_bytes");
+    }
+    return batch_device_impl(d_arena, d_off, d_len, d_seed, d_out, n, flags, stream,
+                             static_cast<uint8_t *>(d_workspace), d_workspace ? workspace_bytes : 0, hint);
+}
 
 int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
                               const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,

@@ -95,6 +95,8 @@ def lib() -> ctypes.CDLL:
     L.lv_crc32c_batch_device_ws.restype = ctypes.c_int
     L.lv_crc32c_batch_device_ws.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, sz, vp]
     L.lv_crc32c_batch_strided.restype = ctypes.c_int
+    L.lv_crc32c_batch_device_hint.restype = ctypes.c_int
+    L.lv_crc32c_batch_device_hint.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, vp, sz, vp]
     L.lv_crc32c_batch_strided.argtypes = [vp, u64, u32, sz, vp, vp, u32, vp]
     L.lv_crc32c_batch_host.restype = ctypes.c_int
     L.lv_crc32c_batch_host.argtypes = [vp, sz, vp, vp, vp, vp, sz, u32, ctypes.c_int]
@@ -237,6 +239,37 @@ def batch_ws(arena, off, length, workspace, seed=None, out=None, masked=False, s
         _dev_ptr(arena, "arena"), _dev_ptr(off, "off"), _dev_ptr(length, "length"),
         _dev_ptr(seed, "seed"), _dev_ptr(out, "out"), n, _flags(masked, None),
         _dev_ptr(workspace, "workspace"), workspace.numel(), _stream_ptr(stream)))
+    return out
+
+
+class BatchHint(ctypes.Structure):
+    """lv_batch_hint (include/lvgpu/crc32c.h): host-side facts about a batch."""
+    _fields_ = [("total_bytes", ctypes.c_uint64), ("max_len", ctypes.c_uint32), ("uniform", ctypes.c_uint32)]
+
+
+def hint_for(lengths) -> BatchHint:
+    """The exact hint of a host-side length list (numpy-convertible)."""
+    import numpy as np
+    ln = np.asarray(lengths, dtype=np.uint64)
+    mx = int(ln.max()) if ln.size else 0
+    return BatchHint(int(ln.sum()), mx, int(ln.size > 0 and bool((ln == mx).all())))
+
+
+def batch_hint(arena, off, length, hint: BatchHint, seed=None, out=None, masked=False, workspace=None,
+               stream=None):
+    """`batch` with host-side facts about the lengths (lv_crc32c_batch_device_hint):
+    the library leaves out launches they prove empty.  `hint` must be exact."""
+    torch = _torch()
+    n = off.numel()
+    if length.numel() != n or (seed is not None and seed.numel() != n):
+        raise LvError("off/length/seed size mismatch")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=arena.device)
+    _check(lib().lv_crc32c_batch_device_hint(
+        _dev_ptr(arena, "arena"), _dev_ptr(off, "off"), _dev_ptr(length, "length"),
+        _dev_ptr(seed, "seed"), _dev_ptr(out, "out"), n, _flags(masked, None),
+        ctypes.byref(hint) if hint is not None else None, _dev_ptr(workspace, "workspace"),
+        workspace.numel() if workspace is not None else 0, _stream_ptr(stream)))
     return out
 
 

@@ -611,7 +611,7 @@ def test_kernel_choice_query(torch_dev):
     o = torch.arange(1025, dtype=torch.int64, device=dev) * 100
     ln = torch.full((1025,), 100, dtype=torch.int32, device=dev)
     lvgpu.batch(t, o, ln)
-    assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel"
+    assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel+combine_long_kernel"
     torch.cuda.synchronize()
 
 
@@ -871,7 +871,7 @@ def test_offsets_api_straddling_joins_repeat(torch_dev, case, api):
                 lvgpu.batch(a2, o2, l2)
             else:
                 lvgpu.batch_ws(a2, o2, l2, ws)
-            assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel"
+            assert lvgpu.last_kernel() == "sort+crc32c_classes_kernel+combine_long_kernel"
 
 
 @pytest.mark.parametrize("n,L,distinct", [(300, 1 << 30, 5), (2000, 256 << 20, 7), (40000, (8 << 20) + 1, 3)])
@@ -898,3 +898,70 @@ def test_offsets_api_huge_batch_piece_budget(torch_dev, n, L, distinct):
     want = want_pair[k]
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, (bad.size, bad[:10])
+
+
+HINT_CASES = {
+    # name: (lengths, offsets layout, join expected with the hint)
+    "uniform_1024x64KiB": (lambda r: np.full(1024, 65536), "packed", False),  # every split buffer is local
+    "uniform_1x16MiB": (lambda r: np.full(1, 16 << 20), "packed", True),      # 4,096 pieces straddle
+    "uniform_16x1MiB": (lambda r: np.full(16, 1 << 20), "odd", True),
+    "uniform_300x4KiB": (lambda r: np.full(300, 4096), "odd", False),          # nothing splits
+    "small_mixed_fused": (lambda r: r.integers(0, 16385, 900), "odd", False),  # <= 16 KiB never splits
+    "sorted_no_split": (lambda r: r.integers(0, 9000, 5000), "odd", False),    # the three-pass sort, no join
+    "sorted_long": (lambda r: np.concatenate([r.integers(0, 5000, 3000), [3 << 20, 70000]]), "odd", True),
+    "fused_long_ragged": (lambda r: np.concatenate([r.integers(0, 300, 100), [1 << 20, 5 << 20]]), "odd", True),
+}
+
+
+@pytest.mark.parametrize("case", sorted(HINT_CASES))
+@pytest.mark.parametrize("seeded", [False, True])
+def test_offsets_api_with_hint(torch_dev, case, seeded):
+    """lv_crc32c_batch_device_hint: exact host-side
+    facts (total bytes, max length, uniform) let the library leave out the
+    long-buffer join when no buffer can split, or when every split buffer of
+    a uniform small batch is joined inside the walk; CRCs bit-exact vs the
+    oracle with and without the hint, and the join launched exactly when a
+    split buffer straddles workgroups."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(sum(map(ord, case)) * 7919)
+    make, layout, join = HINT_CASES[case]
+    lens = np.asarray(make(rng), dtype=np.uint32)
+    n = lens.size
+    gaps = rng.integers(0, 16, n) if layout == "odd" else np.zeros(n, dtype=np.int64)
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        offs[i] = pos
+        pos += int(lens[i])
+    arena = rng.integers(0, 256, pos + 16, dtype=np.uint8).tobytes()
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    want = oracle_batch(arena, offs, lens, seeds, True)
+    a = torch.frombuffer(bytearray(arena), dtype=torch.uint8).to(dev)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    hint = lvgpu.hint_for(lens)
+    assert bool(hint.uniform) == case.startswith("uniform")
+    out = lvgpu.batch_hint(a, o, ln, hint, seed=sd, masked=True)
+    kern = lvgpu.last_kernel()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert ("combine_long_kernel" in kern) == join, kern
+    # the same call without the hint, and with a caller workspace
+    ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
+    out2 = lvgpu.batch_hint(a, o, ln, None, seed=sd, masked=True, workspace=ws)
+    assert "combine_long_kernel" in lvgpu.last_kernel()
+    out3 = lvgpu.batch_hint(a, o, ln, hint, seed=sd, masked=True, workspace=ws)
+    torch.cuda.synchronize()
+    assert np.array_equal(out2.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(out3.cpu().numpy().view(np.uint32), want)
+
+
+def test_hint_rejects_inconsistent_uniform(torch_dev):
+    torch, dev = torch_dev
+    a = torch.zeros(64, dtype=torch.uint8, device=dev)
+    o = torch.zeros(2, dtype=torch.int64, device=dev)
+    ln = torch.full((2,), 8, dtype=torch.int32, device=dev)
+    with pytest.raises(lvgpu.LvError):
+        lvgpu.batch_hint(a, o, ln, lvgpu.BatchHint(17, 8, 1))

@@ -70,7 +70,7 @@ def test_offsets_api_random_sweep(torch_dev, trial):
     else:
         out = lvgpu.batch(arena, o, ln, sd, masked=masked)
     kern = lvgpu.last_kernel()
-    assert kern == ("crc32c_fused_small_kernel+combine_long_kernel" if n <= 1024 else "sort+crc32c_classes_kernel")
+    assert kern == ("crc32c_fused_small_kernel+combine_long_kernel" if n <= 1024 else "sort+crc32c_classes_kernel+combine_long_kernel")
     got = out.cpu().numpy().view(np.uint32)
     want = oracle_batch(arena.cpu().numpy().tobytes(), offs, lens, seeds, masked)
     bad = np.nonzero(got != want)[0]
