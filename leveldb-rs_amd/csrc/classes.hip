@@ -569,7 +569,7 @@ static uint32_t host_split_rule(uint32_t L, uint64_t total, uint32_t *p) {
 // <= kFusedMax buffers also when every split buffer's pieces fall in one
 // workgroup's static rounds of the fused kernel, which joins those itself
 // (the same unit layout crc32c_fused_small_kernel computes on the device).
-static bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
+bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
     uint32_t p = 0;
     if (host_split_rule(h.max_len, h.total_bytes, &p) == 0) return false;  // monotone: nothing splits
     if (!h.uniform || n > lvk::kFusedMax || !LVK_FUSED_LOCAL_JOIN) return true;
@@ -589,7 +589,7 @@ static bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
 // Length-sorted launch of the offsets API, no host sync: the sort (one or
 // three launches), the persistent class kernel, the long-buffer join.
 int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join = true) {
+                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join) {
     uint32_t *ws = reinterpret_cast<uint32_t *>(ws_bytes);
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(arena);

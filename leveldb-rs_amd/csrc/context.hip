@@ -491,7 +491,15 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     uint8_t *ws = nullptr;
     std::unique_lock<std::mutex> ws_lk;
     if (int rc = stream_ws(*c, s, n, &ws, &ws_lk)) return rc;
-    if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s))
+    // the lengths are on the host here: the join is launched only if needed
+    lv_batch_hint hint{0, 0, 1};
+    for (size_t i = 0; i < n; ++i) {
+        hint.total_bytes += h_len[i];
+        hint.max_len = std::max(hint.max_len, h_len[i]);
+    }
+    for (size_t i = 0; i < n && hint.uniform; ++i) hint.uniform = h_len[i] == hint.max_len;
+    const bool join = hint_needs_join(hint, n, static_cast<uint32_t>(c->cus));
+    if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s, join))
         return rc;
     if (int rc = check_launch()) return rc;
     LV_HIP(hipMemcpyAsync(c->h_meta, d_out, n * 4, hipMemcpyDeviceToHost, s));

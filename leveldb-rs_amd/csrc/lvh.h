@@ -142,8 +142,13 @@ uint4 *launch_sort(uint8_t *ws_bytes, const uint64_t *off, const uint32_t *len, 
 void launch_sort_scan(uint32_t *M, uint32_t wgs, uint32_t *ws, uint64_t *wgb, hipStream_t s);
 // The whole offsets API on a workspace: sort, class kernel, long-buffer
 // join (classes.hip).
+// join = false leaves out the join launch (the caller proved it empty with
+// hint_needs_join).
 int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s);
+                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join = true);
+// Whether a batch with these host-side facts needs the long-buffer join
+// (lv_crc32c_batch_device_hint; classes.hip).
+bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus);
 // The persistent class kernel over a sorted list (classes.hip).
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s);
 // One group-size kernel over a batch, offsets or strided (blocks.hip).
