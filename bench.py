@@ -875,6 +875,29 @@ def hash_bench(args):
     L.oracle_hash_batch(host.ctypes.data, offs[:k].ctypes.data, lens[:k].ctypes.data, None, want.ctypes.data, k)
     if not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
         raise SystemExit("hash bench parity check failed")
+    # packed keys (lv_hash_batch_packed): the same keys described by n + 1
+    # bounds of 8 or 4 bytes instead of 12 B of offset + length per key
+    packed = {}
+    bnd = np.concatenate([offs, [total]]).astype(np.int64)
+    for width, dt in ((8, torch.int64), (4, torch.int32)):
+        b = torch.from_numpy(bnd.astype(np.int64 if width == 8 else np.int32)).to(dev)
+        pp50, pavg = _event_times(torch, lambda: H.hash_batch_packed(arena, b, out=out, shard=True),
+                                  args.steps, args.warmup)
+        H.hash_batch_packed(arena, b, out=out)
+        torch.cuda.synchronize()
+        if not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
+            raise SystemExit(f"hash bench parity check failed (packed, {width}-byte bounds)")
+        g = total / (pavg * 1e-3) / 1e9
+        mv = total + (width + 4) * n
+        packed[f"packed_u{8 * width}"] = {
+            "api": f"lv_hash_batch_packed, {width}-byte bounds", "value": round(n / (pavg * 1e-3) / 1e9, 3),
+            "unit": "Gkeys/s", "ms_avg": round(pavg, 4), "ms_p50": round(pp50, 4),
+            "roofline": {"bound": "hbm", "achieved": round(g, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(g / HBM_PEAK_GBS, 4), "bytes_per_launch": total,
+                         "algorithmic_bytes": "key bytes only"},
+            "with_metadata": {"bytes_per_launch": mv, "frac_of_8TBps": round(mv / (pavg * 1e-3) / 8e12, 4),
+                              "note": f"key bytes + {width} B bound read + 4 B output written per key"}}
+        del b
     cpu = hash_cpu_baseline(arena, offs, lens, args.cpu_seconds) if args.cpu_seconds > 0 else None
     moved = total + 16 * n  # key bytes + off/len + out
     key_gbs = total / (avg * 1e-3) / 1e9
@@ -887,7 +910,8 @@ def hash_bench(args):
            "with_metadata": {"bytes_per_launch": moved, "GB_per_s": round(moved / (avg * 1e-3) / 1e9, 1),
                              "frac_of_8TBps": round(moved / (avg * 1e-3) / 8e12, 4),
                              "note": "key bytes + 8 B offset + 4 B length read + 4 B output written per key"},
-           "parity": "first 100000 keys vs oracle", "cpu_baseline": cpu,
+           "parity": "first 100000 keys vs oracle (every API)", "cpu_baseline": cpu,
+           "api": "lv_hash_batch_device (offset + length per key)", **packed,
            "data": "synthetic splitmix64 keys in HBM"}
     print(json.dumps(res), flush=True)
     return res

@@ -33,6 +33,14 @@ uint32_t lv_cache_shard(uint32_t hash);
 int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
                          const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags, void *stream);
 
+/* Packed keys (keys laid end to end, as a block's or an Arrow-style string
+ * array's): key i = d_arena[b[i] .. b[i+1]) for n + 1 bounds b of
+ * `bound_bytes` bytes each (4: uint32_t, 8: uint64_t; nondecreasing), at
+ * d_bounds (device memory, aligned to bound_bytes).  Same output as
+ * lv_hash_batch_device, with 4 or 8 B of metadata per key instead of 12. */
+int lv_hash_batch_packed(const uint8_t *d_arena, const void *d_bounds, uint32_t bound_bytes, const uint32_t *d_seed,
+                         uint32_t *d_out, size_t n, uint32_t flags, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -225,37 +225,70 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
     return h;
 }
 
+// Metadata of one wave-set: this lane's key (offset, length, seed).
+// Offsets API: off[] / len[] / seed[] per key.
+struct OffsetsMeta {
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint32_t *seed;
+    __device__ __forceinline__ void load(uint64_t i, uint32_t n, uint32_t lane, uint64_t &o, uint32_t &L,
+                                         uint32_t &sd) const {
+        (void)lane;
+        const bool v = i < n;
+        o = v ? off[i] : 0u;
+        L = v ? len[i] : 0u;
+        sd = v && seed ? seed[i] : 0u;
+    }
+};
+
+// Packed keys (lv_hash_batch_packed): key i = arena[b[i], b[i+1]) with n + 1
+// bounds of B bytes (u32: an Arrow-style string array, u64: a large one).  A
+// lane reads its start; its end is the next lane's start, and lane 63 reads
+// the one after the set -- 4 or 8 B of metadata per key instead of 12.
+template <typename B>
+struct PackedMeta {
+    const B *b;
+    const uint32_t *seed;
+    __device__ __forceinline__ void load(uint64_t i, uint32_t n, uint32_t lane, uint64_t &o, uint32_t &L,
+                                         uint32_t &sd) const {
+        const bool v = i < n;
+        const uint64_t s = v ? static_cast<uint64_t>(b[i]) : 0u;
+        uint64_t e = __shfl_down(s, 1);
+        if (lane == 63u || i + 1 >= n) e = v ? static_cast<uint64_t>(b[i + 1]) : 0u;
+        o = s;
+        L = v ? static_cast<uint32_t>(e - s) : 0u;
+        sd = v && seed ? seed[i] : 0u;
+    }
+};
+
 // Persistent: wave w of the grid hashes wave-sets w, w + W, ... of 64 keys.
 // The next set's metadata is requested before this set's keys, so its
 // latency overlaps theirs: one memory round trip per set instead of two
 // (a one-set-per-wave grid: meta, then span, then compute, 65 -> 71 % of
 // 8 TB/s was the ceiling of that shape).
-__global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ base,
-                                                   const uint64_t *__restrict__ off,
-                                                   const uint32_t *__restrict__ len,
-                                                   const uint32_t *__restrict__ seed, uint32_t *__restrict__ out,
-                                                   uint32_t n, uint32_t flags) {
+// XCD-aware (round 4): workgroups are dealt round-robin over the 8 XCDs
+// (b and b + 8 share one), so the logical workgroup index puts consecutive
+// sets on one XCD: neighbouring sets share the 128-B lines at their span
+// and metadata edges, and a line shared across XCDs is fetched by each L2.
+template <typename Meta>
+__global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ base, Meta meta,
+                                                   uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
     __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpanBytes / 4 + kSpanPad];
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t lb = (G & 7u) ? b : (b & 7u) * (G >> 3) + (b >> 3);  // logical workgroup
+    uint64_t set = static_cast<uint64_t>(lb) * 4u + wv;
     if (set * 64u >= n) return;  // wave-uniform
-    auto meta = [&](uint64_t st, uint64_t &o, uint32_t &L, uint32_t &sd) {
-        const uint64_t i = st * 64u + lane;
-        const bool v = i < n;
-        o = v ? off[i] : 0u;
-        L = v ? len[i] : 0u;
-        sd = v && seed ? seed[i] : 0u;
-    };
     uint64_t o, on;
     uint32_t L, sd, Ln, sdn;
-    meta(set, o, L, sd);
+    meta.load(set * 64u + lane, n, lane, o, L, sd);
     uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late
     bool pst = false;
     for (;;) {
         const uint64_t nxt = set + W;
         const bool more = nxt * 64u < n;  // wave-uniform
-        if (more) meta(nxt, on, Ln, sdn);
+        if (more) meta.load(nxt * 64u + lane, n, lane, on, Ln, sdn);
         const uint64_t i = set * 64u + lane;
         const bool valid = i < n;
         const uint32_t h = hash_set(base, span[wv], valid, o, L, sd, lane, pout, pval, pst);
@@ -272,6 +305,19 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
         L = Ln;
         sd = sdn;
     }
+}
+
+// persistent grid: 8 workgroups (32 waves) per CU at most
+uint32_t hash_grid(size_t n) {
+    static std::atomic<int> cus_cache[64];
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) cus = cus_cache[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        if (dev >= 0 && dev < 64) cus_cache[dev].store(cus, std::memory_order_relaxed);
+    }
+    const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * kWgsPerCu;
+    return static_cast<uint32_t>(want < cap ? want : cap);
 }
 
 }  // namespace lvh
@@ -308,18 +354,31 @@ int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const ui
     if (!d_arena || !d_off || !d_len || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
     if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
-    // persistent grid: 8 workgroups (32 waves) per CU at most
-    static std::atomic<int> cus_cache[64];
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) cus = cus_cache[dev].load(std::memory_order_relaxed);
-    if (cus == 0) {
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        if (dev >= 0 && dev < 64) cus_cache[dev].store(cus, std::memory_order_relaxed);
-    }
-    const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * lvh::kWgsPerCu;
-    const uint32_t grid = static_cast<uint32_t>(want < cap ? want : cap);
-    hipLaunchKernelGGL(lvh::hash_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), d_arena, d_off,
-                       d_len, d_seed, d_out, static_cast<uint32_t>(n), flags);
+    hipLaunchKernelGGL(lvh::hash_kernel<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed}, d_out,
+                       static_cast<uint32_t>(n), flags);
+    return lvgpu_internal::launch_status();
+}
+
+int lv_hash_batch_packed(const uint8_t *d_arena, const void *d_bounds, uint32_t bound_bytes, const uint32_t *d_seed,
+                         uint32_t *d_out, size_t n, uint32_t flags, void *stream) {
+    lvgpu_internal::clear_error();
+    if (n == 0) return LV_OK;
+    if (!d_arena || !d_bounds || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
+    if (n > 0xffffffffull - 1) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-2 keys per call");
+    if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
+    if (bound_bytes != 4 && bound_bytes != 8) return lvgpu_internal::set_error(LV_ERR_INVALID, "bound_bytes must be 4 or 8");
+    if (reinterpret_cast<uintptr_t>(d_bounds) % bound_bytes)
+        return lvgpu_internal::set_error(LV_ERR_INVALID, "bounds must be aligned to bound_bytes");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (bound_bytes == 4)
+        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint32_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+                           lvh::PackedMeta<uint32_t>{static_cast<const uint32_t *>(d_bounds), d_seed}, d_out,
+                           static_cast<uint32_t>(n), flags);
+    else
+        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint64_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+                           lvh::PackedMeta<uint64_t>{static_cast<const uint64_t *>(d_bounds), d_seed}, d_out,
+                           static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
 }
 

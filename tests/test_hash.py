@@ -181,3 +181,51 @@ def test_gpu_permuted_and_empty_keys_in_span(gpu):
     out = H.hash_batch(a, _dev(gpu, offs, np.int64), _dev(gpu, lens.view(np.int32), np.int32),
                        _dev(gpu, seeds.view(np.int32), np.int32))
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("width", [4, 8])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 20011])
+def test_gpu_packed_bounds(gpu, width, n):
+    """lv_hash_batch_packed: key i = arena[b[i], b[i+1]) from n + 1 bounds of
+    4 or 8 bytes (lengths from the bound deltas, lane 63 reading the bound
+    after its set), empty keys, keys past the 64-B register path and spans
+    past the 4 KiB stage, seeded and not, hashes and shards, vs the oracle."""
+    import torch
+    from lvgpu import hash as H
+    L = _oracle()
+    rng = np.random.default_rng(n * 10 + width)
+    lens = rng.integers(0, 80, n).astype(np.uint32)
+    lens[rng.integers(0, n, max(1, n // 50))] = 0
+    if n > 5100:
+        lens[5000:5064] = rng.integers(70, 101, 64)
+    bounds = np.zeros(n + 1, dtype=np.uint64)
+    bounds[1:] = np.cumsum(lens, dtype=np.uint64)
+    bounds += 7
+    arena = rng.integers(0, 256, size=int(bounds[-1]) + 3, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    offs = bounds[:-1].copy()
+    a = torch.from_numpy(arena).to(gpu)
+    b = _dev(gpu, bounds, np.int32 if width == 4 else np.int64)
+    for sd in (None, seeds):
+        want = np.zeros(n, dtype=np.uint32)
+        L.oracle_hash_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                            None if sd is None else sd.ctypes.data, want.ctypes.data, n)
+        ds = None if sd is None else _dev(gpu, sd.view(np.int32), np.int32)
+        got = H.hash_batch_packed(a, b, ds).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want)
+        sh = H.hash_batch_packed(a, b, ds, shard=True).cpu().numpy().view(np.uint32)
+        assert np.array_equal(sh, want >> 28)
+
+
+@pytest.mark.gpu
+def test_gpu_packed_bad_args(gpu):
+    import torch
+    from lvgpu import hash as H
+    L = H._bind()
+    assert L.lv_hash_batch_packed(None, None, 8, None, None, 0, 0, None) == 0
+    a = torch.zeros(16, dtype=torch.uint8, device=gpu)
+    b = torch.zeros(3, dtype=torch.int64, device=gpu)
+    o = torch.zeros(2, dtype=torch.int32, device=gpu)
+    assert L.lv_hash_batch_packed(a.data_ptr(), b.data_ptr(), 2, None, o.data_ptr(), 2, 0, None) != 0
+    assert L.lv_hash_batch_packed(a.data_ptr(), b.data_ptr() + 4, 8, None, o.data_ptr(), 2, 0, None) != 0

@@ -15,4 +15,10 @@ timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$out/sm
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > "$out/default_driver.json" 2> "$out/default_driver.err" &&
 echo "bench done" &&
 LVGPU_BENCH_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 > "$out/gloo2.json" 2> "$out/gloo2.err" &&
+echo "gloo done" &&
+timeout -k 10 300 python3 bench.py --hash > "$out/hash.json" 2> "$out/hash.err" &&
+timeout -k 10 300 python3 bench.py --table > "$out/table.json" 2> "$out/table.err" &&
+timeout -k 10 300 python3 bench.py --wal-device > "$out/wal_device.json" 2> "$out/wal_device.err" &&
+timeout -k 10 300 python3 bench.py --wal > "$out/wal.json" 2> "$out/wal.err" &&
+timeout -k 10 300 python3 bench.py --long > "$out/long.json" 2> "$out/long.err" &&
 echo "all steps done"
