@@ -35,7 +35,8 @@
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_FUSED_ONE_ROUND) || \
     defined(LVK_FUSED_LOCAL_JOIN) || \
-    defined(LVK_EXP_SEAL_COMPACT))
+    defined(LVK_EXP_SEAL_COMPACT) || \
+    defined(LVK_SEAL_SECTORS))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -110,6 +111,9 @@
 #endif
 #ifndef LVK_FUSED_LOCAL_JOIN  // fused small-batch kernel: one-pass batches join workgroup-local split buffers in place
 #define LVK_FUSED_LOCAL_JOIN 1
+#endif
+#ifndef LVK_SEAL_SECTORS  // seal: write each trailer's whole 32-B sector(s) (merged in registers) instead of 5 byte stores
+#define LVK_SEAL_SECTORS 0
 #endif
 #ifndef LVK_EXP_SEAL_COMPACT  // experiment (no trailers): the seal stores its masked crcs to a per-block array
 #define LVK_EXP_SEAL_COMPACT 0

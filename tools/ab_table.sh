@@ -10,11 +10,11 @@ for spec in $vars; do
   bash tools/build_variant.sh "$name" ${flags//,/ } > "$out/build_$name.txt" 2>&1
 done
 for r in $(seq 1 $rounds); do
-  timeout -k 10 200 python3 bench.py --table > "$out/prod_table_$r.json" 2>> "$out/err.txt"
+  timeout -k 10 200 python3 bench.py --table --cpu-seconds 0 > "$out/prod_table_$r.json" 2>> "$out/err.txt"
   for spec in $vars; do
     name=${spec%%:*}
     LVGPU_EXPERIMENT=1 LVGPU_LIB=$root/leveldb-rs_amd/lib/variants/liblvgpu_$name.so \
-      timeout -k 10 200 python3 bench.py --table > "$out/${name}_table_$r.json" 2>> "$out/err.txt"
+      timeout -k 10 200 python3 bench.py --table --cpu-seconds 0 > "$out/${name}_table_$r.json" 2>> "$out/err.txt"
   done
 done
 echo table ab done
