@@ -569,8 +569,10 @@ def long_bench(args):
         ln = torch.full((n,), bl, dtype=torch.int32, device=dev)
         ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
         row = {"blocks": n, "block_bytes": bl}
+        hint = lvgpu.BatchHint(n * bl, bl, 1)  # uniform: what a caller that knows its lengths passes
         for api, fn in (("strided", lambda: lvgpu.batch_strided(arena, bl, bl, n, out=out)),
-                        ("offsets", lambda: lvgpu.batch_ws(arena, o, ln, ws, out=out))):
+                        ("offsets", lambda: lvgpu.batch_ws(arena, o, ln, ws, out=out)),
+                        ("offsets_hint", lambda: lvgpu.batch_hint(arena, o, ln, hint, out=out, workspace=ws))):
             p50, avg = _event_times(torch, fn, max(20, min(args.steps, 100)), max(10, min(args.warmup, 50)))
             fn()
             kern = lvgpu.last_kernel()

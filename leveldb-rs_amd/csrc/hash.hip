@@ -23,6 +23,7 @@
 #include "../../include/lvgpu/crc32c.h"
 #include "../../include/lvgpu/hash.h"
 #include "lv_internal.h"
+#include "lvk/knobs.h"
 
 namespace lvh {
 
@@ -43,15 +44,10 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t bs
 }
 
 // One wave's staged key bytes: the 16-B granules spanning its 64 keys.
-#ifndef LVH_SPAN_READLANE
-#define LVH_SPAN_READLANE 1
-#endif
+
 
 constexpr uint32_t kSpanBytes = 4096;
-#ifndef LVH_WGS_PER_CU
-#define LVH_WGS_PER_CU 8
-#endif
-constexpr uint64_t kWgsPerCu = LVH_WGS_PER_CU;
+constexpr uint64_t kWgsPerCu = LVK_HASH_WGS_PER_CU;
 constexpr uint32_t kSpanPad = 20;  // dwords past the span a masked fast-path read may address
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
@@ -85,7 +81,7 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
     // stages the granules spanning its 64 keys through LDS with coalesced
     // 16-B loads, instead of 64 lanes gathering byte-aligned keys.  Waves
     // whose keys span more than kSpanBytes read keys straight from memory.
-#if LVH_SPAN_READLANE
+#if LVK_HASH_SPAN_READLANE
     // Candidate span from the first and the last lane of the wave (keys are
     // usually packed in order); the wave stages it only if every key lies
     // inside it.  Two lane reads and one ballot instead of two 64-bit
@@ -225,39 +221,61 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
     return h;
 }
 
-// Metadata of one wave-set: this lane's key (offset, length, seed).
+// Metadata of one wave-set: load() requests this lane's words (issued one
+// set ahead), get() turns them into (offset, length, seed) when the set is
+// hashed -- any cross-lane step sits there, so the prefetch never waits.
+struct MetaRaw {
+    uint64_t o, x;
+    uint32_t L, sd;
+};
+
 // Offsets API: off[] / len[] / seed[] per key.
 struct OffsetsMeta {
     const uint64_t *off;
     const uint32_t *len;
     const uint32_t *seed;
-    __device__ __forceinline__ void load(uint64_t i, uint32_t n, uint32_t lane, uint64_t &o, uint32_t &L,
-                                         uint32_t &sd) const {
-        (void)lane;
+    __device__ __forceinline__ MetaRaw load(uint64_t i, uint32_t n, uint32_t) const {
         const bool v = i < n;
-        o = v ? off[i] : 0u;
-        L = v ? len[i] : 0u;
-        sd = v && seed ? seed[i] : 0u;
+        MetaRaw r;
+        r.o = v ? off[i] : 0u;
+        r.x = 0;
+        r.L = v ? len[i] : 0u;
+        r.sd = v && seed ? seed[i] : 0u;
+        return r;
+    }
+    __device__ __forceinline__ void get(const MetaRaw &r, uint64_t, uint32_t, uint32_t, uint64_t &o, uint32_t &L,
+                                        uint32_t &sd) const {
+        o = r.o;
+        L = r.L;
+        sd = r.sd;
     }
 };
 
 // Packed keys (lv_hash_batch_packed): key i = arena[b[i], b[i+1]) with n + 1
 // bounds of B bytes (u32: an Arrow-style string array, u64: a large one).  A
-// lane reads its start; its end is the next lane's start, and lane 63 reads
-// the one after the set -- 4 or 8 B of metadata per key instead of 12.
+// lane reads its start; its end is the next lane's start, and lane 63 (or
+// the last key) reads the bound after it -- 4 or 8 B of metadata per key
+// instead of 12.
 template <typename B>
 struct PackedMeta {
     const B *b;
     const uint32_t *seed;
-    __device__ __forceinline__ void load(uint64_t i, uint32_t n, uint32_t lane, uint64_t &o, uint32_t &L,
-                                         uint32_t &sd) const {
+    __device__ __forceinline__ MetaRaw load(uint64_t i, uint32_t n, uint32_t lane) const {
         const bool v = i < n;
-        const uint64_t s = v ? static_cast<uint64_t>(b[i]) : 0u;
-        uint64_t e = __shfl_down(s, 1);
-        if (lane == 63u || i + 1 >= n) e = v ? static_cast<uint64_t>(b[i + 1]) : 0u;
-        o = s;
-        L = v ? static_cast<uint32_t>(e - s) : 0u;
-        sd = v && seed ? seed[i] : 0u;
+        MetaRaw r;
+        r.o = v ? static_cast<uint64_t>(b[i]) : 0u;
+        r.x = v && (lane == 63u || i + 1 >= n) ? static_cast<uint64_t>(b[i + 1]) : 0u;
+        r.L = 0;
+        r.sd = v && seed ? seed[i] : 0u;
+        return r;
+    }
+    __device__ __forceinline__ void get(const MetaRaw &r, uint64_t i, uint32_t n, uint32_t lane, uint64_t &o,
+                                        uint32_t &L, uint32_t &sd) const {
+        const uint64_t nx = __shfl_down(r.o, 1);
+        const uint64_t e = (lane == 63u || i + 1 >= n) ? r.x : nx;
+        o = r.o;
+        L = i < n ? static_cast<uint32_t>(e - r.o) : 0u;
+        sd = r.sd;
     }
 };
 
@@ -277,20 +295,21 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
     const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t lb = (G & 7u) ? b : (b & 7u) * (G >> 3) + (b >> 3);  // logical workgroup
+    const uint32_t lb = (!LVK_HASH_XCD_MAP || (G & 7u)) ? b : (b & 7u) * (G >> 3) + (b >> 3);  // logical workgroup
     uint64_t set = static_cast<uint64_t>(lb) * 4u + wv;
     if (set * 64u >= n) return;  // wave-uniform
-    uint64_t o, on;
-    uint32_t L, sd, Ln, sdn;
-    meta.load(set * 64u + lane, n, lane, o, L, sd);
+    MetaRaw cur = meta.load(set * 64u + lane, n, lane), nx{};
     uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late
     bool pst = false;
     for (;;) {
         const uint64_t nxt = set + W;
         const bool more = nxt * 64u < n;  // wave-uniform
-        if (more) meta.load(nxt * 64u + lane, n, lane, on, Ln, sdn);
+        if (more) nx = meta.load(nxt * 64u + lane, n, lane);
         const uint64_t i = set * 64u + lane;
         const bool valid = i < n;
+        uint64_t o;
+        uint32_t L, sd;
+        meta.get(cur, i, n, lane, o, L, sd);
         const uint32_t h = hash_set(base, span[wv], valid, o, L, sd, lane, pout, pval, pst);
         pout = out + (valid ? i : 0u);
         pval = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
@@ -301,9 +320,7 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
         }
         __builtin_amdgcn_wave_barrier();  // this set's LDS reads precede the next stage
         set = nxt;
-        o = on;
-        L = Ln;
-        sd = sdn;
+        cur = nx;
     }
 }
 
