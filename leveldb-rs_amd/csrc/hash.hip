@@ -284,19 +284,18 @@ struct PackedMeta {
 // latency overlaps theirs: one memory round trip per set instead of two
 // (a one-set-per-wave grid: meta, then span, then compute, 65 -> 71 % of
 // 8 TB/s was the ceiling of that shape).
-// XCD-aware (round 4): workgroups are dealt round-robin over the 8 XCDs
-// (b and b + 8 share one), so the logical workgroup index puts consecutive
-// sets on one XCD: neighbouring sets share the 128-B lines at their span
-// and metadata edges, and a line shared across XCDs is fetched by each L2.
+// (Round 4: an XCD-aware set order -- the logical workgroup (b % 8) * (G / 8)
+// + b / 8, so that neighbouring sets, which share the 128-B lines at their
+// span and metadata edges, sit on one XCD's L2 -- measured 1 % slower on the
+// offsets API and 3 % on packed keys, three interleaved reps each:
+// profiles/r04/ab1/.)
 template <typename Meta>
 __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ base, Meta meta,
                                                    uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
     __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpanBytes / 4 + kSpanPad];
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t lb = (!LVK_HASH_XCD_MAP || (G & 7u)) ? b : (b & 7u) * (G >> 3) + (b >> 3);  // logical workgroup
-    uint64_t set = static_cast<uint64_t>(lb) * 4u + wv;
+    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
     if (set * 64u >= n) return;  // wave-uniform
     MetaRaw cur = meta.load(set * 64u + lane, n, lane), nx{};
     uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late

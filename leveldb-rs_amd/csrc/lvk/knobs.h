@@ -36,9 +36,7 @@
     defined(LVK_FUSED_ONE_ROUND) || \
     defined(LVK_FUSED_LOCAL_JOIN) || \
     defined(LVK_EXP_SEAL_COMPACT) || \
-    defined(LVK_SEAL_SECTORS) || \
     defined(LVK_HASH_SPAN_READLANE) || \
-    defined(LVK_HASH_XCD_MAP) || \
     defined(LVK_HASH_WGS_PER_CU))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
@@ -118,14 +116,8 @@
 #ifndef LVK_HASH_SPAN_READLANE  // hash: a wave's span from its first and last lanes (0: two wave reductions)
 #define LVK_HASH_SPAN_READLANE 1
 #endif
-#ifndef LVK_HASH_XCD_MAP  // hash: consecutive wave-sets on one XCD (0: round 3's round-robin placement)
-#define LVK_HASH_XCD_MAP 1
-#endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8
-#endif
-#ifndef LVK_SEAL_SECTORS  // seal: write each trailer's whole 32-B sector(s) (merged in registers) instead of 5 byte stores
-#define LVK_SEAL_SECTORS 0
 #endif
 #ifndef LVK_EXP_SEAL_COMPACT  // experiment (no trailers): the seal stores its masked crcs to a per-block array
 #define LVK_EXP_SEAL_COMPACT 0

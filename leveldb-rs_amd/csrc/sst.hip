@@ -92,61 +92,6 @@ struct TableUnits {
             if (CRCOUT) g_ocrc[wave][32 + slot] = ok ? crc : 0u;
         }
     }
-    // Seal by whole 32-B sectors: the trailer [E, E + 5) (E = offset + size)
-    // lies in the sector at S = E & ~31, or in the two from S when E & 31 > 27;
-    // they are loaded, the 5 trailer bytes merged in registers and the sectors
-    // stored whole, so no partial-sector write reaches HBM (the byte stores'
-    // WRITE_SIZE is 36 B per 5-B trailer).  Only where the sectors hold this
-    // block's contents, its trailer and the NEXT block's contents alone -- both
-    // blocks >= 64 B and the next handle the block right after the trailer --
-    // are other blocks' bytes rewritten (with the values just read; nobody
-    // writes a block's contents), so no other trailer shares a sector.
-    // Otherwise (tiny blocks, handles out of file order, the last block) the
-    // byte stores.  Returns true when the sectors were written.
-    __device__ __forceinline__ bool seal_sectors(const Params &P, uint32_t bi, uint64_t o, uint64_t sz, uint32_t f,
-                                                 uint32_t m) const {
-        if (sz < 64u || bi + 1u >= P.n) return false;
-        const uint2 no = handles[2 * (bi + 1)], ns = handles[2 * (bi + 1) + 1];
-        const uint64_t o2 = (static_cast<uint64_t>(no.y) << 32) | no.x, sz2 = (static_cast<uint64_t>(ns.y) << 32) | ns.x;
-        if (o2 != o + sz + 5u || sz2 < 64u || !sst_in_range(o2, sz2, file_bytes)) return false;
-        const uint64_t E = P.base + o + sz;
-        const uint64_t S = E & ~31ull;
-        const uint32_t r = static_cast<uint32_t>(E - S);  // 0..31
-        const uint64_t tv = f | (static_cast<uint64_t>(m) << 8);  // the 5 trailer bytes, little-endian
-        uint4 v[4] = {};
-        v[0] = load16_rt(S);
-        v[1] = load16_rt(S + 16);
-        const bool two = r > 27u;
-        if (two) {
-            v[2] = load16_rt(S + 32);
-            v[3] = load16_rt(S + 48);
-        }
-        auto merge = [&](uint32_t w, uint32_t k) -> uint32_t {  // dword k (bytes 4k .. 4k+3)
-            const uint32_t lo = r > 4u * k ? r - 4u * k : 0u;
-            const uint32_t hi0 = r + 5u - 4u * k;
-            if (r + 5u <= 4u * k || r >= 4u * k + 4u) return w;
-            const uint32_t hi = hi0 < 4u ? hi0 : 4u;
-            const uint64_t bm64 = ((1ull << (8u * hi)) - 1u) ^ ((1ull << (8u * lo)) - 1u);
-            const uint32_t bm = static_cast<uint32_t>(bm64);
-            const uint32_t val = 4u * k >= r ? static_cast<uint32_t>(tv >> (8u * (4u * k - r)))
-                                             : static_cast<uint32_t>(tv << (8u * (r - 4u * k)));
-            return (w & ~bm) | (val & bm);
-        };
-#pragma unroll
-        for (uint32_t g = 0; g < 4; ++g) {
-            v[g].x = merge(v[g].x, 4 * g);
-            v[g].y = merge(v[g].y, 4 * g + 1);
-            v[g].z = merge(v[g].z, 4 * g + 2);
-            v[g].w = merge(v[g].w, 4 * g + 3);
-        }
-        *reinterpret_cast<uint4 *>(S) = v[0];
-        *reinterpret_cast<uint4 *>(S + 16) = v[1];
-        if (two) {
-            *reinterpret_cast<uint4 *>(S + 32) = v[2];
-            *reinterpret_cast<uint4 *>(S + 48) = v[3];
-        }
-        return true;
-    }
     __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
         if constexpr (SEAL) {
             if (lane >= nslots) return;
@@ -161,7 +106,6 @@ struct TableUnits {
             uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
             const uint32_t f = types ? types[bi] : 0u;
             const uint32_t m = g_ocrc[wave][lane];
-            if (LVK_SEAL_SECTORS && seal_sectors(P, bi, o, sz, f, m)) return;
             p[0] = static_cast<uint8_t>(f);
             p[1] = static_cast<uint8_t>(m);
             p[2] = static_cast<uint8_t>(m >> 8);

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/ab1/; the switch it measured was then retired with its code.)
 # Round 4 A/B pass 1: hash tests + the hash bench (product: XCD-aware sets,
 # packed keys with the deferred length shuffle) alternated with the
 # round-robin placement (LVK_HASH_XCD_MAP=0); the few-long-buffer bench with

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/ab1/; the switch it measured was then retired with its code.)
 # Round 4: the sector-merge seal (LVK_SEAL_SECTORS=1) -- its parity under the
 # table tests, then the table bench alternated with the product library, and
 # a WRITE_SIZE pass of each.  usage: tools/r04_seal_ab.sh OUTDIR
