@@ -43,31 +43,13 @@ struct TableUnits {
     // the trailer stores are partial-line writes, and fewer, larger bursts of
     // them measured faster); verify: 64 slots of {block, status}, or with
     // crc_out 32 slots of four words
-    uint64_t nblk;         // blocks (P.n is the round-padded entry count when kRun > 0)
     static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
-    // Runs (LVK_SST_RUN = R > 0): the wave's rounds come in chunks of R, and
-    // group g of chunk c walks blocks c 4R + g R + j in rounds j = 0 .. R-1, so
-    // a group's consecutive rounds are consecutive blocks of the file: the
-    // 256-B row a block's tail shares with the next block's head is requested
-    // again right after (the next round's first batch is prefetched during the
-    // last batch), instead of by another wave rounds later, past L2 (the
-    // table walk fetched 1.06x its bytes, profiles/r03/prof8f/).
-    static constexpr uint64_t kRun = LVK_SST_RUN;
-    __device__ __forceinline__ uint64_t block_of(uint64_t e) const {
-        if constexpr (kRun == 0) {
-            return e;
-        } else {
-            const uint64_t rho = e >> 2, grp = e & 3u;
-            return (rho / kRun) * 4u * kRun + grp * kRun + rho % kRun;
-        }
-    }
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
     static constexpr bool kOneRound = false;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
-        const uint64_t b = block_of(e);
-        const bool valid = e < P.n && b < nblk;
-        const uint64_t ec = valid ? b : nblk - 1;
+        const bool valid = e < P.n;
+        const uint64_t ec = valid ? e : P.n - 1;
         const uint2 ho = handles[2 * ec], hs = handles[2 * ec + 1];  // u64 pairs: 8-B alignment is enough
         const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
         const bool ok = sst_in_range(o, sz, file_bytes);
@@ -156,29 +138,12 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
     const uint32_t lane = threadIdx.x & 63u;
     const Lut L = make_lut(lane);
     const uint64_t grid = gridDim.x;
-    if constexpr (TableUnits<SEAL, CRCOUT>::kRun == 0) {
-        auto pool = [&]() -> uint64_t {
-            uint32_t k = 0;
-            if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
-            return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
-        };
-        sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
-    } else {
-        // the workgroup's pool hands out chunks of kRun rounds; a wave walks
-        // its chunk's rounds in order (wave-uniform)
-        constexpr uint64_t R = TableUnits<SEAL, CRCOUT>::kRun;
-        uint64_t cur = 0, end = 0;
-        auto pool = [&]() -> uint64_t {
-            if (cur == end) {
-                uint32_t k = 0;
-                if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
-                cur = (blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0))) * R;
-                end = cur + R;
-            }
-            return cur++;
-        };
-        sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
-    }
+    auto pool = [&]() -> uint64_t {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
+        return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+    };
+    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
 }
 
 }  // namespace lvk
@@ -192,23 +157,21 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     if (int rc = current_ctx(&c)) return rc;
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(d_file);
-    constexpr uint64_t kChunk = 4u * (LVK_SST_RUN ? LVK_SST_RUN : 1u);  // blocks per pool claim
-    P.n = (n + kChunk - 1) / kChunk * kChunk;  // rounds of the walk (padding entries are not blocks)
+    P.n = n;
     P.flags = 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (n + kChunk - 1) / kChunk))), block(lvk::kThreads);
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (n + 3) / 4))), block(lvk::kThreads);
     if (seal) {
-        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes, n};
+        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
         g_kernel = "sst_blocks_kernel<seal>";
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P, c->image[kTableImage], u);
     } else if (d_crc) {
-        lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes,
-                                       n};
+        lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
         g_kernel = "sst_blocks_kernel<verify,crc>";
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, true>), grid, block, 0, s, P, c->image[kTableImage], u);
     } else {
         lvk::TableUnits<false, false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, nullptr,
-                                        file_bytes, n};
+                                        file_bytes};
         g_kernel = "sst_blocks_kernel<verify>";
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, false>), grid, block, 0, s, P, c->image[kTableImage], u);
     }

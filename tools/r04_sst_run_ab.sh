@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/sst_run/; the switch it measured was then retired with its code.)
 # Round 4: run-ordered table walk (LVK_SST_RUN = R: a group walks R
 # consecutive blocks in consecutive rounds).  Parity of each variant under
 # the table tests, the table bench alternated with the product library, and
