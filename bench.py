@@ -354,6 +354,17 @@ def cpu_loop_baseline(pass_fn, n, seconds, sample, unit_scale=2**30, unit="GiB/s
             "host_cpu": _cpu_model(), "host_nproc": os.cpu_count()}
 
 
+def wal_oracle_check(log, expect_records):
+    """The oracle's whole-log verify (oracle_wal_verify, log_reader.rs:271-364)
+    finds every record intact: the stored header CRCs equal the oracle's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    mm = ctypes.c_uint64()
+    ok = W.lib().oracle_wal_verify(log.ctypes.data, int(log.size), ctypes.byref(mm), None)
+    if ok != expect_records or mm.value:
+        raise SystemExit(f"WAL oracle verify found {ok} good / {mm.value} bad records, expected {expect_records}")
+
+
 def wal_cpu_baseline(log, seconds, expect_records):
     """The reference reader's verify (log_reader.rs:271-364: 32 KiB reads,
     header framing, unmask(header) == value([type || payload]) per record)
@@ -678,8 +689,22 @@ def wal_device_bench(args):
             st = (int(h_info[k]) >> 8) & 0xff
             if st == 0 and int(h_crc[k]) != W.value(raw[int(h_hdr[k]) + 6:int(h_hdr[k]) + 7 + ln]):
                 raise SystemExit("WAL device scan parity check failed")
-        parity = "first 2000 records' CRCs vs oracle value()"
+        # every record: the GPU value([type||payload]) == unmask(its header's
+        # stored CRC); the oracle's whole-log verify (wal_oracle_check below)
+        # pins the stored CRCs to the oracle's, so the two give every record
+        hc = h_hdr.astype(np.int64)
+        stored = (log[hc].astype(np.uint32) | (log[hc + 1].astype(np.uint32) << 8)
+                  | (log[hc + 2].astype(np.uint32) << 16) | (log[hc + 3].astype(np.uint32) << 24))
+        r = (stored - np.uint32(0xa282ead8)).astype(np.uint32)
+        unm = ((r >> np.uint32(17)) | (r << np.uint32(15))).astype(np.uint32)  # crc32c.rs:59-63
+        okst = ((h_info >> 8) & 0xff) == 0
+        if not np.array_equal(h_crc[okst], unm[okst]) or not okst.all():
+            raise SystemExit("WAL device scan: a record's CRC differs from its header")
+        parity = ("every record's GPU CRC == unmask(its header CRC), and the oracle's whole-log verify "
+                  "(oracle_wal_verify) accepts every header; first 2000 records also vs oracle value()")
     variant = os.environ.get("LVGPU_EXPERIMENT") == "1"
+    if not variant:  # the oracle's verify of the whole log, untimed (the cpu_baseline below times it)
+        wal_oracle_check(log, cap)
     cpu = wal_cpu_baseline(log, args.cpu_seconds, cap) if args.cpu_seconds > 0 and not variant else None
     gbs = log.size / (avg * 1e-3) / 1e9
     res = {"metric": "device-resident WAL verify scan (framing + CRC of every record), HBM", "unit": "GB/s",
@@ -744,7 +769,8 @@ def table_bench(args):
                     "ms_p50": round(seal_p50, 4), "frac_of_8TBps": round(unit / (seal_avg * 1e-3) / 8e12, 4)},
            "verify": {"GiB_per_s": round(unit / 2**30 / (ver_avg * 1e-3), 1), "ms_avg": round(ver_avg, 4),
                       "ms_p50": round(ver_p50, 4), "frac_of_8TBps": round(unit / (ver_avg * 1e-3) / 8e12, 4)},
-           "timing": "HIP events around each call (CRC batch + trailer kernels)", "parity": "first 2000 blocks vs oracle",
+           "timing": "HIP events around each call (CRC batch + trailer kernels)", "parity": ("first 2000 blocks' CRCs vs oracle value(); every sealed trailer vs the oracle's "
+                      "verify (oracle_units_verify, in the cpu_baseline pass)" if cpu else "first 2000 blocks vs oracle"),
            "host_e2e": host_e2e, "cpu_baseline": cpu,
            "data": "synthetic splitmix64 contents in HBM"}
     print(json.dumps(res), flush=True)
@@ -900,6 +926,15 @@ def hash_bench(args):
             "with_metadata": {"bytes_per_launch": mv, "frac_of_8TBps": round(mv / (pavg * 1e-3) / 8e12, 4),
                               "note": f"key bytes + {width} B bound read + 4 B output written per key"}}
         del b
+    # every key vs the oracle (untimed), then the CPU baseline
+    full = np.zeros(n, dtype=np.uint32)
+    host_all = arena.cpu().numpy()
+    L.oracle_hash_batch(host_all.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, full.ctypes.data, n)
+    H.hash_batch(arena, o, ln, out=out)
+    torch.cuda.synchronize()
+    if not np.array_equal(out.cpu().numpy().view(np.uint32), full):
+        raise SystemExit("hash bench parity check failed (all keys)")
+    del host_all
     cpu = hash_cpu_baseline(arena, offs, lens, args.cpu_seconds) if args.cpu_seconds > 0 else None
     moved = total + 16 * n  # key bytes + off/len + out
     key_gbs = total / (avg * 1e-3) / 1e9
@@ -912,7 +947,7 @@ def hash_bench(args):
            "with_metadata": {"bytes_per_launch": moved, "GB_per_s": round(moved / (avg * 1e-3) / 1e9, 1),
                              "frac_of_8TBps": round(moved / (avg * 1e-3) / 8e12, 4),
                              "note": "key bytes + 8 B offset + 4 B length read + 4 B output written per key"},
-           "parity": "first 100000 keys vs oracle (every API)", "cpu_baseline": cpu,
+           "parity": "all keys vs oracle (offsets API), first 100000 keys (every API)", "cpu_baseline": cpu,
            "api": "lv_hash_batch_device (offset + length per key)", **packed,
            "data": "synthetic splitmix64 keys in HBM"}
     print(json.dumps(res), flush=True)

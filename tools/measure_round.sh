@@ -10,9 +10,12 @@
 #   the N=2 launcher rehearsal (gloo, both ranks on the one GPU).  Every GPU
 #   step has its own timeout and the chain stops at the first failure;
 #   tools/round_summary.py writes summary.md (events beside rocprof sums).
-# usage: tools/measure_round.sh OUTDIR
+# usage: tools/measure_round.sh OUTDIR [bench|prof|all]
+#   (round 4: the bench lines carry CPU baselines and the default lines a
+#   c5_strong sub-record, so the pass is run as two GPU calls: bench, prof)
 set -o pipefail
 out=${1:-gpurun_out/round}
+part=${2:-all}
 mkdir -p "$out"
 root=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$root"
@@ -22,6 +25,7 @@ p() { local name=$1; shift
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_$name" -o "$name" -- \
          python3 "$root/bench.py" --steps 50 --warmup 100 --cpu-seconds 0 --traffic off --c5-strong off "$@") > "$out/prof_$name.log" 2>&1 &&
       python3 tools/kstats_steady.py "$(ls "$out/prof_$name"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_${name}_steady.json" > /dev/null; }
+bench_part() {
 b default_driver --steps 20 --warmup 5 &&
 b default &&
 b c3_offsets --workload c3 --api offsets --cpu-seconds 5 &&
@@ -36,7 +40,8 @@ timeout -k 10 300 python3 bench.py --table > "$out/table.json" 2> "$out/table.er
 timeout -k 10 300 python3 bench.py --hash > "$out/hash.json" 2> "$out/hash.err" &&
 timeout -k 10 300 python3 bench.py --sweep > "$out/sweep.json" 2> "$out/sweep.err" &&
 timeout -k 10 300 python3 bench.py --wal-device > "$out/wal_device.json" 2> "$out/wal_device.err" &&
-timeout -k 10 300 python3 bench.py --long > "$out/long.json" 2> "$out/long.err" &&
+timeout -k 10 300 python3 bench.py --long > "$out/long.json" 2> "$out/long.err"; }
+prof_part() {
 p c3 &&
 p c2 --workload c2 --api offsets &&
 p c4 --workload c4 --api offsets &&
@@ -46,6 +51,11 @@ python3 tools/kstats_steady.py "$(ls "$out/prof_wal"/*kernel_trace.csv | head -n
 bash tools/prof_8f.sh "$out/prof8f" table hash &&
 bash tools/prof_long.sh "$out/prof_long" &&
 LVGPU_BENCH_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 > "$out/gloo2.json" 2> "$out/gloo2.err" &&
-for d in "$out"/prof_*/; do find "$d" -name '*kernel_trace.csv' -size +1M -delete; done;
+for d in "$out"/prof_*/; do find "$d" -name '*kernel_trace.csv' -size +1M -delete; done; }
+case $part in
+  bench) bench_part ;;
+  prof) prof_part ;;
+  *) bench_part && prof_part ;;
+esac &&
 python3 tools/round_summary.py "$out" > "$out/summary.md" &&
 echo "all steps done"
