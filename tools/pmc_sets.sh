@@ -22,7 +22,7 @@ agg = collections.defaultdict(list)
 for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
         name = row.get("Kernel_Name", "")
-        if "lvk::" in name and "fill_" not in name:
+        if ("lvk::" in name or "lvh::" in name) and "fill_" not in name:
             short = name.split("(")[0].replace("void ", "")
             agg[(short, row["Counter_Name"])].append(float(row["Counter_Value"]))
 with open(os.path.join(out, "summary.txt"), "w") as fo:
