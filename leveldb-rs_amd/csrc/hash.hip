@@ -9,6 +9,14 @@
 // memory.  Either way the words are dword-aligned reads funnel-shifted by the
 // key's byte misalignment (v_alignbyte_b32), never touching a dword past the
 // key's last byte, and keys of <= 64 B run the chain from registers.
+// Round 4 (profiles/r04/hash_pmc/, hash_ab/): the kernel is not bound by its
+// bytes -- packed keys fetch 15 % less (n + 1 bounds instead of an offset and
+// a length per key) in the same time -- nor by its instruction stream: a
+// branch-free chain and span staging (selects instead of exec-mask branches,
+// ~180 scalar instructions per set of 64 keys fewer) measured the same.  The
+// waves sit in s_waitcnt 56 % of their cycles (SQ_WAIT_ANY): each set's span
+// load waits for the set's metadata, so a set costs one exposed memory round
+// trip per wave at full occupancy.
 // The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
 // requests the next set's metadata ahead, and stores each result one set
 // late, after the next set's loads, so no wait includes a store.  (A
@@ -105,17 +113,10 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
         u32x4 *dst = reinterpret_cast<u32x4 *>(span);
         constexpr uint32_t kCh = kSpanBytes / 16 / 64;
         u32x4 t[kCh];
-        // (branch-free: a row k of chunks is wave-uniformly present or not;
-        // lanes past the span re-read its last chunk and store it again,
-        // instead of exec-mask branches around each load and store)
 #pragma unroll
         for (uint32_t k = 0; k < kCh; ++k) {
             const uint32_t c = lane + 64u * k;
-            if (LVK_HASH_BRANCHFREE) {
-                if (64u * k < nch) t[k] = __builtin_nontemporal_load(src + (c < nch ? c : nch - 1u));
-            } else if (c < nch) {
-                t[k] = __builtin_nontemporal_load(src + c);
-            }
+            if (c < nch) t[k] = __builtin_nontemporal_load(src + c);
         }
         // the previous set's result leaves after this set's loads: waiting
         // for them (vmcnt is in order) then does not wait for the store
@@ -123,11 +124,7 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
 #pragma unroll
         for (uint32_t k = 0; k < kCh; ++k) {
             const uint32_t c = lane + 64u * k;
-            if (LVK_HASH_BRANCHFREE) {
-                if (64u * k < nch) dst[c < nch ? c : nch - 1u] = t[k];
-            } else if (c < nch) {
-                dst[c] = t[k];
-            }
+            if (c < nch) dst[c] = t[k];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -141,13 +138,10 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
         // they fit and single dwords at its end), zeros past the key; the
         // chain then runs from registers, predicated per lane.
         uint32_t w[kFastDw + 1];
-        const uint32_t *sd = span + ((o - bs - lo16) >> 2);  // (staged) the key's first dword in the stage
         if (staged) {
-            // every dword read unconditionally (the stage is padded by
-            // kSpanPad dwords): words past the key never reach the hash --
-            // a word j < nw lies inside the key, the tail keeps diff bytes
+            const uint32_t *sd = span + ((o - bs - lo16) >> 2);
 #pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = LVK_HASH_BRANCHFREE ? sd[j] : (j < ndw ? sd[j] : 0u);
+            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = j < ndw ? sd[j] : 0u;
         } else {
             const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
             w[0] = d[0];
@@ -168,41 +162,21 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
         }
         w[kFastDw] = 0u;
         uint32_t tw = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kFastDw; ++j) {
+            const uint32_t wj = funnel(w[j + 1], w[j], bs);
+            if (j < nw)
+                h = mix(h, wj);
+            else if (j == nw)
+                tw = wj;
+        }
         const uint32_t diff = L - 4 * nw;          // hash.rs:38-48
-        if constexpr (LVK_HASH_BRANCHFREE) {
-            // Every step for every lane, the result selected (v_cndmask): the
-            // per-lane `if (j < nw)` compiled to exec-mask branches, ~180
-            // scalar instructions per set of 64 keys (SQ_INSTS_SALU,
-            // profiles/r04/hash_pmc/) on a kernel whose waves issue-stall.
-#pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j) {
-                const uint32_t wj = funnel(w[j + 1], w[j], bs);
-                const uint32_t hm = mix(h, wj);
-                h = j < nw ? hm : h;
-                if (!staged) tw = j == nw ? wj : tw;  // wave-uniform branch
-            }
-            if (staged) tw = funnel(sd[nw + 1], sd[nw], bs);  // the tail word straight from the stage
-            uint32_t ht = h + (diff >= 3 ? ((tw >> 16) & 0xffu) << 16 : 0u) + (diff >= 2 ? ((tw >> 8) & 0xffu) << 8 : 0u) +
-                          (tw & 0xffu);
-            ht *= kM;
-            ht ^= ht >> 24;
-            h = diff ? ht : h;
-        } else {
-#pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j) {
-                const uint32_t wj = funnel(w[j + 1], w[j], bs);
-                if (j < nw)
-                    h = mix(h, wj);
-                else if (j == nw)
-                    tw = wj;
-            }
-            if (diff) {
-                if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
-                if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;
-                h += tw & 0xffu;
-                h *= kM;
-                h ^= h >> 24;
-            }
+        if (diff) {
+            if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
+            if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;
+            h += tw & 0xffu;
+            h *= kM;
+            h ^= h >> 24;
         }
     } else if (valid && L) {
         const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/hash_ab/; the switch it measured was then retired with its code.)
 # Round 4: the branch-free hash chain and span staging (LVK_HASH_BRANCHFREE=1,
 # the product) against the round-3 branchy form (=0): hash tests, then the
 # hash bench alternated three times.  usage: tools/r04_hash_ab.sh OUTDIR
