@@ -102,6 +102,11 @@ int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, c
                                 const lv_batch_hint *hint, void *d_workspace, size_t workspace_bytes,
                                 void *stream);
 
+/* Debug query: 1 if a batch of n buffers with these facts, on a device with
+ * `cus` compute units, launches the long-buffer join (the decision
+ * lv_crc32c_batch_device_hint makes on the host), 0 if it is left out. */
+int lv_crc32c_hint_needs_join(const lv_batch_hint *hint, size_t n, uint32_t cus);
+
 /* Fixed-stride form for table blocks: buffer i is
  * d_base[i*stride .. i*stride + block_len).  Same semantics as above. */
 int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t block_len, size_t n,

@@ -678,6 +678,11 @@ int lv_crc32c_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const 
 
 size_t lv_crc32c_workspace_bytes(size_t n) { return sort_ws_bytes(n); }
 
+int lv_crc32c_hint_needs_join(const lv_batch_hint *hint, size_t n, uint32_t cus) {
+    if (!hint) return 1;
+    return hint_needs_join(*hint, n, cus) ? 1 : 0;
+}
+
 int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, const uint32_t *d_len,
                                 const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
                                 const lv_batch_hint *hint, void *d_workspace, size_t workspace_bytes, void *stream) {

@@ -184,3 +184,77 @@ def test_device_counters_query():
     assert L.lv_device_counters(0, None, 3) != 0
     assert L.lv_device_counters(0, None, 0) == 0
     assert set(lvgpu.device_counters(0)) == {"h2d", "d2h", "allocs"}
+
+
+def _ceil_log2(x):
+    return 0 if x <= 1 else (x - 1).bit_length()
+
+
+def _split_rule(L, total, pmin=12, maxp=4096):
+    """lvk::split_rule (csrc/lvk/sort.h) in Python: (pieces, log2 piece length)."""
+    if L <= 16384:
+        return 0, 0
+    q = max(_ceil_log2(total // 16384), _ceil_log2((L + maxp - 1) // maxp), pmin)
+    q = min(q, 31)
+    if L <= (2 << q):
+        return 0, 0
+    return (L + (1 << q) - 1) >> q, q
+
+
+def _needs_join(lens, cus, fused_max=1024, waves=16):
+    """Whether the device launches combine_long_kernel with work to do: a
+    split buffer that the fused small-batch kernel does not join in place
+    (crc32c_fused_small_kernel's unit layout, csrc/classes.hip), or any split
+    buffer on the sorted path."""
+    total = sum(lens)
+    sp = [_split_rule(L, total) for L in lens]
+    if not any(m for m, _ in sp):
+        return False
+    if len(lens) > fused_max:
+        return True
+    units = [m if m else 1 for m, _ in sp]
+    pre = [0]
+    for u in units[:-1]:
+        pre.append(pre[-1] + u)
+    nunits = sum(units)
+    onepass = nunits <= 4 * waves * cus
+    S = 4 * ((nunits + 4 * cus - 1) // (4 * cus)) if onepass else 1
+    pb = min(max(_ceil_log2(total // 16384), 12), 31)
+    for (m, p), pr in zip(sp, pre):
+        local = onepass and m and p == pb and pr // S == (pr + m - 1) // S
+        if m and not local:
+            return True
+    return False
+
+
+def test_hint_join_decision_matches_the_device_layout():
+    """lv_crc32c_hint_needs_join (the host half of lv_crc32c_batch_device_hint)
+    leaves the join out exactly when the device would find nothing to join:
+    uniform batches against a Python replica of split_rule and the fused
+    kernel's unit layout; other batches whenever the longest buffer cannot
+    split (conservative otherwise)."""
+    import random
+    L = lvgpu.lib()
+    L.lv_crc32c_hint_needs_join.restype = ctypes.c_int
+    L.lv_crc32c_hint_needs_join.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32]
+    rng = random.Random(404)
+    cases = [(1024, 65536, 256, False), (1, 16 << 20, 256, True), (16, 1 << 20, 256, True), (300, 4096, 256, False),
+             (64, 16 << 20, 256, True), (2048, 65536, 256, True), (4096, 16384, 256, False)]
+    for _ in range(3000):
+        n = rng.choice([1, 2, 3, 7, 16, 64, 100, 255, 256, 512, 1000, 1024, 1025, 4096])
+        size = rng.choice([rng.randrange(0, 70000), 1 << rng.randrange(10, 25), rng.randrange(1, 1 << 24)])
+        cases.append((n, size, rng.choice([64, 80, 256, 304]), None))
+    for n, size, cus, want in cases:
+        h = lvgpu.BatchHint(n * size, size, 1)
+        got = L.lv_crc32c_hint_needs_join(ctypes.addressof(h), n, cus)
+        ref = _needs_join([size] * n, cus)
+        assert bool(got) == ref, (n, size, cus)
+        if want is not None:
+            assert ref == want, (n, size, cus)
+    for _ in range(500):  # non-uniform: join iff the longest buffer can split
+        n = rng.randrange(1, 3000)
+        lens = [rng.randrange(0, 1 << rng.randrange(4, 22)) for _ in range(n)]
+        h = lvgpu.hint_for(lens)
+        got = L.lv_crc32c_hint_needs_join(ctypes.addressof(h), n, 256)
+        assert bool(got) == (_split_rule(max(lens), sum(lens))[0] > 0)
+        assert bool(got) >= _needs_join(lens, 256)  # never leaves out a join the device needs
