@@ -16,7 +16,11 @@
 // ~180 scalar instructions per set of 64 keys fewer) measured the same.  The
 // waves sit in s_waitcnt 56 % of their cycles (SQ_WAIT_ANY): each set's span
 // load waits for the set's metadata, so a set costs one exposed memory round
-// trip per wave at full occupancy.
+// trip per wave at full occupancy.  Prefetching the next set's span one
+// set ahead into a second LDS stage by LDS-DMA (global_load_lds_dwordx4, two
+// 2.5 KiB stages per wave, 7 workgroups per CU) was correct but slower:
+// 145 -> 172 us on the offsets API, packed u32 unchanged
+// (profiles/r04/hash_glds/) -- so the round trip is not the bound either.
 // The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
 // requests the next set's metadata ahead, and stores each result one set
 // late, after the next set's loads, so no wait includes a store.  (A
@@ -77,9 +81,7 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 }
 
 // Hash of this lane's key of one wave-set of 64 keys (metadata already
-// loaded); span is the wave's LDS stage.  NOSTAGE: read the keys from
-// memory (the LDS-DMA kernel's sets that its stage cannot take).
-template <bool NOSTAGE = false>
+// loaded); span is the wave's LDS stage.
 __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, uint32_t *span, bool valid,
                                              uint64_t o, uint32_t L, uint32_t sdv, uint32_t lane,
                                              uint32_t *pout, uint32_t pval, bool pst) {
@@ -91,28 +93,23 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
     // stages the granules spanning its 64 keys through LDS with coalesced
     // 16-B loads, instead of 64 lanes gathering byte-aligned keys.  Waves
     // whose keys span more than kSpanBytes read keys straight from memory.
-    uint64_t lo = 0, hi = 0, lo16 = 0;
-    bool staged = false;
-    if constexpr (!NOSTAGE) {  // (no cross-lane step when called from divergent code)
 #if LVK_HASH_SPAN_READLANE
-        // Candidate span from the first and the last lane of the wave (keys
-        // are usually packed in order); the wave stages it only if every key
-        // lies inside it.  Two lane reads and one ballot instead of two
-        // 64-bit six-step shuffle reductions.
-        const uint64_t act = __ballot(valid);
-        const int last = act ? 63 - __builtin_clzll(act) : 0;
-        lo = __shfl(o, 0);
-        hi = __shfl(o + L, last);
-        lo16 = lo & ~15ull;
-        const bool inside = !L || (o >= lo && o + L <= hi);
-        staged = act && hi > lo && hi - lo16 <= kSpanBytes && __all(inside);  // wave-uniform
+    // Candidate span from the first and the last lane of the wave (keys are
+    // usually packed in order); the wave stages it only if every key lies
+    // inside it.  Two lane reads and one ballot instead of two 64-bit
+    // six-step shuffle reductions.
+    const uint64_t act = __ballot(valid);
+    const int last = act ? 63 - __builtin_clzll(act) : 0;
+    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool inside = !L || (o >= lo && o + L <= hi);
+    const bool staged = act && hi > lo && hi - lo16 <= kSpanBytes && __all(inside);  // wave-uniform
 #else
-        lo = wave_min_u64(L ? o : ~0ull);
-        hi = wave_max_u64(L ? o + L : 0ull);
-        lo16 = lo & ~15ull;
-        staged = lo != ~0ull && hi - lo16 <= kSpanBytes;  // wave-uniform
+    const uint64_t lo = wave_min_u64(L ? o : ~0ull);
+    const uint64_t hi = wave_max_u64(L ? o + L : 0ull);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool staged = lo != ~0ull && hi - lo16 <= kSpanBytes;  // wave-uniform
 #endif
-    }
     if (staged) {
         const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -338,156 +335,8 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     }
 }
 
-// ---- the LDS-DMA form (LVK_HASH_GLDS) ----
-// The kernel above pays one exposed memory round trip per set: a set's span
-// load can only be issued once the set's metadata is in, and the wave then
-// waits for it (SQ_WAIT_ANY 56 % of wave cycles, profiles/r04/hash_pmc/).
-// Here the NEXT set's span is requested while this set hashes: its bytes go
-// straight to a second LDS stage by global_load_lds_dwordx4 (no registers
-// held), so a set costs max(latency, compute) instead of their sum.  Two
-// stages of kGStage bytes per wave bound the span a wave stages (64 keys of
-// <= 40 B on average); sets with a longer span, or keys out of order, read
-// their keys from memory as in hash_set.  LDS: 4 waves x 2 stages x (2,560 +
-// 80) B = 21 KiB per workgroup, 7 workgroups per CU.
-constexpr uint32_t kGStage = 2560;                 // bytes of one stage (160 granules)
-constexpr uint32_t kGStageWords = kGStage / 4 + kSpanPad;
-constexpr uint64_t kGWgsPerCu = 7;
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-
-struct GSpan {
-    uint64_t lo16;
-    uint32_t nch;
-    bool staged;
-};
-
-__device__ __forceinline__ GSpan gspan_of(bool valid, uint64_t o, uint32_t L) {
-    const uint64_t act = __ballot(valid);
-    const int last = act ? 63 - __builtin_clzll(act) : 0;
-    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
-    GSpan g;
-    g.lo16 = lo & ~15ull;
-    const bool inside = !L || (o >= lo && o + L <= hi);
-    g.staged = act && hi > lo && hi - g.lo16 <= kGStage && __all(inside);  // wave-uniform
-    g.nch = g.staged ? static_cast<uint32_t>((hi - g.lo16 + 15) >> 4) : 0u;
-    return g;
-}
-
-// The span's granules into `stage` (lane-linear: chunk c at byte 16 c), up
-// to three 1-KiB LDS-DMA instructions, lanes past the span masked off.
-__device__ __forceinline__ void gspan_issue(const uint8_t *__restrict__ base, const GSpan &g, uint32_t *stage,
-                                            uint32_t lane) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(base + g.lo16);
-#pragma unroll
-    for (uint32_t k = 0; k < 3; ++k) {
-        if (64u * k < g.nch) {  // wave-uniform
-            const uint32_t c = lane + 64u * k;
-            if (c < g.nch)
-                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + c), (lds_void_t *)(stage + 256u * k), 16, 0, 0);
-        }
-    }
-}
-
-// A staged key's words (<= 64-B keys), and the hash.rs:25-48 chain over them.
-struct KeyWords {
-    uint32_t w[kFastDw + 1];
-};
-
-__device__ __forceinline__ KeyWords staged_words(const uint32_t *stage, uint64_t lo16, uint64_t o, uint32_t L) {
-    KeyWords k;
-    const uint32_t bs = static_cast<uint32_t>(o & 3u);
-    const uint32_t ndw = (bs + L + 3) >> 2;
-    const uint32_t *sd = stage + ((o - bs - lo16) >> 2);
-#pragma unroll
-    for (uint32_t j = 0; j < kFastDw; ++j) k.w[j] = j < ndw ? sd[j] : 0u;
-    k.w[kFastDw] = 0u;
-    return k;
-}
-
-__device__ __forceinline__ uint32_t chain_words(const KeyWords &k, uint64_t o, uint32_t L, uint32_t sdv) {
-    uint32_t h = sdv ^ (kM * L);
-    const uint32_t bs = static_cast<uint32_t>(o & 3u);
-    const uint32_t nw = L >> 2;
-    uint32_t tw = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kFastDw; ++j) {
-        const uint32_t wj = funnel(k.w[j + 1], k.w[j], bs);
-        if (j < nw)
-            h = mix(h, wj);
-        else if (j == nw)
-            tw = wj;
-    }
-    const uint32_t diff = L - 4 * nw;
-    if (diff) {
-        if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
-        if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;
-        h += tw & 0xffu;
-        h *= kM;
-        h ^= h >> 24;
-    }
-    return h;
-}
-
-template <typename Meta>
-__global__ void __launch_bounds__(256) hash_kernel_glds(const uint8_t *__restrict__ base, Meta meta,
-                                                        uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage[4][2][kGStageWords];
-    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
-    if (set * 64u >= n) return;  // wave-uniform
-    // prologue: set 0's metadata and span, set 1's metadata
-    uint64_t o;
-    uint32_t L, sd;
-    meta.get(meta.load(set * 64u + lane, n, lane), set * 64u + lane, n, lane, o, L, sd);
-    GSpan g = gspan_of(set * 64u + lane < n, o, L);
-    if (g.staged) gspan_issue(base, g, stage[wv][0], lane);
-    MetaRaw nx{};
-    bool more = (set + W) * 64u < n;
-    if (more) nx = meta.load((set + W) * 64u + lane, n, lane);
-    for (uint32_t k = 0;; ++k) {
-        const uint64_t i = set * 64u + lane;
-        const bool valid = i < n;
-        const bool fast = valid && L && ((o & 3u) + L + 3) / 4 <= kFastDw;
-        // 1. this set's words from its stage (its LDS-DMA and the next
-        //    metadata were issued one set ago)
-        KeyWords kw{};
-        if (g.staged) {  // wave-uniform
-            __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the stage has landed (expcnt, lgkmcnt untouched)
-            if (fast) kw = staged_words(stage[wv][k & 1u], g.lo16, o, L);
-        }
-        // 2. the next set: its span requested now, into the other stage
-        const uint64_t nset = set + W;
-        uint64_t on = 0;
-        uint32_t Ln = 0, sdn = 0;
-        GSpan gn{};
-        if (more) {
-            meta.get(nx, nset * 64u + lane, n, lane, on, Ln, sdn);
-            gn = gspan_of(nset * 64u + lane < n, on, Ln);
-            if (gn.staged) gspan_issue(base, gn, stage[wv][(k + 1u) & 1u], lane);
-        }
-        const bool more2 = more && (nset + W) * 64u < n;
-        if (more2) nx = meta.load((nset + W) * 64u + lane, n, lane);
-        // 3. this set's hashes while that DMA is in flight
-        uint32_t h;
-        if (g.staged && fast)
-            h = chain_words(kw, o, L, sd);
-        else  // keys from memory: a long key, or a set its stage cannot take
-            h = hash_set<true>(base, nullptr, valid, o, L, sd, lane, out, 0u, false);
-        if (valid) out[i] = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
-        if (!more) break;
-        set = nset;
-        o = on;
-        L = Ln;
-        sd = sdn;
-        g = gn;
-        more = more2;
-    }
-}
-
 // persistent grid: 8 workgroups (32 waves) per CU at most
-uint32_t hash_grid(size_t n, uint64_t wgs_per_cu = kWgsPerCu) {
+uint32_t hash_grid(size_t n) {
     static std::atomic<int> cus_cache[64];
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) cus = cus_cache[dev].load(std::memory_order_relaxed);
@@ -495,7 +344,7 @@ uint32_t hash_grid(size_t n, uint64_t wgs_per_cu = kWgsPerCu) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
         if (dev >= 0 && dev < 64) cus_cache[dev].store(cus, std::memory_order_relaxed);
     }
-    const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * wgs_per_cu;
+    const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * kWgsPerCu;
     return static_cast<uint32_t>(want < cap ? want : cap);
 }
 
@@ -533,14 +382,9 @@ int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const ui
     if (!d_arena || !d_off || !d_len || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
     if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
-    if (LVK_HASH_GLDS)
-        hipLaunchKernelGGL(lvh::hash_kernel_glds<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n, lvh::kGWgsPerCu)), dim3(256),
-                           0, static_cast<hipStream_t>(stream), d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed}, d_out,
-                           static_cast<uint32_t>(n), flags);
-    else
-        hipLaunchKernelGGL(lvh::hash_kernel<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
-                           static_cast<hipStream_t>(stream), d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed}, d_out,
-                           static_cast<uint32_t>(n), flags);
+    hipLaunchKernelGGL(lvh::hash_kernel<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed}, d_out,
+                       static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
 }
 
@@ -555,23 +399,14 @@ int lv_hash_batch_packed(const uint8_t *d_arena, const void *d_bounds, uint32_t 
     if (reinterpret_cast<uintptr_t>(d_bounds) % bound_bytes)
         return lvgpu_internal::set_error(LV_ERR_INVALID, "bounds must be aligned to bound_bytes");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const lvh::PackedMeta<uint32_t> m32{static_cast<const uint32_t *>(d_bounds), d_seed};
-    const lvh::PackedMeta<uint64_t> m64{static_cast<const uint64_t *>(d_bounds), d_seed};
-    if (LVK_HASH_GLDS) {
-        const dim3 g(lvh::hash_grid(n, lvh::kGWgsPerCu));
-        if (bound_bytes == 4)
-            hipLaunchKernelGGL(lvh::hash_kernel_glds<lvh::PackedMeta<uint32_t>>, g, dim3(256), 0, s, d_arena, m32, d_out,
-                               static_cast<uint32_t>(n), flags);
-        else
-            hipLaunchKernelGGL(lvh::hash_kernel_glds<lvh::PackedMeta<uint64_t>>, g, dim3(256), 0, s, d_arena, m64, d_out,
-                               static_cast<uint32_t>(n), flags);
-    } else if (bound_bytes == 4) {
+    if (bound_bytes == 4)
         hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint32_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
-                           m32, d_out, static_cast<uint32_t>(n), flags);
-    } else {
+                           lvh::PackedMeta<uint32_t>{static_cast<const uint32_t *>(d_bounds), d_seed}, d_out,
+                           static_cast<uint32_t>(n), flags);
+    else
         hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint64_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
-                           m64, d_out, static_cast<uint32_t>(n), flags);
-    }
+                           lvh::PackedMeta<uint64_t>{static_cast<const uint64_t *>(d_bounds), d_seed}, d_out,
+                           static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
 }
 

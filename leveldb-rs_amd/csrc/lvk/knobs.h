@@ -37,7 +37,6 @@
     defined(LVK_FUSED_LOCAL_JOIN) || \
     defined(LVK_EXP_SEAL_COMPACT) || \
     defined(LVK_HASH_SPAN_READLANE) || \
-    defined(LVK_HASH_GLDS) || \
     defined(LVK_HASH_WGS_PER_CU))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
@@ -113,9 +112,6 @@
 #endif
 #ifndef LVK_FUSED_LOCAL_JOIN  // fused small-batch kernel: one-pass batches join workgroup-local split buffers in place
 #define LVK_FUSED_LOCAL_JOIN 1
-#endif
-#ifndef LVK_HASH_GLDS  // hash: the next set's span prefetched into a second LDS stage by LDS-DMA
-#define LVK_HASH_GLDS 0
 #endif
 #ifndef LVK_HASH_SPAN_READLANE  // hash: a wave's span from its first and last lanes (0: two wave reductions)
 #define LVK_HASH_SPAN_READLANE 1

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/hash_glds/; the switch it measured was then retired with its code.)
 # Round 4: the LDS-DMA hash kernel (LVK_HASH_GLDS=1: the next set's span
 # prefetched into a second LDS stage) -- parity under the hash tests, then the
 # hash bench alternated with the product library.  usage: tools/r04_hash_glds_ab.sh OUTDIR
