@@ -5,8 +5,14 @@ straddling split buffers), the length sort + class kernel (n > 1,024, one-key
 batches, split long buffers joined by combine_long_kernel) -- on batches
 drawn from one generator: buffer counts 1-6,000, lengths from empty to 8 MiB
 in a mix of size classes, byte-packed, 256-B-aligned or overlapping offsets,
-seeded or not, masked or not, library or caller workspace.  Every output is
-checked bit-exact (the C restatement of crc32c.rs in oracle/)."""
+seeded or not, masked or not, library or caller workspace, with or without
+the exact host-side length hint (lv_crc32c_batch_device_hint, whose join
+decision is checked against the kernels it launched).  Every output is
+checked bit-exact (the C restatement of crc32c.rs in oracle/).
+LVGPU_STRESS_TRIALS sets the number of trials (default 40)."""
+import ctypes
+import os
+
 import numpy as np
 import pytest
 
@@ -51,7 +57,10 @@ def _batch(rng):
     return lens, offs, end, layout
 
 
-@pytest.mark.parametrize("trial", range(40))
+TRIALS = int(os.environ.get("LVGPU_STRESS_TRIALS", "40"))
+
+
+@pytest.mark.parametrize("trial", range(TRIALS))
 def test_offsets_api_random_sweep(torch_dev, trial):
     torch, dev = torch_dev
     rng = np.random.default_rng(77_000 + trial)
@@ -64,14 +73,26 @@ def test_offsets_api_random_sweep(torch_dev, trial):
     o = torch.from_numpy(offs).to(dev)
     ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
     sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
-    if caller:
-        ws = torch.full((lvgpu.workspace_bytes(n),), 0xA5, dtype=torch.uint8, device=dev)
+    hinted = bool(np.random.default_rng(91_000 + trial).integers(0, 2))  # (its own stream: the batches stay round 3's)
+    ws = torch.full((lvgpu.workspace_bytes(n),), 0xA5, dtype=torch.uint8, device=dev) if caller else None
+    if hinted:
+        hint = lvgpu.hint_for(lens)
+        out = lvgpu.batch_hint(arena, o, ln, hint, seed=sd, masked=masked, workspace=ws)
+    elif caller:
         out = lvgpu.batch_ws(arena, o, ln, ws, sd, masked=masked)
     else:
         out = lvgpu.batch(arena, o, ln, sd, masked=masked)
     kern = lvgpu.last_kernel()
-    assert kern == ("crc32c_fused_small_kernel+combine_long_kernel" if n <= 1024 else "sort+crc32c_classes_kernel+combine_long_kernel")
+    base = "crc32c_fused_small_kernel" if n <= 1024 else "sort+crc32c_classes_kernel"
+    join = True
+    if hinted:
+        L = lvgpu.lib()
+        L.lv_crc32c_hint_needs_join.restype = ctypes.c_int
+        L.lv_crc32c_hint_needs_join.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32]
+        join = bool(L.lv_crc32c_hint_needs_join(ctypes.addressof(hint), n,
+                                                torch.cuda.get_device_properties(dev).multi_processor_count))
+    assert kern == base + ("+combine_long_kernel" if join else ""), (kern, hinted)
     got = out.cpu().numpy().view(np.uint32)
     want = oracle_batch(arena.cpu().numpy().tobytes(), offs, lens, seeds, masked)
     bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, (n, layout, seeded, masked, caller, [(int(i), int(lens[i])) for i in bad[:8]])
+    assert bad.size == 0, (n, layout, seeded, masked, caller, hinted, [(int(i), int(lens[i])) for i in bad[:8]])
