@@ -528,13 +528,18 @@ def sweep_bench(args):
         ln = torch.full((n,), bl, dtype=torch.int32, device=dev)
         ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
         row = {"block_KiB": kib, "blocks": n}
+        hint = lvgpu.BatchHint(n * bl, bl, 1)  # uniform, nothing splits: the class kernel alone, no sort
         for api, fn in (("strided", lambda: lvgpu.batch_strided(arena, bl, bl, n, out=out)),
-                        ("offsets", lambda: lvgpu.batch_ws(arena, o, ln, ws, out=out))):
+                        ("offsets", lambda: lvgpu.batch_ws(arena, o, ln, ws, out=out)),
+                        ("offsets_hint", lambda: lvgpu.batch_hint(arena, o, ln, hint, out=out, workspace=ws))):
+            out.fill_(0)
             _, avg = _event_times(torch, fn, steps, warm)
             fn()
+            kern = lvgpu.last_kernel()
             torch.cuda.synchronize()
             k = 64
             base = 0 if api == "strided" else 13
+            row.setdefault("kernels", {})[api] = kern
             host = arena[:base + k * bl].cpu().numpy()
             want = np.zeros(k, dtype=np.uint32)
             ho = (np.arange(k, dtype=np.uint64) * bl + base).astype(np.uint64)

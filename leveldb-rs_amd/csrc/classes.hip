@@ -34,8 +34,13 @@ constexpr uint32_t kSmallRounds = LVK_SMALL_ROUNDS;  // small-class rounds per w
 template <bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, const uint4 *__restrict__ image,
                                                                   const uint32_t *ws) {
-    const uint32_t *cls = ws + kWsCls;
-    const bool ident = ws[kWsIdent] != 0u;  // sort_scatter skipped a one-key batch
+    // the class ranges: from the sort's workspace header, or (a hinted
+    // uniform batch that no sort ran for) from the host
+    const bool hostid = P.hident != 0u;
+    uint32_t cls[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) cls[k] = hostid ? P.hcls[k] : ws[kWsCls + k];
+    const bool ident = hostid || ws[kWsIdent] != 0u;  // sort_scatter skipped a one-key batch
     stage_tables(image);
     if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
     __syncthreads();
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         // that start together stream their pieces in lockstep, which reads
         // slower; stagger them as crc32c_blocks_kernel does (64 x 16 MiB:
         // 223 -> 201 us per call).
-        const uint64_t bytes = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];
+        const uint64_t bytes = hostid ? 0u : (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];
         if (4ull * np >= 3ull * (n23 + np) && bytes >= (64ull << 10) * grid * kWaves)
             for (uint32_t k = 0; k < wave * LVK_STAGGER; ++k) __builtin_amdgcn_s_sleep(32);
 #endif
@@ -664,6 +669,32 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
         // no initialisation: every workspace word the sort reads, it wrote first
     } else if (int rc = stream_ws(*c, s, n, &d_ws, &ws_lk)) {
         return rc;
+    }
+    if (hint && hint->uniform && n > lvk::kFusedMax) {
+        uint32_t p = 0;
+        if (host_split_rule(hint->max_len, hint->total_bytes, &p) == 0) {
+            // one sort key in index order and nothing to split: the class
+            // kernel alone, its class ranges from the host (no sort, no join)
+            lvk::Params P{};
+            P.base = reinterpret_cast<uint64_t>(d_arena);
+            P.off = d_off;
+            P.len = d_len;
+            P.seed = d_seed;
+            P.out = d_out;
+            P.n = n;
+            P.nplain = n;
+            P.flags = flags;
+            P.hident = 1;
+            const uint32_t L = hint->max_len;
+            const uint32_t cl = L <= 256u ? 0u : L <= 2048u ? 1u : L <= 32768u ? 2u : 3u;  // lvk::len_class
+            for (uint32_t k = 0; k < 4; ++k) {
+                P.hcls[k] = k <= cl ? 0u : static_cast<uint32_t>(n);
+                P.hcls[4 + k] = k == cl ? static_cast<uint32_t>(n) : 0u;
+            }
+            g_kernel = "crc32c_classes_kernel";
+            launch_classes(*c, d_seed != nullptr, P, reinterpret_cast<const uint32_t *>(d_ws), s);
+            return check_launch();
+        }
     }
     const bool join = hint ? hint_needs_join(*hint, n, static_cast<uint32_t>(c->cus)) : true;
     if (int rc = launch_binned(*c, d_ws, d_arena, d_off, d_len, d_seed, d_out, n, flags, s, join)) return rc;

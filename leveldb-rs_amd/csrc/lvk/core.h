@@ -320,6 +320,11 @@ struct Params {
     uint32_t *part;         // piece registers (long-buffer split of the offsets API)
     const uint32_t *mats;   // blocks kernel, FUSE: Shift_{j plen}, j < 2^pshift (32 column words each)
     const uint32_t *tabs;   // fused small-batch kernel: the byte tables Shift_{2^i}, 1,024 words each
+    // class kernel, lv_crc32c_batch_device_hint: a uniform batch none of whose
+    // buffers can split is one sort key in index order, known on the host --
+    // no sort runs; hcls holds the class ranges the sort would have written
+    uint32_t hident;
+    uint32_t hcls[8];
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of

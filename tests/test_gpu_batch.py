@@ -910,7 +910,24 @@ HINT_CASES = {
     "sorted_no_split": (lambda r: r.integers(0, 9000, 5000), "odd", False),    # the three-pass sort, no join
     "sorted_long": (lambda r: np.concatenate([r.integers(0, 5000, 3000), [3 << 20, 70000]]), "odd", True),
     "fused_long_ragged": (lambda r: np.concatenate([r.integers(0, 300, 100), [1 << 20, 5 << 20]]), "odd", True),
+    # uniform, > 1,024 buffers, nothing splits: the class kernel alone, no sort (class 0 .. 3)
+    "uniform_5000x100B": (lambda r: np.full(5000, 100), "odd", False),
+    "uniform_3000x1500B": (lambda r: np.full(3000, 1500), "packed", False),
+    "uniform_2000x16KiB": (lambda r: np.full(2000, 16384), "odd", False),
+    "uniform_8200x40000B": (lambda r: np.full(8200, 40000), "overlap", False),  # class 3, 8,200 > 2 x 40000 / 16384
+    "uniform_1025x0B": (lambda r: np.zeros(1025), "packed", False),
+    # uniform, > 1,024 buffers, split: the sort path and the join
+    "uniform_1100x160KiB": (lambda r: np.full(1100, 160 << 10), "overlap", True),
 }
+
+
+def _hint_kernel(n, hint, join):
+    """The launch lv_crc32c_batch_device_hint picks (classes.hip)."""
+    if n <= 1024:
+        return "crc32c_fused_small_kernel" + ("+combine_long_kernel" if join else "")
+    if hint.uniform and not join:
+        return "crc32c_classes_kernel"  # a host-known identity list: no sort
+    return "sort+crc32c_classes_kernel" + ("+combine_long_kernel" if join else "")
 
 
 @pytest.mark.parametrize("case", sorted(HINT_CASES))
@@ -927,13 +944,17 @@ def test_offsets_api_with_hint(torch_dev, case, seeded):
     make, layout, join = HINT_CASES[case]
     lens = np.asarray(make(rng), dtype=np.uint32)
     n = lens.size
-    gaps = rng.integers(0, 16, n) if layout == "odd" else np.zeros(n, dtype=np.int64)
-    offs = np.zeros(n, dtype=np.uint64)
-    pos = 0
-    for i in range(n):
-        pos += int(gaps[i])
-        offs[i] = pos
-        pos += int(lens[i])
+    if layout == "overlap":  # every buffer inside one window (keeps big batches' arenas small)
+        offs = rng.integers(0, 4096, n).astype(np.uint64)
+        pos = int(lens.max()) + 4096
+    else:
+        gaps = rng.integers(0, 16, n) if layout == "odd" else np.zeros(n, dtype=np.int64)
+        offs = np.zeros(n, dtype=np.uint64)
+        pos = 0
+        for i in range(n):
+            pos += int(gaps[i])
+            offs[i] = pos
+            pos += int(lens[i])
     arena = rng.integers(0, 256, pos + 16, dtype=np.uint8).tobytes()
     seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if seeded else None
     want = oracle_batch(arena, offs, lens, seeds, True)
@@ -947,7 +968,7 @@ def test_offsets_api_with_hint(torch_dev, case, seeded):
     kern = lvgpu.last_kernel()
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
-    assert ("combine_long_kernel" in kern) == join, kern
+    assert kern == _hint_kernel(n, hint, join), kern
     # the same call without the hint, and with a caller workspace
     ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
     out2 = lvgpu.batch_hint(a, o, ln, None, seed=sd, masked=True, workspace=ws)
