@@ -37,7 +37,10 @@
     defined(LVK_FUSED_LOCAL_JOIN) || \
     defined(LVK_EXP_SEAL_COMPACT) || \
     defined(LVK_HASH_SPAN_READLANE) || \
-    defined(LVK_HASH_WGS_PER_CU))
+    defined(LVK_HASH_WGS_PER_CU) || \
+    defined(LVK_HASH_DEEP) || \
+    defined(LVK_HASH_MASKED_META) || \
+    defined(LVK_WALK_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -118,6 +121,15 @@
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8
+#endif
+#ifndef LVK_HASH_DEEP  // hash: the next set's span in flight in registers while this set hashes (0: one set)
+#define LVK_HASH_DEEP 0
+#endif
+#ifndef LVK_HASH_MASKED_META  // hash: round 4's first form -- exec-masked metadata loads, the prefetch under `more`
+#define LVK_HASH_MASKED_META 0
+#endif
+#ifndef LVK_WALK_EXACT  // sorted_stream: the same unconditional loads in every step, so the waits count exactly
+#define LVK_WALK_EXACT 0
 #endif
 #ifndef LVK_EXP_SEAL_COMPACT  // experiment (no trailers): the seal stores its masked crcs to a per-block array
 #define LVK_EXP_SEAL_COMPACT 0

@@ -127,9 +127,18 @@ __device__ __forceinline__ void fix_rbatch(const RGeo &q, uint32_t nbw, uint32_t
     }
 }
 
+// Granules outside a buffer load from this zero block (load_rbatch_al, and
+// with LVK_WALK_EXACT every lane's tail).
+static __device__ __attribute__((aligned(256))) uint4 g_zero_granules[16];  // zero-initialised
+
 // The granule after the last whole granule (k = (alow+len) & 15 bytes of it
 // belong to the buffer).
 __device__ __forceinline__ uint4 load_rtail(const RGeo &q, uint32_t gl) {
+    if constexpr (LVK_WALK_EXACT) {  // every lane loads (others: the zero block): no exec-masked load
+        const bool on = gl == 0 && ((q.alow() + q.len) & 15u);
+        return load16_rt(on ? q.abase() + (static_cast<uint64_t>(q.ng()) << 4)
+                            : reinterpret_cast<uint64_t>(&g_zero_granules[gl & 15u]));
+    }
     if (gl == 0 && ((q.alow() + q.len) & 15u)) return load16_rt(q.abase() + (static_cast<uint64_t>(q.ng()) << 4));
     return make_uint4(0, 0, 0, 0);
 }
@@ -228,7 +237,6 @@ __device__ __forceinline__ uint32_t round_jfix_al(const RGeo &q, uint32_t nbw) {
 // zero block instead of being zeroed after the load, so only the head batches
 // need a fix-up pass (fix_rbatch_al); the load address costs the same selects
 // a clamp would.
-static __device__ __attribute__((aligned(256))) uint4 g_zero_granules[16];  // zero-initialised
 
 // jfix: the round's last head batch (round_jfix_al).  Past it and before the
 // last batch every group's granules lie inside its buffer (a group's rows end
@@ -451,7 +459,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     uint32_t jfix = AL ? round_jfix_al<NU>(q, nbw) : round_jfix<G>(q, nbw);
     uint32_t pad = round_pad<G, NU>(q, nbw);
     RGeo qn = q;
-    if (rhon < nr) qn = src.load(P, rhon * K + grp);
+    if (LVK_WALK_EXACT || rhon < nr) qn = src.load(P, rhon * K + grp);
     uint32_t nbwn = 0;
     uint4 tail;
     uint2 tr;
@@ -503,6 +511,10 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         const bool lastj = j + 1 == nbw;
         const bool more = rhon < nr;
         if (!lastj) {
+            if constexpr (LVK_WALK_EXACT) {  // the same loads as the last step's (see the knob)
+                tail = load_rtail(q, gl);
+                tr = src.trailer(q, gl);
+            }
             if constexpr (AL)
                 load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt, Src::kAlMid ? jfix : 0xffffffffu);
             else
@@ -510,7 +522,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         } else {
             tail = load_rtail(q, gl);  // consumed after this batch's fold
             tr = src.trailer(q, gl);
-            if (more) {
+            if (LVK_WALK_EXACT || more) {  // (exact: past the list, qn is the clamped last entry)
                 if constexpr (AL) {
                     nbwn = round_nbw_al<NU>(al_geo(qn));
                     load_rbatch_al<NU>(qn, nbwn, 0, gl, nxt);
@@ -563,7 +575,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         }
         pad = round_pad<G, NU>(q, nbw);
         rhon = next();
-        if (rhon < nr) qn = src.load(P, rhon * K + grp);
+        if (LVK_WALK_EXACT || rhon < nr) qn = src.load(P, rhon * K + grp);  // (src.load clamps)
         j = 0;
         return false;
     };
