@@ -21,12 +21,19 @@
 // 2.5 KiB stages per wave, 7 workgroups per CU) was correct but slower:
 // 145 -> 172 us on the offsets API, packed u32 unchanged
 // (profiles/r04/hash_glds/) -- so the round trip is not the bound either.
-// The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
-// requests the next set's metadata ahead, and stores each result one set
-// late, after the next set's loads, so no wait includes a store.  (A
-// two-deep form -- the next set's span in flight in registers while this
-// set hashes from LDS, metadata two sets ahead, 64 VGPRs at 8 waves/SIMD --
-// measured 106 vs 117 G keys/s, three interleaved reps: not kept.)
+// The grid is persistent: a wave walks sets of 64 keys.  Round 4 found
+// what bounded it: the metadata prefetch was exec-masked (and under a
+// `more` branch), so the compiler could not count the loads in flight and
+// the set's first wait was a vmcnt(0) covering the prefetch just issued --
+// two exposed round trips per set.  The product kernel (hash_kernel_deep,
+// LVK_HASH_DEEP) issues every load from every lane (clamped indices, a
+// dummy block for span chunks past the span and for invalid lanes'
+// results), so every wait counts exactly, and runs two sets deep: set s
+// hashes from LDS while set s + W's span is in flight in registers and set
+// s + 2W's metadata behind it (80 VGPRs, 6 workgroups per CU):
+// 0.32 -> 0.46 of 8 TB/s in key bytes on the same box (profiles/r04/
+// new_ab/, hash_wait/; the one-set kernel with exact waits 0.29 -> 0.32).
+// (Round 2's two-deep form kept the masked loads: 106 vs 117 G keys/s.)
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -447,13 +454,16 @@ __global__ void __launch_bounds__(256) hash_kernel_deep(const uint8_t *__restric
         L = L1;
         sd = sd1;
         sp = sp1;
-#pragma unroll
-        for (uint32_t k = 0; k < kSpanCh; ++k) t[k] = t1[k];
+        static_assert(kSpanCh == 4, "span registers: four 16-B chunks per lane");
+        t[0] = t1[0];
+        t[1] = t1[1];
+        t[2] = t1[2];
+        t[3] = t1[3];
         mn = m2;
     }
 }
 
-// persistent grid: 8 workgroups (32 waves) per CU at most
+// persistent grid: LVK_HASH_WGS_PER_CU workgroups (of 4 waves) per CU at most
 uint32_t hash_grid(size_t n) {
     static std::atomic<int> cus_cache[64];
     int dev = 0, cus = 0;

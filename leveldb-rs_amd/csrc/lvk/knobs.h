@@ -119,17 +119,17 @@
 #ifndef LVK_HASH_SPAN_READLANE  // hash: a wave's span from its first and last lanes (0: two wave reductions)
 #define LVK_HASH_SPAN_READLANE 1
 #endif
-#ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
-#define LVK_HASH_WGS_PER_CU 8
+#ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU (the two-deep kernel's 80 VGPRs fit 6)
+#define LVK_HASH_WGS_PER_CU 6
 #endif
 #ifndef LVK_HASH_DEEP  // hash: the next set's span in flight in registers while this set hashes (0: one set)
-#define LVK_HASH_DEEP 0
+#define LVK_HASH_DEEP 1
 #endif
 #ifndef LVK_HASH_MASKED_META  // hash: round 4's first form -- exec-masked metadata loads, the prefetch under `more`
 #define LVK_HASH_MASKED_META 0
 #endif
 #ifndef LVK_WALK_EXACT  // sorted_stream: the same unconditional loads in every step, so the waits count exactly
-#define LVK_WALK_EXACT 0
+#define LVK_WALK_EXACT 1
 #endif
 #ifndef LVK_EXP_SEAL_COMPACT  // experiment (no trailers): the seal stores its masked crcs to a per-block array
 #define LVK_EXP_SEAL_COMPACT 0

@@ -133,8 +133,9 @@ static __device__ __attribute__((aligned(256))) uint4 g_zero_granules[16];  // z
 
 // The granule after the last whole granule (k = (alow+len) & 15 bytes of it
 // belong to the buffer).
+template <bool EXACT = false>
 __device__ __forceinline__ uint4 load_rtail(const RGeo &q, uint32_t gl) {
-    if constexpr (LVK_WALK_EXACT) {  // every lane loads (others: the zero block): no exec-masked load
+    if constexpr (EXACT) {  // every lane loads (others: the zero block): no exec-masked load
         const bool on = gl == 0 && ((q.alow() + q.len) & 15u);
         return load16_rt(on ? q.abase() + (static_cast<uint64_t>(q.ng()) << 4)
                             : reinterpret_cast<uint64_t>(&g_zero_granules[gl & 15u]));
@@ -388,6 +389,7 @@ struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
+    static constexpr bool kExact = true;      // sorted_stream: exact wait counts (LVK_WALK_EXACT)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         if (!ident) return load_rgeo<SEEDED>(P, e);
@@ -427,15 +429,28 @@ struct SortedList {
 // stride, or a workgroup's shared pool) until it returns rho >= nr.  Batches
 // are prefetched one ahead, across rounds, in two ping-pong register slots;
 // all control is wave-uniform.  Results are staged in LDS (g_oidx/g_ocrc)
-// and stored every G rounds.  (Issuing the same loads in every step --
-// entries and tail re-read each batch -- measured 4-5 % slower: the extra
-// loads and spills cost more than the conservative wait counts they remove.)
+// and stored every G rounds.
+// Wait counts (round 4): the compiler counts loads in flight per path and
+// merges paths by their minimum, so a load that only some paths issue (an
+// exec-masked tail load, the next round's loads under `more`) makes the
+// fold of a batch wait with vmcnt(0..3) -- i.e. also for the prefetch
+// issued just before it, one exposed round trip per batch.  With
+// Src::kExact every step issues the same unconditional loads (tail and
+// trailer every step, the next round's entries and first batch always,
+// clamped), the waits count exactly (vmcnt(8..5) in the class kernel's
+// small-class loops) and the prefetch stays in flight: C3 via offsets
+// 0.67 -> 0.70, WAL scan 0.58 -> 0.61, C2 / C4 +1 % (profiles/r04/new_ab/).
+// The table walk (tail + two trailer dwords per step, 9 % slower) and the
+// fused small-batch kernel (+1 us) keep the masked form.  (Round 2 issued the
+// same loads in every step by re-reading the entries each batch as well:
+// 4-5 % slower from the extra loads and spills.)
 // The image is always the G = 16 one: groups of G = 1 and 4 take their
 // row-shift and merge tables from the plain combine tables.
 template <int G, class Src, class Next, uint32_t ALR = kAlRows>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {
     constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
+    constexpr bool EX = LVK_WALK_EXACT && Src::kExact;  // exact wait counts (below)
     constexpr uint32_t NU = AL ? ALR : U;              // rows per batch
     // Latin row shift Shift_{16 G NU}: region A's second half (the image's W4
     // for NU = 4; Shift_768 in the table image for NU = 3) or region B's W2
@@ -459,7 +474,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     uint32_t jfix = AL ? round_jfix_al<NU>(q, nbw) : round_jfix<G>(q, nbw);
     uint32_t pad = round_pad<G, NU>(q, nbw);
     RGeo qn = q;
-    if (LVK_WALK_EXACT || rhon < nr) qn = src.load(P, rhon * K + grp);
+    if (EX || rhon < nr) qn = src.load(P, rhon * K + grp);
     uint32_t nbwn = 0;
     uint4 tail;
     uint2 tr;
@@ -484,7 +499,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             load_rbatch_al<NU>(q, nbw, nbw > 1u ? 1u : 0u, gl, v1, jfix);
             load_rbatch_al<NU>(q, nbw, nbw > 2u ? 2u : 0u, gl, v2, jfix);
             load_rbatch_al<NU>(q, nbw, nbw > 3u ? 3u : 0u, gl, v3, jfix);
-            tail = load_rtail(q, gl);
+            tail = load_rtail<EX>(q, gl);
             tr = src.trailer(q, gl);
             auto fold_j = [&](uint4(&v)[NU], uint32_t jj) {
                 if (!LVK_EXP_NOFIX && jj <= jfix) fix_rbatch_al<NU>(q, nbw, jj, gl, v);
@@ -511,8 +526,8 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         const bool lastj = j + 1 == nbw;
         const bool more = rhon < nr;
         if (!lastj) {
-            if constexpr (LVK_WALK_EXACT) {  // the same loads as the last step's (see the knob)
-                tail = load_rtail(q, gl);
+            if constexpr (EX) {  // the same loads as the last step's (see the knob)
+                tail = load_rtail<EX>(q, gl);
                 tr = src.trailer(q, gl);
             }
             if constexpr (AL)
@@ -520,9 +535,9 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             else
                 load_rbatch<G>(q, nbw, j + 1, gl, nxt);
         } else {
-            tail = load_rtail(q, gl);  // consumed after this batch's fold
+            tail = load_rtail<EX>(q, gl);  // consumed after this batch's fold
             tr = src.trailer(q, gl);
-            if (LVK_WALK_EXACT || more) {  // (exact: past the list, qn is the clamped last entry)
+            if (EX || more) {  // (exact: past the list, qn is the clamped last entry)
                 if constexpr (AL) {
                     nbwn = round_nbw_al<NU>(al_geo(qn));
                     load_rbatch_al<NU>(qn, nbwn, 0, gl, nxt);
@@ -575,7 +590,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         }
         pad = round_pad<G, NU>(q, nbw);
         rhon = next();
-        if (LVK_WALK_EXACT || rhon < nr) qn = src.load(P, rhon * K + grp);  // (src.load clamps)
+        if (EX || rhon < nr) qn = src.load(P, rhon * K + grp);  // (src.load clamps)
         j = 0;
         return false;
     };
