@@ -344,9 +344,9 @@ struct FusedUnits {
     static constexpr uint32_t kFlush = 16;
     static constexpr bool kAlMid = true;
     static constexpr bool kOneRound = LVK_FUSED_ONE_ROUND;  // sorted_stream: a one-round wave loads all batches at once
-    // exact wait counts (LVK_WALK_EXACT) measured 0.7-1.3 us slower on the
-    // few-long-buffer calls (profiles/r04/new_ab/long_*.json): kept masked
-    static constexpr bool kExact = false;
+    // wait-count modes 1 / 2 (walk.h) measured 0.7-1.3 / 0.5-0.9 us slower on
+    // the few-long-buffer calls (profiles/r04/new_ab/, mode2_ab/): masked
+    static constexpr uint32_t kExact = LVK_FUSED_EXACT;
     uint32_t nbuf;  // buffers (<= kFusedMax); P.n = units
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;

@@ -40,7 +40,9 @@
     defined(LVK_HASH_WGS_PER_CU) || \
     defined(LVK_HASH_DEEP) || \
     defined(LVK_HASH_MASKED_META) || \
-    defined(LVK_WALK_EXACT))
+    defined(LVK_WALK_EXACT) || \
+    defined(LVK_TABLE_EXACT) || \
+    defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
 #endif
 
@@ -128,8 +130,17 @@
 #ifndef LVK_HASH_MASKED_META  // hash: round 4's first form -- exec-masked metadata loads, the prefetch under `more`
 #define LVK_HASH_MASKED_META 0
 #endif
-#ifndef LVK_WALK_EXACT  // sorted_stream: the same unconditional loads in every step, so the waits count exactly
+// sorted_stream wait-count mode per source (walk.h): 0 = exec-masked loads,
+// 1 = the same unconditional loads every step, 2 = unconditional loads
+// within each path (no re-reads)
+#ifndef LVK_WALK_EXACT  // the class kernel's sorted lists (offsets API, WAL scan)
 #define LVK_WALK_EXACT 1
+#endif
+#ifndef LVK_TABLE_EXACT  // the SST table walk's verify (the seal keeps mode 0)
+#define LVK_TABLE_EXACT 2
+#endif
+#ifndef LVK_FUSED_EXACT  // the fused small-batch kernel
+#define LVK_FUSED_EXACT 0
 #endif
 #ifndef LVK_EXP_SEAL_COMPACT  // experiment (no trailers): the seal stores its masked crcs to a per-block array
 #define LVK_EXP_SEAL_COMPACT 0

@@ -389,7 +389,7 @@ struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
-    static constexpr bool kExact = true;      // sorted_stream: exact wait counts (LVK_WALK_EXACT)
+    static constexpr uint32_t kExact = LVK_WALK_EXACT;  // sorted_stream: wait-count mode (below)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         if (!ident) return load_rgeo<SEEDED>(P, e);
@@ -450,7 +450,10 @@ template <int G, class Src, class Next, uint32_t ALR = kAlRows>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {
     constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
-    constexpr bool EX = LVK_WALK_EXACT && Src::kExact;  // exact wait counts (below)
+    // exact wait counts (below): Src::kExact 0 = masked loads, 1 = the same
+    // unconditional loads every step (tail / trailer re-read), 2 =
+    // unconditional loads within each path only
+    constexpr bool EX = Src::kExact != 0, RELOAD = Src::kExact == 1;
     constexpr uint32_t NU = AL ? ALR : U;              // rows per batch
     // Latin row shift Shift_{16 G NU}: region A's second half (the image's W4
     // for NU = 4; Shift_768 in the table image for NU = 3) or region B's W2
@@ -526,7 +529,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         const bool lastj = j + 1 == nbw;
         const bool more = rhon < nr;
         if (!lastj) {
-            if constexpr (EX) {  // the same loads as the last step's (see the knob)
+            if constexpr (RELOAD) {  // the same loads as the last step's (see the knob)
                 tail = load_rtail<EX>(q, gl);
                 tr = src.trailer(q, gl);
             }

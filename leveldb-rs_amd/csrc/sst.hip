@@ -46,10 +46,12 @@ struct TableUnits {
     static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
     static constexpr bool kOneRound = false;
-    // exact wait counts (LVK_WALK_EXACT: the tail and trailer re-read every
-    // step) measured 9 % slower here (profiles/r04/exact_ab/: seal 0.67 ->
-    // 0.61, verify 0.69 -> 0.64), so the table walk keeps the masked loads
-    static constexpr bool kExact = false;
+    // Wait-count mode (walk.h sorted_stream): verify runs mode 2 (every load
+    // unconditional within its path: 0.689 -> 0.709), the seal keeps the
+    // masked loads (mode 2: 0.667 -> 0.639; mode 1, the tail and trailer
+    // re-read every step: seal 0.67 -> 0.61, verify 0.69 -> 0.64;
+    // profiles/r04/mode2_ab/, exact_ab/)
+    static constexpr uint32_t kExact = SEAL ? 0u : LVK_TABLE_EXACT;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
@@ -65,13 +67,26 @@ struct TableUnits {
         q.seed = 0;
         q.bid = valid ? static_cast<uint32_t>(ec) : 0xffffffffu;
         uint32_t t = 0;
-        if (SEAL && types && ok) t = types[ec];
+        if constexpr (kExact != 0) {
+            if (SEAL && types) t = ok ? types[ec] : 0u;  // every lane loads (ec is clamped)
+        } else if (SEAL && types && ok) {
+            t = types[ec];
+        }
         q.aux = (ok ? 1u : 0u) | (t << 8);
         return q;
     }
     // verify: the stored masked crc at the unit's end (two aligned dwords)
     __device__ __forceinline__ uint2 trailer(const RGeo &q, uint32_t gl) const {
-        if (SEAL || gl != 0 || !(q.aux & 1u)) return make_uint2(0, 0);
+        if (SEAL) return make_uint2(0, 0);
+        if constexpr (kExact != 0) {  // every lane loads two dwords (others: the zero block)
+            const bool on = gl == 0 && (q.aux & 1u);
+            const uint64_t end = q.a + q.len;
+            const uint32_t *w = on ? reinterpret_cast<const uint32_t *>(end & ~static_cast<uint64_t>(3))
+                                   : reinterpret_cast<const uint32_t *>(&g_zero_granules[0]);
+            const uint32_t w0 = w[0], w1 = w[(end & 3u) ? 1 : 0];  // (aligned: no dword past the stored crc)
+            return on ? make_uint2(w0, (end & 3u) ? w1 : 0u) : make_uint2(0, 0);
+        }
+        if (gl != 0 || !(q.aux & 1u)) return make_uint2(0, 0);
         const uint64_t end = q.a + q.len;
         const uint32_t *w = reinterpret_cast<const uint32_t *>(end & ~static_cast<uint64_t>(3));
         return make_uint2(w[0], (end & 3u) ? w[1] : 0u);
