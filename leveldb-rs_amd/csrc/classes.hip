@@ -34,12 +34,18 @@ constexpr uint32_t kSmallRounds = LVK_SMALL_ROUNDS;  // small-class rounds per w
 template <bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, const uint4 *__restrict__ image,
                                                                   const uint32_t *ws) {
-    // the class ranges: from the sort's workspace header, or (a hinted
-    // uniform batch that no sort ran for) from the host
-    const bool hostid = P.hident != 0u;
-    uint32_t cls[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) cls[k] = hostid ? P.hcls[k] : ws[kWsCls + k];
+    // The class ranges [start k, count 4 + k): the sort's workspace header,
+    // or -- a hinted uniform batch that no sort ran for (P.hident = its
+    // class + 1) -- every buffer in that one class.  Read or computed where
+    // used (an array of the eight selected values cost the kernel 24 VGPRs
+    // of spills and C3 via offsets 0.75 -> 0.67).
+    const uint32_t hc = P.hident;
+    const bool hostid = hc != 0u;
+    auto cls = [&](uint32_t k) -> uint32_t {
+        if (!hostid) return ws[kWsCls + k];
+        const uint32_t c = hc - 1u, nn = static_cast<uint32_t>(P.n);
+        return k < 4u ? (k <= c ? 0u : nn) : (k - 4u == c ? nn : 0u);
+    };
     const bool ident = hostid || ws[kWsIdent] != 0u;  // sort_scatter skipped a one-key batch
     stage_tables(image);
     if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
@@ -48,7 +54,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     const Lut L = make_lut(lane);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t grid = gridDim.x;
-    const uint32_t n23 = cls[6] + cls[7];
+    const uint32_t n23 = cls(6) + cls(7);
     // pieces of split long buffers (walked after classes 2+3; a split buffer
     // is longer than 16 KiB, so class 2 or 3, and n23 > 0 whenever there are
     // pieces)
@@ -68,7 +74,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
 #endif
 #if LVK_SMALL_ADAPT
     if (n23) {
-        const uint64_t rounds = (cls[4] + 63ull) / 64u + (cls[5] + 15ull) / 16u;
+        const uint64_t rounds = (cls(4) + 63ull) / 64u + (cls(5) + 15ull) / 16u;
         const uint64_t per = static_cast<uint64_t>(kSmallRounds) * gridDim.x;
         const uint64_t ns = (rounds + per - 1) / per;
         nsmall = static_cast<uint32_t>(ns < 1 ? 1 : (ns > kSmallWaves ? kSmallWaves : ns));
@@ -78,11 +84,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         const uint64_t sw = blockIdx.x * nsmall + wave, nsw = grid * nsmall;
         uint64_t k = 0;
         auto stride = [&]() { return sw + (++k) * nsw; };
-        if (cls[4]) {
-            sorted_stream<1>(sub_list(P, cls[0], cls[4]), SortedList<SEEDED>{ident}, lane, L, sw, stride);
+        if (cls(4)) {
+            sorted_stream<1>(sub_list(P, cls(0), cls(4)), SortedList<SEEDED>{ident}, lane, L, sw, stride);
             k = 0;
         }
-        if (cls[5]) sorted_stream<4>(sub_list(P, cls[1], cls[5]), SortedList<SEEDED>{ident}, lane, L, sw, stride);
+        if (cls(5)) sorted_stream<4>(sub_list(P, cls(1), cls(5)), SortedList<SEEDED>{ident}, lane, L, sw, stride);
     }
     if (n23) {
 #if LVK_CLASS_STAGGER
@@ -102,8 +108,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         // rotation is on the wave-uniform round index (scalar registers: an
         // entry remap in SortedList::load cost the class kernel 5 VGPRs of
         // spills and C3 via offsets 5 %).
-        const uint64_t rrot = (LVK_CLASS3_FIRST && cls[6] && cls[7]) ? n23 / 4u : 0u;  // K = 4 entries per round
-        const uint64_t s3 = cls[6] / 4u;
+        const uint64_t rrot = (LVK_CLASS3_FIRST && cls(6) && cls(7)) ? n23 / 4u : 0u;  // K = 4 entries per round
+        const uint64_t s3 = cls(6) / 4u;
         auto pool = [&]() -> uint64_t {
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
@@ -114,7 +120,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
             }
             return rho;
         };
-        sorted_stream<16>(sub_list(P, cls[6] ? cls[2] : cls[3], n23, np), SortedList<SEEDED>{ident}, lane, L, pool(),
+        sorted_stream<16>(sub_list(P, cls(6) ? cls(2) : cls(3), n23, np), SortedList<SEEDED>{ident}, lane, L, pool(),
                           pool);
     }
 }
@@ -687,13 +693,8 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
             P.n = n;
             P.nplain = n;
             P.flags = flags;
-            P.hident = 1;
             const uint32_t L = hint->max_len;
-            const uint32_t cl = L <= 256u ? 0u : L <= 2048u ? 1u : L <= 32768u ? 2u : 3u;  // lvk::len_class
-            for (uint32_t k = 0; k < 4; ++k) {
-                P.hcls[k] = k <= cl ? 0u : static_cast<uint32_t>(n);
-                P.hcls[4 + k] = k == cl ? static_cast<uint32_t>(n) : 0u;
-            }
+            P.hident = 1u + (L <= 256u ? 0u : L <= 2048u ? 1u : L <= 32768u ? 2u : 3u);  // 1 + lvk::len_class(L)
             g_kernel = "crc32c_classes_kernel";
             launch_classes(*c, d_seed != nullptr, P, reinterpret_cast<const uint32_t *>(d_ws), s);
             return check_launch();

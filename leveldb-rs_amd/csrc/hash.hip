@@ -21,19 +21,22 @@
 // 2.5 KiB stages per wave, 7 workgroups per CU) was correct but slower:
 // 145 -> 172 us on the offsets API, packed u32 unchanged
 // (profiles/r04/hash_glds/) -- so the round trip is not the bound either.
-// The grid is persistent: a wave walks sets of 64 keys.  Round 4 found
-// what bounded it: the metadata prefetch was exec-masked (and under a
-// `more` branch), so the compiler could not count the loads in flight and
-// the set's first wait was a vmcnt(0) covering the prefetch just issued --
-// two exposed round trips per set.  The product kernel (hash_kernel_deep,
-// LVK_HASH_DEEP) issues every load from every lane (clamped indices, a
-// dummy block for span chunks past the span and for invalid lanes'
-// results), so every wait counts exactly, and runs two sets deep: set s
-// hashes from LDS while set s + W's span is in flight in registers and set
-// s + 2W's metadata behind it (80 VGPRs, 6 workgroups per CU):
-// 0.32 -> 0.46 of 8 TB/s in key bytes on the same box (profiles/r04/
-// new_ab/, hash_wait/; the one-set kernel with exact waits 0.29 -> 0.32).
-// (Round 2's two-deep form kept the masked loads: 106 vs 117 G keys/s.)
+// Wait counts (round 4): the next set's metadata was loaded under an exec
+// mask and a `more` branch, so the compiler could not count the loads in
+// flight and waited vmcnt(0) -- for the prefetch just issued -- at the top of
+// every set.  Every lane now loads its (clamped) metadata and the validity
+// select waits until the set is hashed (LVK_HASH_PREFETCH_EXACT): offsets
+// API unchanged (0.515 vs 0.516), packed u32 keys 0.504 -> 0.542
+// (profiles/r04/hash_exact/).  A two-deep kernel with every load exact --
+// the next set's span in registers while this set hashes, 80 VGPRs, 6
+// workgroups per CU -- measured 0.46 against 0.52 on one box
+// (profiles/r04/base_ab/) and was removed.
+// The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
+// requests the next set's metadata ahead, and stores each result one set
+// late, after the next set's loads, so no wait includes a store.  (A
+// two-deep form -- the next set's span in flight in registers while this
+// set hashes from LDS, metadata two sets ahead, 64 VGPRs at 8 waves/SIMD --
+// measured 106 vs 117 G keys/s, three interleaved reps: not kept.)
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -87,14 +90,62 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return v;
 }
 
-// Hash of this lane's key, its bytes in the wave's staged span (staged) or
-// in memory.
-__device__ __forceinline__ uint32_t hash_key(const uint8_t *__restrict__ base, const uint32_t *span, bool staged,
-                                             uint64_t lo16, bool valid, uint64_t o, uint32_t L, uint32_t sdv) {
+// Hash of this lane's key of one wave-set of 64 keys (metadata already
+// loaded); span is the wave's LDS stage.
+__device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, uint32_t *span, bool valid,
+                                             uint64_t o, uint32_t L, uint32_t sdv, uint32_t lane,
+                                             uint32_t *pout, uint32_t pval, bool pst) {
     uint32_t h = sdv ^ (kM * L);  // hash.rs:25
     const uint32_t bs = static_cast<uint32_t>(o & 3u);
     const uint32_t nw = L >> 2;               // whole words, hash.rs:29
     const uint32_t ndw = (bs + L + 3) >> 2;   // dwords covering the buffer
+    // Keys of a batch are usually packed (cache keys, log keys): the wave
+    // stages the granules spanning its 64 keys through LDS with coalesced
+    // 16-B loads, instead of 64 lanes gathering byte-aligned keys.  Waves
+    // whose keys span more than kSpanBytes read keys straight from memory.
+#if LVK_HASH_SPAN_READLANE
+    // Candidate span from the first and the last lane of the wave (keys are
+    // usually packed in order); the wave stages it only if every key lies
+    // inside it.  Two lane reads and one ballot instead of two 64-bit
+    // six-step shuffle reductions.
+    const uint64_t act = __ballot(valid);
+    const int last = act ? 63 - __builtin_clzll(act) : 0;
+    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool inside = !L || (o >= lo && o + L <= hi);
+    const bool staged = act && hi > lo && hi - lo16 <= kSpanBytes && __all(inside);  // wave-uniform
+#else
+    const uint64_t lo = wave_min_u64(L ? o : ~0ull);
+    const uint64_t hi = wave_max_u64(L ? o + L : 0ull);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool staged = lo != ~0ull && hi - lo16 <= kSpanBytes;  // wave-uniform
+#endif
+    if (staged) {
+        const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(base + lo16);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(span);
+        constexpr uint32_t kCh = kSpanBytes / 16 / 64;
+        u32x4 t[kCh];
+#pragma unroll
+        for (uint32_t k = 0; k < kCh; ++k) {
+            const uint32_t c = lane + 64u * k;
+            if (c < nch) t[k] = __builtin_nontemporal_load(src + c);
+        }
+        // the previous set's result leaves after this set's loads: waiting
+        // for them (vmcnt is in order) then does not wait for the store
+        if (pst) *pout = pval;
+#pragma unroll
+        for (uint32_t k = 0; k < kCh; ++k) {
+            const uint32_t c = lane + 64u * k;
+            if (c < nch) dst[c] = t[k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else if (pst) {
+        *pout = pval;
+    }
     if (valid && L && ndw <= kFastDw) {
         // Keys of up to ~64 B (cache keys): every dword of the key is read at
         // once (from the wave's staged span, or whole quads from memory where
@@ -192,128 +243,77 @@ __device__ __forceinline__ uint32_t hash_key(const uint8_t *__restrict__ base, c
     return h;
 }
 
-// Hash of this lane's key of one wave-set of 64 keys (metadata already
-// loaded); span is the wave's LDS stage.
-__device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, uint32_t *span, bool valid,
-                                             uint64_t o, uint32_t L, uint32_t sdv, uint32_t lane,
-                                             uint32_t *pout, uint32_t pval, bool pst) {
-    // Keys of a batch are usually packed (cache keys, log keys): the wave
-    // stages the granules spanning its 64 keys through LDS with coalesced
-    // 16-B loads, instead of 64 lanes gathering byte-aligned keys.  Waves
-    // whose keys span more than kSpanBytes read keys straight from memory.
-#if LVK_HASH_SPAN_READLANE
-    // Candidate span from the first and the last lane of the wave (keys are
-    // usually packed in order); the wave stages it only if every key lies
-    // inside it.  Two lane reads and one ballot instead of two 64-bit
-    // six-step shuffle reductions.
-    const uint64_t act = __ballot(valid);
-    const int last = act ? 63 - __builtin_clzll(act) : 0;
-    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
-    const uint64_t lo16 = lo & ~15ull;
-    const bool inside = !L || (o >= lo && o + L <= hi);
-    const bool staged = act && hi > lo && hi - lo16 <= kSpanBytes && __all(inside);  // wave-uniform
-#else
-    const uint64_t lo = wave_min_u64(L ? o : ~0ull);
-    const uint64_t hi = wave_max_u64(L ? o + L : 0ull);
-    const uint64_t lo16 = lo & ~15ull;
-    const bool staged = lo != ~0ull && hi - lo16 <= kSpanBytes;  // wave-uniform
-#endif
-    if (staged) {
-        const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(base + lo16);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(span);
-        constexpr uint32_t kCh = kSpanBytes / 16 / 64;
-        u32x4 t[kCh];
-#pragma unroll
-        for (uint32_t k = 0; k < kCh; ++k) {
-            const uint32_t c = lane + 64u * k;
-            if (c < nch) t[k] = __builtin_nontemporal_load(src + c);
-        }
-        // the previous set's result leaves after this set's loads: waiting
-        // for them (vmcnt is in order) then does not wait for the store
-        if (pst) *pout = pval;
-#pragma unroll
-        for (uint32_t k = 0; k < kCh; ++k) {
-            const uint32_t c = lane + 64u * k;
-            if (c < nch) dst[c] = t[k];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else if (pst) {
-        *pout = pval;
-    }
-    return hash_key(base, span, staged, lo16, valid, o, L, sdv);
-}
-
 // Metadata of one wave-set: load() requests this lane's words (issued one
 // set ahead), get() turns them into (offset, length, seed) when the set is
-// hashed -- any cross-lane step or widening sits there, so the prefetch never
-// waits.  Every lane issues every load (past the end: the last key's words,
-// discarded in get(); no seeds: a load of the lengths / bounds, discarded):
-// an exec-masked or branched-over load leaves the compiler unable to count
-// the loads in flight, and its next wait is a vmcnt(0) that also waits for
-// the prefetch just issued -- two exposed round trips per set instead of one.
+// hashed -- any cross-lane step sits there, so the prefetch never waits.
+struct MetaRaw {
+    uint64_t o, x;
+    uint32_t L, sd;
+};
 
 // Offsets API: off[] / len[] / seed[] per key.
 struct OffsetsMeta {
-    struct Raw {
-        uint64_t o;
-        uint32_t L, sd;
-    };
     const uint64_t *off;
     const uint32_t *len;
-    const uint32_t *seed;  // or len (unseeded: loaded and discarded)
-    bool seeded;
-    __device__ __forceinline__ Raw load(uint64_t i, uint32_t n, uint32_t) const {
-        if (LVK_HASH_MASKED_META) {
-            const bool v = i < n;
-            return Raw{v ? off[i] : 0u, v ? len[i] : 0u, v && seeded ? seed[i] : 0u};
-        }
-        const uint64_t ic = i < n ? i : n - 1u;
-        return Raw{off[ic], len[ic], seed[ic]};
-    }
-    __device__ __forceinline__ void get(const Raw &r, uint64_t i, uint32_t n, uint32_t, uint64_t &o, uint32_t &L,
-                                        uint32_t &sd) const {
+    const uint32_t *seed;
+    __device__ __forceinline__ MetaRaw load(uint64_t i, uint32_t n, uint32_t) const {
         const bool v = i < n;
+        MetaRaw r;
+        if constexpr (LVK_HASH_PREFETCH_EXACT) {  // every lane loads (clamped; get() zeroes lanes past n)
+            const uint64_t ic = v ? i : n - 1u;
+            r.o = off[ic];
+            r.L = len[ic];
+            r.sd = seed ? seed[ic] : 0u;  // (wave-uniform)
+        } else {
+            r.o = v ? off[i] : 0u;
+            r.L = v ? len[i] : 0u;
+            r.sd = v && seed ? seed[i] : 0u;
+        }
+        r.x = 0;
+        return r;
+    }
+    __device__ __forceinline__ void get(const MetaRaw &r, uint64_t i, uint32_t n, uint32_t, uint64_t &o, uint32_t &L,
+                                        uint32_t &sd) const {
+        const bool v = !LVK_HASH_PREFETCH_EXACT || i < n;
         o = v ? r.o : 0u;
         L = v ? r.L : 0u;
-        sd = v && seeded ? r.sd : 0u;
+        sd = v ? r.sd : 0u;
     }
 };
 
 // Packed keys (lv_hash_batch_packed): key i = arena[b[i], b[i+1]) with n + 1
 // bounds of B bytes (u32: an Arrow-style string array, u64: a large one).  A
 // lane reads its start; its end is the next lane's start, and lane 63 (or
-// the last key) uses the bound after it -- 4 or 8 B of metadata per key
+// the last key) reads the bound after it -- 4 or 8 B of metadata per key
 // instead of 12.
 template <typename B>
 struct PackedMeta {
-    struct Raw {
-        B o, x;
-        uint32_t sd;
-    };
     const B *b;
-    const uint32_t *seed;  // or the bounds (unseeded: loaded and discarded)
-    bool seeded;
-    __device__ __forceinline__ Raw load(uint64_t i, uint32_t n, uint32_t lane) const {
-        if (LVK_HASH_MASKED_META) {
-            const bool v = i < n;
-            return Raw{v ? b[i] : B(0), v && (lane == 63u || i + 1 >= n) ? b[i + 1] : B(0), v && seeded ? seed[i] : 0u};
-        }
-        const uint64_t ic = i < n ? i : n - 1u;
-        return Raw{b[ic], b[ic + 1], seed[ic]};
-    }
-    __device__ __forceinline__ void get(const Raw &r, uint64_t i, uint32_t n, uint32_t lane, uint64_t &o,
-                                        uint32_t &L, uint32_t &sd) const {
-        const uint64_t s0 = static_cast<uint64_t>(r.o);
-        const uint64_t nx = __shfl_down(s0, 1);
-        const uint64_t e = (lane == 63u || i + 1 >= n) ? static_cast<uint64_t>(r.x) : nx;
+    const uint32_t *seed;
+    __device__ __forceinline__ MetaRaw load(uint64_t i, uint32_t n, uint32_t lane) const {
         const bool v = i < n;
-        o = v ? s0 : 0u;
-        L = v ? static_cast<uint32_t>(e - s0) : 0u;
-        sd = v && seeded ? r.sd : 0u;
+        MetaRaw r;
+        if constexpr (LVK_HASH_PREFETCH_EXACT) {  // every lane loads (clamped; get() zeroes lanes past n)
+            const uint64_t ic = v ? i : n - 1u;
+            r.o = static_cast<uint64_t>(b[ic]);
+            r.x = static_cast<uint64_t>(b[ic + 1]);  // used by lane 63 and the last key
+            r.sd = seed ? seed[ic] : 0u;
+        } else {
+            r.o = v ? static_cast<uint64_t>(b[i]) : 0u;
+            r.x = v && (lane == 63u || i + 1 >= n) ? static_cast<uint64_t>(b[i + 1]) : 0u;
+            r.sd = v && seed ? seed[i] : 0u;
+        }
+        r.L = 0;
+        return r;
+    }
+    __device__ __forceinline__ void get(const MetaRaw &r, uint64_t i, uint32_t n, uint32_t lane, uint64_t &o,
+                                        uint32_t &L, uint32_t &sd) const {
+        const uint64_t nx = __shfl_down(r.o, 1);
+        const uint64_t e = (lane == 63u || i + 1 >= n) ? r.x : nx;
+        const bool v = i < n;
+        o = v ? r.o : 0u;
+        L = v ? static_cast<uint32_t>(e - r.o) : 0u;
+        sd = v ? r.sd : 0u;
     }
 };
 
@@ -335,16 +335,13 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
     uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
     if (set * 64u >= n) return;  // wave-uniform
-    typename Meta::Raw cur = meta.load(set * 64u + lane, n, lane), nx{};
-    // nothing in flight at the loop head from this edge either, so the
-    // loop's first wait need not cover the prefetch issued at its top
-    if (!LVK_HASH_MASKED_META) __builtin_amdgcn_s_waitcnt(0);
+    MetaRaw cur = meta.load(set * 64u + lane, n, lane), nx{};
     uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late
     bool pst = false;
     for (;;) {
         const uint64_t nxt = set + W;
         const bool more = nxt * 64u < n;  // wave-uniform
-        if (!LVK_HASH_MASKED_META || more) nx = meta.load(nxt * 64u + lane, n, lane);  // unconditional (clamped): see OffsetsMeta
+        if (LVK_HASH_PREFETCH_EXACT || more) nx = meta.load(nxt * 64u + lane, n, lane);  // (clamped)
         const uint64_t i = set * 64u + lane;
         const bool valid = i < n;
         uint64_t o;
@@ -364,106 +361,7 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     }
 }
 
-// Two sets deep: while set s hashes from LDS, set s + W's span is in flight
-// in registers and set s + 2W's metadata behind it.  Every load is issued by
-// every lane -- span chunks past the span and invalid lanes' results go to a
-// dummy block -- so the compiler counts the loads in flight exactly and the
-// waits for set s's span cover no later request.
-static __device__ __attribute__((aligned(16))) uint4 g_hash_dummy[64];
-
-struct SpanPlan {
-    uint64_t lo16;
-    uint32_t nch;  // 16-B chunks (0: not staged)
-};
-
-__device__ __forceinline__ SpanPlan span_plan(bool valid, uint64_t o, uint32_t L) {
-    const uint64_t act = __ballot(valid);
-    const int last = act ? 63 - __builtin_clzll(act) : 0;
-    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
-    SpanPlan s;
-    s.lo16 = lo & ~15ull;
-    const bool inside = !L || (o >= lo && o + L <= hi);
-    const bool staged = act && hi > lo && hi - s.lo16 <= kSpanBytes && __all(inside);  // wave-uniform
-    s.nch = staged ? static_cast<uint32_t>((hi - s.lo16 + 15) >> 4) : 0u;
-    return s;
-}
-
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-constexpr uint32_t kSpanCh = kSpanBytes / 16 / 64;
-
-__device__ __forceinline__ void span_issue(const uint8_t *__restrict__ base, const SpanPlan &s, uint32_t lane,
-                                           u32x4v (&t)[kSpanCh]) {
-#pragma unroll
-    for (uint32_t k = 0; k < kSpanCh; ++k) {
-        const uint32_t c = lane + 64u * k;
-        const u32x4v *src = c < s.nch ? reinterpret_cast<const u32x4v *>(base + s.lo16) + c
-                                      : reinterpret_cast<const u32x4v *>(g_hash_dummy) + lane;
-        t[k] = __builtin_nontemporal_load(src);
-    }
-}
-
-template <typename Meta>
-__global__ void __launch_bounds__(256) hash_kernel_deep(const uint8_t *__restrict__ base, Meta meta,
-                                                        uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
-    __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpanBytes / 4 + kSpanPad];
-    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
-    if (set * 64u >= n) return;  // wave-uniform
-    typename Meta::Raw mc = meta.load(set * 64u + lane, n, lane);
-    typename Meta::Raw mn = meta.load((set + W) * 64u + lane, n, lane);
-    __builtin_amdgcn_s_waitcnt(0);
-    uint64_t o;
-    uint32_t L, sd;
-    meta.get(mc, set * 64u + lane, n, lane, o, L, sd);
-    SpanPlan sp = span_plan(set * 64u + lane < n, o, L);
-    u32x4v t[kSpanCh];
-    span_issue(base, sp, lane, t);
-    uint32_t *const sink = reinterpret_cast<uint32_t *>(g_hash_dummy) + lane;
-    for (;;) {
-        const uint64_t i = set * 64u + lane;
-        const bool valid = i < n;
-        const bool more = (set + W) * 64u < n;  // wave-uniform
-        // set + 2W's metadata, set + W's span (both clamped: always issued)
-        const typename Meta::Raw m2 = meta.load((set + 2u * W) * 64u + lane, n, lane);
-        uint64_t o1;
-        uint32_t L1, sd1;
-        meta.get(mn, i + 64u * W, n, lane, o1, L1, sd1);
-        const SpanPlan sp1 = span_plan(i + 64u * W < n, o1, L1);
-        u32x4v t1[kSpanCh];
-        span_issue(base, sp1, lane, t1);
-        // this set: its span to LDS, then the keys
-        uint32_t *const sw = span[wv];
-        if (sp.nch) {  // wave-uniform
-            u32x4v *dst = reinterpret_cast<u32x4v *>(sw);
-#pragma unroll
-            for (uint32_t k = 0; k < kSpanCh; ++k) {
-                const uint32_t c = lane + 64u * k;
-                if (c < sp.nch) dst[c] = t[k];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        const uint32_t h = hash_key(base, sw, sp.nch != 0u, sp.lo16, valid, o, L, sd);
-        *(valid ? out + i : sink) = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
-        if (!more) break;
-        __builtin_amdgcn_wave_barrier();  // this set's LDS reads precede the next stage
-        set += W;
-        o = o1;
-        L = L1;
-        sd = sd1;
-        sp = sp1;
-        static_assert(kSpanCh == 4, "span registers: four 16-B chunks per lane");
-        t[0] = t1[0];
-        t[1] = t1[1];
-        t[2] = t1[2];
-        t[3] = t1[3];
-        mn = m2;
-    }
-}
-
-// persistent grid: LVK_HASH_WGS_PER_CU workgroups (of 4 waves) per CU at most
+// persistent grid: 8 workgroups (32 waves) per CU at most
 uint32_t hash_grid(size_t n) {
     static std::atomic<int> cus_cache[64];
     int dev = 0, cus = 0;
@@ -474,16 +372,6 @@ uint32_t hash_grid(size_t n) {
     }
     const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * kWgsPerCu;
     return static_cast<uint32_t>(want < cap ? want : cap);
-}
-
-template <typename Meta>
-void launch_hash(const uint8_t *base, const Meta &meta, uint32_t *out, size_t n, uint32_t flags, hipStream_t s) {
-    if (LVK_HASH_DEEP)
-        hipLaunchKernelGGL(hash_kernel_deep<Meta>, dim3(hash_grid(n)), dim3(256), 0, s, base, meta, out,
-                           static_cast<uint32_t>(n), flags);
-    else
-        hipLaunchKernelGGL(hash_kernel<Meta>, dim3(hash_grid(n)), dim3(256), 0, s, base, meta, out,
-                           static_cast<uint32_t>(n), flags);
 }
 
 }  // namespace lvh
@@ -520,8 +408,9 @@ int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const ui
     if (!d_arena || !d_off || !d_len || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
     if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
-    lvh::launch_hash(d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed ? d_seed : d_len, d_seed != nullptr}, d_out, n, flags,
-                     static_cast<hipStream_t>(stream));
+    hipLaunchKernelGGL(lvh::hash_kernel<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed}, d_out,
+                       static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
 }
 
@@ -536,13 +425,14 @@ int lv_hash_batch_packed(const uint8_t *d_arena, const void *d_bounds, uint32_t 
     if (reinterpret_cast<uintptr_t>(d_bounds) % bound_bytes)
         return lvgpu_internal::set_error(LV_ERR_INVALID, "bounds must be aligned to bound_bytes");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const uint32_t *sp = d_seed ? d_seed : static_cast<const uint32_t *>(d_bounds);  // unseeded: loaded, discarded
     if (bound_bytes == 4)
-        lvh::launch_hash(d_arena, lvh::PackedMeta<uint32_t>{static_cast<const uint32_t *>(d_bounds), sp, d_seed != nullptr},
-                         d_out, n, flags, s);
+        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint32_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+                           lvh::PackedMeta<uint32_t>{static_cast<const uint32_t *>(d_bounds), d_seed}, d_out,
+                           static_cast<uint32_t>(n), flags);
     else
-        lvh::launch_hash(d_arena, lvh::PackedMeta<uint64_t>{static_cast<const uint64_t *>(d_bounds), sp, d_seed != nullptr},
-                         d_out, n, flags, s);
+        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint64_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+                           lvh::PackedMeta<uint64_t>{static_cast<const uint64_t *>(d_bounds), d_seed}, d_out,
+                           static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
 }
 

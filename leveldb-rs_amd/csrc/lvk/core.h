@@ -322,9 +322,8 @@ struct Params {
     const uint32_t *tabs;   // fused small-batch kernel: the byte tables Shift_{2^i}, 1,024 words each
     // class kernel, lv_crc32c_batch_device_hint: a uniform batch none of whose
     // buffers can split is one sort key in index order, known on the host --
-    // no sort runs; hcls holds the class ranges the sort would have written
+    // no sort runs; hident = 1 + its length class (0: the sort's ranges)
     uint32_t hident;
-    uint32_t hcls[8];
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of

@@ -38,8 +38,7 @@
     defined(LVK_EXP_SEAL_COMPACT) || \
     defined(LVK_HASH_SPAN_READLANE) || \
     defined(LVK_HASH_WGS_PER_CU) || \
-    defined(LVK_HASH_DEEP) || \
-    defined(LVK_HASH_MASKED_META) || \
+    defined(LVK_HASH_PREFETCH_EXACT) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
@@ -121,14 +120,11 @@
 #ifndef LVK_HASH_SPAN_READLANE  // hash: a wave's span from its first and last lanes (0: two wave reductions)
 #define LVK_HASH_SPAN_READLANE 1
 #endif
-#ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU (the two-deep kernel's 80 VGPRs fit 6)
-#define LVK_HASH_WGS_PER_CU 6
+#ifndef LVK_HASH_PREFETCH_EXACT  // hash: the next set's metadata loaded by every lane (clamped), no exec mask
+#define LVK_HASH_PREFETCH_EXACT 1
 #endif
-#ifndef LVK_HASH_DEEP  // hash: the next set's span in flight in registers while this set hashes (0: one set)
-#define LVK_HASH_DEEP 1
-#endif
-#ifndef LVK_HASH_MASKED_META  // hash: round 4's first form -- exec-masked metadata loads, the prefetch under `more`
-#define LVK_HASH_MASKED_META 0
+#ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
+#define LVK_HASH_WGS_PER_CU 8
 #endif
 // sorted_stream wait-count mode per source (walk.h): 0 = exec-masked loads,
 // 1 = the same unconditional loads every step, 2 = unconditional loads
