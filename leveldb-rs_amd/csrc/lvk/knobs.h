@@ -130,7 +130,7 @@
 // 1 = the same unconditional loads every step, 2 = unconditional loads
 // within each path (no re-reads)
 #ifndef LVK_WALK_EXACT  // the class kernel's sorted lists (offsets API, WAL scan)
-#define LVK_WALK_EXACT 1
+#define LVK_WALK_EXACT 0
 #endif
 #ifndef LVK_TABLE_EXACT  // the SST table walk's verify (the seal keeps mode 0)
 #define LVK_TABLE_EXACT 2

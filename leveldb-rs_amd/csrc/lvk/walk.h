@@ -433,19 +433,18 @@ struct SortedList {
 // Wait counts (round 4): the compiler counts loads in flight per path and
 // merges paths by their minimum, so a load that only some paths issue (an
 // exec-masked tail load, the next round's loads under `more`) makes the
-// fold of a batch wait with vmcnt(0..3) -- i.e. also for the prefetch
-// issued just before it, one exposed round trip per batch.  With
-// Src::kExact every step issues the same unconditional loads (tail and
-// trailer every step, the next round's entries and first batch always,
-// clamped), the waits count exactly (vmcnt(8..5) in the class kernel's
-// small-class loops) and the prefetch stays in flight: C3 via offsets
-// 0.67 -> 0.70, WAL scan 0.58 -> 0.61, C2 / C4 +1 % (profiles/r04/new_ab/).
-// The table walk (tail + two trailer dwords per step, 9 % slower) and the
-// fused small-batch kernel (+1 us) keep the masked form.  (Round 2 issued the
-// same loads in every step by re-reading the entries each batch as well:
-// 4-5 % slower from the extra loads and spills.)
-// The image is always the G = 16 one: groups of G = 1 and 4 take their
-// row-shift and merge tables from the plain combine tables.
+// fold of a batch wait with vmcnt(0..3) -- also for the prefetch issued
+// just before it.  Src::kExact selects the load form: 0 = masked loads;
+// 1 = the same unconditional loads every step (tail and trailer re-read,
+// the next round's entries and first batch always, clamped); 2 =
+// unconditional loads within each path.  Exact waits (vmcnt(8..5) in the
+// fold) measured, against mode 0 on one box (profiles/r04/walk_modes/,
+// mode2_ab/): class kernel mode 1 / 2 -- C3 via offsets -2.5 / -3 %, C2 0,
+// C4 -0.6 %, WAL scan +0.6 / -0.3 % -- so it keeps mode 0 (16 waves per CU
+// hide the exposed round trip); SST verify mode 2 +2.8 % (0.703 -> 0.723,
+// final_ab/), the seal -4 % (mode 0); the fused small-batch kernel +0.5-1.3
+// us (mode 0).  (Round 2 issued the same loads in every step by re-reading
+// the entries each batch as well: 4-5 % slower from extra loads and spills.)
 template <int G, class Src, class Next, uint32_t ALR = kAlRows>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {

@@ -47,10 +47,10 @@ struct TableUnits {
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
     static constexpr bool kOneRound = false;
     // Wait-count mode (walk.h sorted_stream): verify runs mode 2 (every load
-    // unconditional within its path: 0.689 -> 0.709), the seal keeps the
-    // masked loads (mode 2: 0.667 -> 0.639; mode 1, the tail and trailer
-    // re-read every step: seal 0.67 -> 0.61, verify 0.69 -> 0.64;
-    // profiles/r04/mode2_ab/, exact_ab/)
+    // unconditional within its path: 0.703 -> 0.723 against the session-start
+    // build, profiles/r04/final_ab/), the seal keeps the masked loads (mode
+    // 2: 0.667 -> 0.639; mode 1, the tail and trailer re-read every step:
+    // seal 0.67 -> 0.61, verify 0.69 -> 0.64; mode2_ab/, exact_ab/)
     static constexpr uint32_t kExact = SEAL ? 0u : LVK_TABLE_EXACT;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {

@@ -169,6 +169,37 @@ def test_product_build_refuses_kernel_switches():
     assert ok.returncode == 0, ok.stderr[-2000:]
 
 
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+def test_streaming_kernels_do_not_spill():
+    """The streaming kernels stay within their register budget: no VGPR spill
+    in the unseeded class kernel (C2 / C4 / C3 via offsets / the WAL scan),
+    the uniform-block kernels (the headline) or the SST walk.  Round 4 had a
+    change put eight selected class bounds in registers: 24 VGPRs of spills,
+    C3 via offsets 0.75 -> 0.67 -- a spill reload is a vector memory
+    operation, so its wait also waits for every prefetch in flight."""
+    import re
+    import subprocess
+    want = {"classes.hip": ["crc32c_classes_kernelILb0E"], "blocks.hip": ["crc32c_blocks_kernelILi16ELb0ELb0ELb0E"],
+            "sst.hip": ["sst_blocks_kernelILb0ELb0E", "sst_blocks_kernelILb1ELb0E"]}
+    for src, kernels in want.items():
+        r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                            "-munsafe-fp-atomics", "--cuda-device-only", "-c", "-o", os.devnull,
+                            os.path.join(CSRC, src), "-Rpass-analysis=kernel-resource-usage"],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        spills, name = {}, None
+        for line in r.stderr.splitlines():
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                name = m.group(1)
+            m = re.search(r"VGPRs Spill: (\d+)", line)
+            if m and name:
+                spills[name] = int(m.group(1))
+        for k in kernels:
+            hits = {n: v for n, v in spills.items() if k in n}
+            assert hits and all(v == 0 for v in hits.values()), (src, hits)
+
+
 def test_device_counters_query():
     """lv_device_counters: readable without a GPU (zero before any host-path
     call), bounds-checked, and a short `n` fills only that many slots."""
