@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/hash_wait/; the hash switches it measured -- LVK_HASH_DEEP, LVK_HASH_MASKED_META -- were then retired with their code.)
 # Round 4: hash metadata loads and the compiler's wait counts.  prod = every
 # metadata load issued by every lane (clamped) with a clean wait state at the
 # loop head; masked = the earlier form (exec-masked loads, the prefetch under

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/new_ab/; the hash switches it measured -- LVK_HASH_DEEP, LVK_HASH_MASKED_META -- were then retired with their code.)
 # Round 4: the product with exact wait counts in the sorted walk (class and
 # fused kernels) and the two-deep hash, against the previous product
 # (variant "old": LVK_WALK_EXACT=0 LVK_HASH_DEEP=0 LVK_HASH_WGS_PER_CU=8).
