@@ -643,11 +643,11 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     // (An empty launch -- C2 / C4, or a batch whose split buffers were all
     // joined in the fused kernel -- takes 4-5 us in the trace, with 64
     // workgroups as with one per CU: profiles/r03/fused_small/local_join/.)
-    // (at most one split buffer per buffer: no more workgroups than buffers)
+    // (A grid of min(buffers, CUs) workgroups instead measured the same on
+    // 1 x 16 MiB, 16 x 1 MiB and 64 x 16 MiB: profiles/r04/join_grid/.)
     if (longs && join)
-        hipLaunchKernelGGL(lvk::combine_long_kernel,
-                           dim3(static_cast<uint32_t>(std::min<uint64_t>(LVK_JOIN_GRID_N ? n : c.cus, c.cus))),
-                           dim3(1024), 0, s, ws, longs, P.part, c.base_tabs, out, flags);
+        hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(1024), 0, s, ws, longs,
+                           P.part, c.base_tabs, out, flags);
     return 0;
 }
 

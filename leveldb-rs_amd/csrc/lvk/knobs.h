@@ -40,7 +40,6 @@
     defined(LVK_HASH_WGS_PER_CU) || \
     defined(LVK_HASH_PREFETCH_EXACT) || \
     defined(LVK_WALK_EXACT) || \
-    defined(LVK_JOIN_GRID_N) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -126,9 +125,6 @@
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8
-#endif
-#ifndef LVK_JOIN_GRID_N  // combine_long_kernel: min(buffers, CUs) workgroups (0: one per CU)
-#define LVK_JOIN_GRID_N 1
 #endif
 // sorted_stream wait-count mode per source (walk.h): 0 = exec-masked loads,
 // 1 = the same unconditional loads every step, 2 = unconditional loads

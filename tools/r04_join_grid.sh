@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Run once in round 4, profiles/r04/join_grid/; LVK_JOIN_GRID_N was then retired with its code: no difference.)
 # Round 4: combine_long_kernel launched with min(buffers, CUs) workgroups
 # (product) against one per CU (variant g0), on the few-long-buffer calls;
 # the GPU batch tests under the product first.  usage: tools/r04_join_grid.sh OUTDIR
