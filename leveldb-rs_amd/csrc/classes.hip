@@ -144,9 +144,23 @@ __global__ __launch_bounds__(1024) void combine_long_kernel(const uint32_t *__re
                                                            const uint4 *__restrict__ longs,
                                                            const uint32_t *__restrict__ part,
                                                            const uint32_t *__restrict__ tabs,
-                                                           uint32_t *__restrict__ out, uint32_t flags) {
+                                                           uint32_t *__restrict__ out, uint32_t flags,
+                                                           const uint32_t *__restrict__ tmp,
+                                                           const uint32_t *__restrict__ spos, uint64_t nb) {
+    // Unsort (the sorted path): the class kernel stored each CRC at its
+    // buffer's sorted position, in runs of consecutive words; out[i] =
+    // tmp[spos[i]] writes whole lines in buffer order.  Split buffers
+    // (spos = ~0u) are the join's below; a one-key batch (kWsIdent) was walked
+    // in buffer order straight into out[].
+    if (tmp && ws[kWsIdent] == 0u) {  // grid-uniform
+        const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+        for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nb; i += stride) {
+            const uint32_t sp = spos[i];
+            if (sp != 0xffffffffu) out[i] = tmp[sp];
+        }
+    }
     // the counter counts every claim; records exist only below the budget
-    const uint32_t nl = min(ws[kWsLongs], kPieceBudget / 2);
+    const uint32_t nl = longs ? min(ws[kWsLongs], kPieceBudget / 2) : 0u;
     if (blockIdx.x >= nl) return;  // block-uniform (every workgroup below nl has a wave or a record)
     // Shift_{2^i}(v) by four byte-table lookups (tables in HBM, L2-resident:
     // 192 KiB for every i) instead of a staged 32-column matrix product
@@ -585,8 +599,13 @@ static uint32_t host_split_rule(uint32_t L, uint64_t total, uint32_t *p) {
 // (the same unit layout crc32c_fused_small_kernel computes on the device).
 bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
     uint32_t p = 0;
-    if (host_split_rule(h.max_len, h.total_bytes, &p) == 0) return false;  // monotone: nothing splits
-    if (!h.uniform || n > lvk::kFusedMax || !LVK_FUSED_LOCAL_JOIN) return true;
+    const bool nosplit = host_split_rule(h.max_len, h.total_bytes, &p) == 0;  // monotone: nothing splits
+    // > kFusedMax buffers: the sorted path's join launch also unsorts the
+    // CRCs; only a uniform batch with nothing to split (the identity list,
+    // no sort) goes without it
+    if (n > lvk::kFusedMax) return !(h.uniform && nosplit);
+    if (nosplit) return false;
+    if (!h.uniform || !LVK_FUSED_LOCAL_JOIN) return true;
     const uint32_t m = host_split_rule(h.max_len, h.total_bytes, &p);
     const uint64_t nunits = n * m;
     const uint64_t grid = cus;
@@ -631,9 +650,15 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
             hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<false>, dim3(static_cast<uint32_t>(c.cus)),
                                dim3(lvk::kThreads), 0, s, P, c.image[2], ws, longs);
     } else {
+        // sorted path: the join launch also unsorts the class kernel's CRCs
+        // (combine_long_kernel), so it always runs
         longs = launch_sort(ws_bytes, off, len, seed, n, s, &P);
-        g_kernel = join ? "sort+crc32c_classes_kernel+combine_long_kernel" : "sort+crc32c_classes_kernel";
+        g_kernel = "sort+crc32c_classes_kernel+combine_long_kernel";
         launch_classes(c, seed != nullptr, P, ws, s);
+        hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(1024), 0, s, ws, longs,
+                           P.part, c.base_tabs, out, flags, P.tmp,
+                           reinterpret_cast<const uint32_t *>(ws_bytes + ws_layout(n).pos), n);
+        return 0;
     }
     // joins split long buffers (exits at once when the sort split none).  (A
     // last-finisher join inside the class kernel -- agent-scope release and
@@ -647,7 +672,7 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
     // 1 x 16 MiB, 16 x 1 MiB and 64 x 16 MiB: profiles/r04/join_grid/.)
     if (longs && join)
         hipLaunchKernelGGL(lvk::combine_long_kernel, dim3(static_cast<uint32_t>(c.cus)), dim3(1024), 0, s, ws, longs,
-                           P.part, c.base_tabs, out, flags);
+                           P.part, c.base_tabs, out, flags, nullptr, nullptr, 0);
     return 0;
 }
 

@@ -117,7 +117,7 @@ constexpr size_t al16(size_t x) { return (x + 15) & ~static_cast<size_t>(15); }
 uint64_t sort_wgs(uint64_t n, uint64_t *chunk);
 // Byte offsets of the sort workspace regions (layout in lvk/sort.h).
 struct WsLayout {
-    size_t m, wgb, ent, sseed, part, longs, total;
+    size_t m, wgb, ent, sseed, part, longs, tmp, pos, total;
 };
 WsLayout ws_layout(uint64_t n);
 size_t sort_ws_bytes(uint64_t n);

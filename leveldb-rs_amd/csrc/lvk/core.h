@@ -318,6 +318,7 @@ struct Params {
     const uint32_t *sseed;  // optional: seeds in sorted-entry order
     uint64_t nplain;        // sorted walk: entries [nplain, n) are long-buffer pieces
     uint32_t *part;         // piece registers (long-buffer split of the offsets API)
+    uint32_t *tmp;          // class kernel, sorted list: CRCs by sorted position (combine_long_kernel unsorts), or null
     const uint32_t *mats;   // blocks kernel, FUSE: Shift_{j plen}, j < 2^pshift (32 column words each)
     const uint32_t *tabs;   // fused small-batch kernel: the byte tables Shift_{2^i}, 1,024 words each
     // class kernel, lv_crc32c_batch_device_hint: a uniform batch none of whose

@@ -19,6 +19,8 @@
     defined(LVK_EXP_NOFIX) || \
     defined(LVK_EXP_NOMERGE) || \
     defined(LVK_EXP_NOSEALWRITE) || \
+    defined(LVK_EXP_NOOUT) || \
+    defined(LVK_EXP_SORTEDOUT) || \
     defined(LVK_AL_ROWS) || \
     defined(LVK_ALIGNED_ROWS) || \
     defined(LVK_IDENT) || \
@@ -68,6 +70,12 @@
 #endif
 #ifndef LVK_EXP_NOSEALWRITE  // the seal computes its trailers but stores none
 #define LVK_EXP_NOSEALWRITE 0
+#endif
+#ifndef LVK_EXP_NOOUT  // timing only: the class kernel computes its CRCs but stores none
+#define LVK_EXP_NOOUT 0
+#endif
+#ifndef LVK_EXP_SORTEDOUT  // timing only: the class kernel stores each CRC at its sorted position (wrong order)
+#define LVK_EXP_SORTEDOUT 0
 #endif
 #ifndef LVK_AL_ROWS
 #define LVK_AL_ROWS 4

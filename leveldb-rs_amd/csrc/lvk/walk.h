@@ -50,6 +50,11 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, int from) {
 // Geometry of sorted entry e (clamped to the last entry for lanes past the
 // end, so every address stays valid).  Seeds come pre-sorted (sort_scatter),
 // so no load depends on another.
+// bid: the entry's output slot -- its buffer index (v.w), a piece slot
+// (kPieceFlag), ~0u for a split buffer's own entry; with P.tmp the sorted
+// position instead of the buffer index, so a wave's results land in runs of
+// K consecutive words (combine_long_kernel moves them to out[]; scattered
+// single-word stores into out[] cost C2 ~35 us, profiles/r04/outstore/).
 template <bool SEEDED>
 __device__ __forceinline__ RGeo load_rgeo(const Params &P, uint64_t e) {
     const bool valid = e < P.n;
@@ -61,7 +66,9 @@ __device__ __forceinline__ RGeo load_rgeo(const Params &P, uint64_t e) {
     q.a = v.z ? P.base + ((static_cast<uint64_t>(v.y) << 32) | v.x) : P.base;
     q.len = v.z;
     q.seed = SEEDED ? P.sseed[ec] : 0u;
-    q.bid = valid ? v.w : 0xffffffffu;
+    const bool piece = P.nplain < P.n && (v.w & kPieceFlag) && v.w != 0xffffffffu;
+    const uint32_t slot = P.tmp && !piece && v.w != 0xffffffffu ? static_cast<uint32_t>(ec) : v.w;
+    q.bid = valid ? (LVK_EXP_SORTEDOUT ? static_cast<uint32_t>(ec) : slot) : 0xffffffffu;
     q.aux = 0;
     return q;
 }
@@ -419,8 +426,8 @@ struct SortedList {
         // piece slots (flagged in the entry) occur only in the pieces' sub-list (P.nplain < P.n)
         if (P.nplain < P.n && (bi & kPieceFlag))
             P.part[bi & ~kPieceFlag] = cv;
-        else
-            P.out[bi] = cv;
+        else if (!LVK_EXP_NOOUT)
+            (P.tmp && !ident ? P.tmp : P.out)[bi] = cv;  // (an identity list is in buffer order already)
     }
 };
 
@@ -609,6 +616,7 @@ __device__ __forceinline__ Params sub_list(const Params &P0, uint32_t start, uin
     Params P = P0;
     P.ent = P0.ent + start;
     P.sseed = P0.sseed ? P0.sseed + start : nullptr;
+    P.tmp = P0.tmp ? P0.tmp + start : nullptr;
     P.n = static_cast<uint64_t>(count) + pieces;
     P.nplain = count;
     return P;

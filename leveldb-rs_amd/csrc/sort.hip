@@ -216,7 +216,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
                                                              const uint32_t *__restrict__ M,
                                                              uint4 *__restrict__ ent,
                                                              const uint32_t *__restrict__ seed,
-                                                             uint32_t *__restrict__ sseed, uint4 *__restrict__ longs) {
+                                                             uint32_t *__restrict__ sseed, uint4 *__restrict__ longs,
+                                                             uint32_t *__restrict__ spos) {
     __shared__ uint32_t cur[kKeys];
     __shared__ uint32_t sc[kKeys];
     const uint32_t t = threadIdx.x, lane = t & 63u;
@@ -267,6 +268,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
                 ent[pos] = make_uint4(static_cast<uint32_t>(ob[e]), static_cast<uint32_t>(ob[e] >> 32),
                                       split ? 0u : lb[e], split ? 0xffffffffu : static_cast<uint32_t>(i));
                 if (seed) sseed[pos] = sd;
+                spos[i] = split ? 0xffffffffu : pos;  // in buffer order: coalesced
             }
         }
     }
@@ -309,7 +311,11 @@ WsLayout ws_layout(uint64_t n) {
     w.sseed = w.ent + ne * sizeof(uint4);
     w.part = w.sseed + al16(ne * sizeof(uint32_t));
     w.longs = w.part + al16(lvk::kPieceBudget * sizeof(uint32_t));
-    w.total = w.longs + (lvk::kPieceBudget / 2) * sizeof(uint4);
+    // the class kernel's CRCs by sorted position, and each buffer's sorted
+    // position (combine_long_kernel's unsort)
+    w.tmp = w.longs + (lvk::kPieceBudget / 2) * sizeof(uint4);
+    w.pos = w.tmp + al16(n * sizeof(uint32_t));
+    w.total = w.pos + al16(n * sizeof(uint32_t));
     return w;
 }
 
@@ -334,8 +340,10 @@ uint4 *launch_sort(uint8_t *ws_bytes, const uint64_t *off, const uint32_t *len, 
     // retired round 2's one-launch sort_small in round 3)
     hipLaunchKernelGGL(lvk::sort_hist, g, b, 0, s, len, n, chunk, M, ws, wgb);
     launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgb, s);
-    hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed, longs);
+    uint32_t *spos = reinterpret_cast<uint32_t *>(ws_bytes + lay.pos);
+    hipLaunchKernelGGL(lvk::sort_scatter, g, b, 0, s, off, len, n, chunk, ws, M, ent, seed, sseed, longs, spos);
     P->ent = ent;
+    P->tmp = reinterpret_cast<uint32_t *>(ws_bytes + lay.tmp);
     P->sseed = seed ? sseed : nullptr;
     P->part = longs ? part : nullptr;
     return longs;

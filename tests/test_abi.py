@@ -120,10 +120,11 @@ def test_argument_checks_before_any_device_call():
 
 def test_workspace_bytes_cover_pieces():
     """The offsets-API workspace holds n sorted entries plus the long-buffer
-    split's piece budget, whatever n."""
+    split's piece budget, whatever n, and the unsort's two words per buffer."""
     small, big = lvgpu.workspace_bytes(1), lvgpu.workspace_bytes(1 << 20)
     assert small >= 65536 * 16  # the piece entries alone
-    assert big - small >= ((1 << 20) - 1) * 20  # 16-B entry + 4-B seed per buffer
+    # 16-B entry + 4-B seed + the CRC by sorted position + the sorted position, per buffer
+    assert big - small >= ((1 << 20) - 1) * 28
 
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "leveldb-rs_amd", "csrc")
@@ -233,16 +234,18 @@ def _split_rule(L, total, pmin=12, maxp=4096):
 
 
 def _needs_join(lens, cus, fused_max=1024, waves=16):
-    """Whether the device launches combine_long_kernel with work to do: a
-    split buffer that the fused small-batch kernel does not join in place
-    (crc32c_fused_small_kernel's unit layout, csrc/classes.hip), or any split
-    buffer on the sorted path."""
+    """Whether the library launches combine_long_kernel: on the sorted path
+    (> 1,024 buffers) always -- it also unsorts the class kernel's CRCs --
+    but for a uniform batch with nothing to split (the identity list, no
+    sort); for a small batch when a split buffer is not joined in place by
+    the fused kernel (crc32c_fused_small_kernel's unit layout,
+    csrc/classes.hip)."""
     total = sum(lens)
     sp = [_split_rule(L, total) for L in lens]
+    if len(lens) > fused_max:
+        return not (len(set(lens)) == 1 and not any(m for m, _ in sp))
     if not any(m for m, _ in sp):
         return False
-    if len(lens) > fused_max:
-        return True
     units = [m if m else 1 for m, _ in sp]
     pre = [0]
     for u in units[:-1]:
@@ -282,10 +285,10 @@ def test_hint_join_decision_matches_the_device_layout():
         assert bool(got) == ref, (n, size, cus)
         if want is not None:
             assert ref == want, (n, size, cus)
-    for _ in range(500):  # non-uniform: join iff the longest buffer can split
+    for _ in range(500):  # non-uniform: the sorted path always, small batches iff the longest buffer can split
         n = rng.randrange(1, 3000)
         lens = [rng.randrange(0, 1 << rng.randrange(4, 22)) for _ in range(n)]
         h = lvgpu.hint_for(lens)
         got = L.lv_crc32c_hint_needs_join(ctypes.addressof(h), n, 256)
-        assert bool(got) == (_split_rule(max(lens), sum(lens))[0] > 0)
+        assert bool(got) == (n > 1024 or _split_rule(max(lens), sum(lens))[0] > 0)
         assert bool(got) >= _needs_join(lens, 256)  # never leaves out a join the device needs

@@ -907,7 +907,7 @@ HINT_CASES = {
     "uniform_16x1MiB": (lambda r: np.full(16, 1 << 20), "odd", True),
     "uniform_300x4KiB": (lambda r: np.full(300, 4096), "odd", False),          # nothing splits
     "small_mixed_fused": (lambda r: r.integers(0, 16385, 900), "odd", False),  # <= 16 KiB never splits
-    "sorted_no_split": (lambda r: r.integers(0, 9000, 5000), "odd", False),    # the three-pass sort, no join
+    "sorted_no_split": (lambda r: r.integers(0, 9000, 5000), "odd", True),     # the sort; its join launch unsorts
     "sorted_long": (lambda r: np.concatenate([r.integers(0, 5000, 3000), [3 << 20, 70000]]), "odd", True),
     "fused_long_ragged": (lambda r: np.concatenate([r.integers(0, 300, 100), [1 << 20, 5 << 20]]), "odd", True),
     # uniform, > 1,024 buffers, nothing splits: the class kernel alone, no sort (class 0 .. 3)
