@@ -42,6 +42,7 @@
     defined(LVK_HASH_WGS_PER_CU) || \
     defined(LVK_HASH_PREFETCH_EXACT) || \
     defined(LVK_WALK_EXACT) || \
+    defined(LVK_WAL_UNSORT) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -133,6 +134,9 @@
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8
+#endif
+#ifndef LVK_WAL_UNSORT  // WAL scan: CRCs stored by sorted position, then written in log order (wal_unsort)
+#define LVK_WAL_UNSORT 1
 #endif
 // sorted_stream wait-count mode per source (walk.h): 0 = exec-masked loads,
 // 1 = the same unconditional loads every step, 2 = unconditional loads

@@ -225,6 +225,7 @@ struct WalOut {
     uint32_t *info;  // type | status << 8 | length << 16
     uint64_t *count;
     uint64_t cap;
+    uint32_t *spos;  // each record's sorted position (wal_unsort), or null
 };
 
 __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__restrict__ log, uint64_t size,
@@ -309,6 +310,7 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
                                        static_cast<uint32_t>(rid));
                 o.hdr_off[rid] = start + pos;
                 o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
+                if (o.spos) o.spos[rid] = slot;
             }
         }
         // blocks with more records than the cache holds walk on from there
@@ -335,6 +337,7 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
                                            static_cast<uint32_t>(rid));
                     o.hdr_off[rid] = start + pos;
                     o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
+                    if (o.spos) o.spos[rid] = slot;
                     ++rid;
                     pos += kWalHeader + r.len;
                     active = r.status == LV_WAL_REC_OK && blen - pos >= kWalHeader;
@@ -344,6 +347,20 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
         run += tot;
         __syncthreads();  // red is rewritten by the next chunk
     }
+}
+
+// The class kernel stored each record's CRC at its sorted position (runs of
+// consecutive words); crc[rid] = tmp[spos[rid]] writes them in log order,
+// whole lines (scattered single-word stores from the class kernel cost the
+// offsets API's C2 ~35 us, profiles/r04/outstore/).
+__global__ __launch_bounds__(1024) void wal_unsort(const uint32_t *__restrict__ ws, const uint32_t *__restrict__ tmp,
+                                                   const uint32_t *__restrict__ spos, uint32_t *__restrict__ crc,
+                                                   uint64_t cap) {
+    const uint64_t total = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];  // records
+    if (total > cap) return;  // nothing was written: the caller retries with a larger capacity
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride)
+        crc[i] = tmp[spos[i]];
 }
 
 }  // namespace lvk
@@ -361,7 +378,7 @@ static uint64_t wal_wgs(uint64_t nblocks, uint64_t *chunk) {
 }
 
 struct WalWs {
-    size_t m, wgrec, blk, hc, ent, total;
+    size_t m, wgrec, blk, hc, ent, tmp, pos, total;
 };
 
 static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
@@ -374,7 +391,10 @@ static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
     w.blk = w.wgrec + al16(wgs * sizeof(uint64_t));
     w.hc = w.blk + al16(nblocks * sizeof(uint32_t));
     w.ent = w.hc + nblocks * lvk::kHdrCache * sizeof(uint64_t);
-    w.total = w.ent + cap * sizeof(uint4);
+    // with LVK_WAL_UNSORT: the CRCs by sorted position and each record's sorted position
+    w.tmp = w.ent + cap * sizeof(uint4);
+    w.pos = w.tmp + (LVK_WAL_UNSORT ? al16(cap * sizeof(uint32_t)) : 0);
+    w.total = w.pos + (LVK_WAL_UNSORT ? al16(cap * sizeof(uint32_t)) : 0);
     return w;
 }
 
@@ -417,7 +437,9 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     // measured 0.6 % slower: the memset launch and wal_hist's returning
     // atomics cost more than sort_scan, profiles/r03/wal2/atomic_totals/.)
     launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgrec, s);
-    lvk::WalOut o{d_hdr_off, d_info, d_count, cap};
+    uint32_t *tmp = LVK_WAL_UNSORT ? reinterpret_cast<uint32_t *>(wb + lay.tmp) : nullptr;
+    uint32_t *spos = LVK_WAL_UNSORT ? reinterpret_cast<uint32_t *>(wb + lay.pos) : nullptr;
+    lvk::WalOut o{d_hdr_off, d_info, d_count, cap, spos};
     hipLaunchKernelGGL(lvk::wal_scatter, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws, M, wgrec,
                        blk, hc, ent, o);
     lvk::Params P{};
@@ -426,8 +448,14 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     P.n = cap;
     P.nplain = cap;
     P.ent = ent;
+    P.tmp = tmp;
     launch_classes(*c, false, P, ws, s);
     g_kernel = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel";
+    if (tmp && cap) {
+        hipLaunchKernelGGL(lvk::wal_unsort, dim3(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (cap + 1023) / 1024))),
+                           dim3(1024), 0, s, ws, tmp, spos, d_crc, static_cast<uint64_t>(cap));
+        g_kernel = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel+wal_unsort";
+    }
     return check_launch();
 }
 

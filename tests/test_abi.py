@@ -107,8 +107,9 @@ def test_argument_checks_before_any_device_call():
     assert need > 0
     assert W.lv_wal_scan_device(fake, 64, fake, fake, fake, 8, fake, fake, need - 1, None) == -1
     assert b"workspace" in L.lv_last_error()
-    # the workspace grows with the capacity, 16 B per entry
-    assert W.lv_wal_scan_workspace_bytes(64, 1008) - need == 1000 * 16
+    # the workspace grows with the capacity: a 16-B entry, the CRC by sorted
+    # position and the sorted position per record
+    assert W.lv_wal_scan_workspace_bytes(64, 1008) - need == 1000 * 24
     # kernel-choice query: empty on a thread that has launched nothing
     import threading
     seen = []
