@@ -154,8 +154,13 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
         uint32_t w[kFastDw + 1];
         if (staged) {
             const uint32_t *sd = span + ((o - bs - lo16) >> 2);
+            // every dword of the window (the span's pad keeps it inside the
+            // stage): no compare and select per dword; bytes past the key
+            // never reach the chain (funnel shifts by bs < 4 only take
+            // bytes of w[j + 1] below 4 nw + bs, and the tail word is
+            // re-read or masked to its diff bytes)
 #pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = j < ndw ? sd[j] : 0u;
+            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = (LVK_HASH_TAIL_READ && LVK_HASH_LDS_ALL) || j < ndw ? sd[j] : 0u;
         } else {
             const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
             w[0] = d[0];
@@ -176,15 +181,37 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
         }
         w[kFastDw] = 0u;
         uint32_t tw = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kFastDw; ++j) {
-            const uint32_t wj = funnel(w[j + 1], w[j], bs);
-            if (j < nw)
-                h = mix(h, wj);
-            else if (j == nw)
-                tw = wj;
-        }
         const uint32_t diff = L - 4 * nw;          // hash.rs:38-48
+        if constexpr (LVK_HASH_TAIL_READ) {
+            // The loop is VALU-bound (wave64: 4 cycles an op): capturing the
+            // tail word in it cost a compare and a select per word, so the
+            // tail's two dwords are read again after it (LDS or L1)
+#pragma unroll
+            for (uint32_t j = 0; j < kFastDw; ++j)
+                if (j < nw) h = mix(h, funnel(w[j + 1], w[j], bs));
+            if (diff) {  // then nw < ndw
+                uint32_t t0, t1;
+                if (staged) {
+                    const uint32_t *sd = span + ((o - bs - lo16) >> 2);
+                    t0 = sd[nw];
+                    t1 = nw + 1 < ndw ? sd[nw + 1] : 0u;
+                } else {
+                    const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
+                    t0 = d[nw];
+                    t1 = nw + 1 < ndw ? d[nw + 1] : 0u;
+                }
+                tw = funnel(t1, t0, bs);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kFastDw; ++j) {
+                const uint32_t wj = funnel(w[j + 1], w[j], bs);
+                if (j < nw)
+                    h = mix(h, wj);
+                else if (j == nw)
+                    tw = wj;
+            }
+        }
         if (diff) {
             if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
             if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;

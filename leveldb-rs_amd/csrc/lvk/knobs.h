@@ -41,6 +41,8 @@
     defined(LVK_HASH_SPAN_READLANE) || \
     defined(LVK_HASH_WGS_PER_CU) || \
     defined(LVK_HASH_PREFETCH_EXACT) || \
+    defined(LVK_HASH_TAIL_READ) || \
+    defined(LVK_HASH_LDS_ALL) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
     defined(LVK_TABLE_EXACT) || \
@@ -128,6 +130,12 @@
 #endif
 #ifndef LVK_HASH_SPAN_READLANE  // hash: a wave's span from its first and last lanes (0: two wave reductions)
 #define LVK_HASH_SPAN_READLANE 1
+#endif
+#ifndef LVK_HASH_LDS_ALL  // hash: the staged fast path reads all 17 window dwords from LDS, unmasked
+#define LVK_HASH_LDS_ALL 1
+#endif
+#ifndef LVK_HASH_TAIL_READ  // hash: the tail word re-read after the chain, not captured in it
+#define LVK_HASH_TAIL_READ 1
 #endif
 #ifndef LVK_HASH_PREFETCH_EXACT  // hash: the next set's metadata loaded by every lane (clamped), no exec mask
 #define LVK_HASH_PREFETCH_EXACT 1
