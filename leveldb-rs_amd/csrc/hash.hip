@@ -30,7 +30,12 @@
 // (profiles/r04/hash_exact/).  A two-deep kernel with every load exact --
 // the next set's span in registers while this set hashes, 80 VGPRs, 6
 // workgroups per CU -- measured 0.46 against 0.52 on one box
-// (profiles/r04/base_ab/) and was removed.
+// (profiles/r04/base_ab/) and was removed.  What does bound it: the VALU
+// (wave64 = 4 cycles an op; ~300 per set, the 17-word chain ~110 of them).
+// Taking the tail-word capture (a compare and a select per word) out of the
+// chain -- its two dwords re-read after it -- and reading the 17-dword LDS
+// window unmasked: offsets 0.518 -> 0.53, packed u32 0.549 -> 0.575
+// (profiles/r04/hash_tail/, hash_ldsall/).
 // The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
 // requests the next set's metadata ahead, and stores each result one set
 // late, after the next set's loads, so no wait includes a store.  (A
