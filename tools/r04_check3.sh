@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 4 final check on the final tree: the GPU suite (verbose), smoke, a
+# 200-trial randomised sweep of the offsets API, and the default bench line
+# at the driver's flags.  usage: tools/r04_check3.sh OUTDIR
+set -o pipefail
+out=${1:-gpurun_out/r04c}
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$root" && mkdir -p "$out"
+export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$out/pytest.txt" 2>&1 &&
+echo "pytest done" &&
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$out/smoke.txt" 2>&1 &&
+LVGPU_STRESS_TRIALS=200 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_stress.py -m gpu -x -q --timeout 300 \
+  --timeout-method thread > "$out/stress200.txt" 2>&1 &&
+timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > "$out/default_driver.json" 2> "$out/default_driver.err" &&
+echo "all steps done"
