@@ -49,7 +49,8 @@ struct TableUnits {
     // Wait-count mode (walk.h sorted_stream): verify runs mode 2 (every load
     // unconditional within its path: 0.703 -> 0.723 against the session-start
     // build, profiles/r04/final_ab/), the seal keeps the masked loads (mode
-    // 2: 0.667 -> 0.639; mode 1, the tail and trailer re-read every step:
+    // 2: 0.667 -> 0.639, and with its trailer stores unconditional too 0.667
+    // -> 0.640, seal_exact/; mode 1, the tail and trailer re-read every step:
     // seal 0.67 -> 0.61, verify 0.69 -> 0.64; mode2_ab/, exact_ab/)
     static constexpr uint32_t kExact = SEAL ? 0u : LVK_TABLE_EXACT;
 
