@@ -33,7 +33,8 @@ namespace lvk {
 // record (no dependent chain step), walks on only for blocks with more
 // records, and writes every record straight into its sorted slot, plus its
 // log-order header offset and info word.  The class kernel then checksums the
-// units.  Four launches, no host synchronisation (round 1: count pass, hipCUB
+// units (by sorted position; wal_unsort writes them in log order).  Five
+// launches, no host synchronisation (round 1: count pass, hipCUB
 // scan, host readback of the total, emit pass, then the whole offsets API).
 constexpr uint32_t kWalBlock = 32768;  // log_format.rs:63
 constexpr uint32_t kWalHeader = 7;     // log_format.rs:66
@@ -477,7 +478,7 @@ int hip_err(hipError_t e, const char *what) {
 
 // The log goes to the device through the device's host path (cached arena;
 // pinned input: one DMA, pageable: pipelined pinned staging); the scan is
-// lv_wal_scan_device (framing fused into the length sort, four launches)
+// lv_wal_scan_device (framing fused into the length sort, five launches)
 // into the device's cached scratch buffer, so a scan allocates nothing on the
 // device after the first call.  The capacity starts at a guess (one record per
 // 256 log bytes, at least 8 per block); a log with more records is scanned
