@@ -67,6 +67,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     // (profiles/r03/small_waves/): the 1 GiB WAL scan (12 rounds on one wave)
     // 61.0 -> 63.2 % with 1 wave instead of 4, C2 (24 rounds on 3) 73.8 ->
     // 74.2-75.4 %, C4 (23 on 4) best with 4 (-1.2 % with 2, -1.8 % with 1).
+    // Round 4, with the CRCs stored by sorted position: kSmallRounds 52
+    // (fewer small-class waves) over 26, C2 0.770 -> 0.773, C4 0.755 ->
+    // 0.761, WAL unchanged; 13 and 104 lower (profiles/r04/small_rounds*/).
 #if LVK_SMALL_ALL
     uint32_t nsmall = n23 ? kSmallWaves : kWaves;
 #else

@@ -119,8 +119,8 @@
 #ifndef LVK_SMALL_ADAPT  // class kernel: small-class waves per workgroup from the class counts (<= LVK_SMALL_WAVES)
 #define LVK_SMALL_ADAPT 1
 #endif
-#ifndef LVK_SMALL_ROUNDS
-#define LVK_SMALL_ROUNDS 26
+#ifndef LVK_SMALL_ROUNDS  // small-class rounds per wave (round 4, after the unsort: 52 over 26: C2 +0.4 %, C4 +0.6 %)
+#define LVK_SMALL_ROUNDS 52
 #endif
 #ifndef LVK_FUSED_ONE_ROUND  // fused small-batch walk: a wave's only round requests all its batches at once
 #define LVK_FUSED_ONE_ROUND 1
