@@ -84,9 +84,11 @@ int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, con
 /* Host-side facts about a batch whose lengths live on the device.  The WAL
  * group-commit writer and the SST sealer know their fragment / block lengths
  * on the host; with them the library can leave out launches that the facts
- * prove empty -- the long-buffer join when no buffer can be split, or when
- * every split buffer of a uniform batch of <= 1,024 buffers is joined inside
- * the walk -- which the device-only call cannot know without a host sync.
+ * prove empty -- for batches of <= 1,024 buffers the long-buffer join when no
+ * buffer can be split, or when every split buffer of a uniform batch is
+ * joined inside the walk; for larger uniform batches that cannot split, the
+ * whole length sort and the join (the buffers are walked in index order) --
+ * which the device-only call cannot know without a host sync.
  * The facts must be exact (max_len may be any upper bound of the lengths): a
  * hint that understates them gives wrong CRCs. */
 typedef struct lv_batch_hint {
@@ -104,7 +106,9 @@ int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, c
 
 /* Debug query: 1 if a batch of n buffers with these facts, on a device with
  * `cus` compute units, launches the long-buffer join (the decision
- * lv_crc32c_batch_device_hint makes on the host), 0 if it is left out. */
+ * lv_crc32c_batch_device_hint makes on the host), 0 if it is left out.  A
+ * sorted batch (> 1,024 buffers, not uniform-and-unsplittable) always
+ * launches it: that launch also puts the CRCs back in buffer order. */
 int lv_crc32c_hint_needs_join(const lv_batch_hint *hint, size_t n, uint32_t cus);
 
 /* Fixed-stride form for table blocks: buffer i is
