@@ -107,7 +107,7 @@
 #ifndef LVK_SEAL_FLUSH  // rounds per seal flush (<= 16: 64 two-word slots)
 #define LVK_SEAL_FLUSH 16
 #endif
-#ifndef LVK_SST_ROWS
+#ifndef LVK_SST_ROWS  // table walk rows per batch (round 4, verify with exact waits: 4 rows 0.69 vs 3 rows 0.71, profiles/r04/sst_rows/)
 #define LVK_SST_ROWS 3
 #endif
 #ifndef LVK_SORT_MIN_WGS
