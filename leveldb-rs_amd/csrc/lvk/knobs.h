@@ -41,6 +41,7 @@
     defined(LVK_HASH_SPAN_READLANE) || \
     defined(LVK_HASH_WGS_PER_CU) || \
     defined(LVK_HASH_PREFETCH_EXACT) || \
+    defined(LVK_EXP_HASH_MUL24) || \
     defined(LVK_HASH_TAIL_READ) || \
     defined(LVK_HASH_LDS_ALL) || \
     defined(LVK_WALK_EXACT) || \
@@ -136,6 +137,9 @@
 #endif
 #ifndef LVK_HASH_TAIL_READ  // hash: the tail word re-read after the chain, not captured in it
 #define LVK_HASH_TAIL_READ 1
+#endif
+#ifndef LVK_EXP_HASH_MUL24  // timing only: the hash chain's multiply as v_mul_u32_u24 (wrong hashes)
+#define LVK_EXP_HASH_MUL24 0
 #endif
 #ifndef LVK_HASH_PREFETCH_EXACT  // hash: the next set's metadata loaded by every lane (clamped), no exec mask
 #define LVK_HASH_PREFETCH_EXACT 1
