@@ -503,7 +503,9 @@ def sweep_bench(args):
     per block size, 2 GiB of blocks in HBM, (a) lv_crc32c_batch_strided on
     aligned blocks (uniform-block kernel) and (b) lv_crc32c_batch_device on
     the same sizes byte-packed from a 13-B offset (every block misaligned:
-    sort + class kernel).  HIP-event mean over the timed launches; 64 blocks
+    sort + class kernel; with a uniform hint the class kernel alone), and (c)
+    the aligned layout through the offsets API with LV_HINT_ALIGNED16 (the
+    uniform-block kernel reading each start from the offsets).  HIP-event mean over the timed launches; 64 blocks
     of each configuration are checked against the oracle in the run."""
     import numpy as np
     import torch
@@ -529,16 +531,21 @@ def sweep_bench(args):
         ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
         row = {"block_KiB": kib, "blocks": n}
         hint = lvgpu.BatchHint(n * bl, bl, 1)  # uniform, nothing splits: the class kernel alone, no sort
+        # the strided layout through the offsets API with LV_HINT_ALIGNED16: the blocks kernel, gathering
+        o_al = torch.arange(n, dtype=torch.int64, device=dev) * bl
+        hint_al = lvgpu.BatchHint(n * bl, bl, lvgpu.HINT_UNIFORM | lvgpu.HINT_ALIGNED16)
         for api, fn in (("strided", lambda: lvgpu.batch_strided(arena, bl, bl, n, out=out)),
                         ("offsets", lambda: lvgpu.batch_ws(arena, o, ln, ws, out=out)),
-                        ("offsets_hint", lambda: lvgpu.batch_hint(arena, o, ln, hint, out=out, workspace=ws))):
+                        ("offsets_hint", lambda: lvgpu.batch_hint(arena, o, ln, hint, out=out, workspace=ws)),
+                        ("offsets_hint_aligned",
+                         lambda: lvgpu.batch_hint(arena, o_al, ln, hint_al, out=out, workspace=ws))):
             out.fill_(0)
             _, avg = _event_times(torch, fn, steps, warm)
             fn()
             kern = lvgpu.last_kernel()
             torch.cuda.synchronize()
             k = 64
-            base = 0 if api == "strided" else 13
+            base = 0 if api in ("strided", "offsets_hint_aligned") else 13
             row.setdefault("kernels", {})[api] = kern
             host = arena[:base + k * bl].cpu().numpy()
             want = np.zeros(k, dtype=np.uint32)
@@ -551,7 +558,7 @@ def sweep_bench(args):
             row[api] = {"GB_per_s": round(gbs, 1), "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 4),
                         "ms_avg": round(avg, 4)}
         rows.append(row)
-        del out, o, ln, ws
+        del out, o, o_al, ln, ws
     res = {"metric": "device-resident batched CRC32C across the 4-64 KiB target range", "unit": "GB/s",
            "bytes_per_size": total, "results": rows,
            "timing": "HIP events around each call, mean of the timed launches after warmup",
@@ -586,9 +593,13 @@ def long_bench(args):
         ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
         row = {"blocks": n, "block_bytes": bl}
         hint = lvgpu.BatchHint(n * bl, bl, 1)  # uniform: what a caller that knows its lengths passes
+        # ... and that knows its buffers start 16-B aligned (the strided API's kernels, gathering)
+        hint_al = lvgpu.BatchHint(n * bl, bl, lvgpu.HINT_UNIFORM | lvgpu.HINT_ALIGNED16)
         for api, fn in (("strided", lambda: lvgpu.batch_strided(arena, bl, bl, n, out=out)),
                         ("offsets", lambda: lvgpu.batch_ws(arena, o, ln, ws, out=out)),
-                        ("offsets_hint", lambda: lvgpu.batch_hint(arena, o, ln, hint, out=out, workspace=ws))):
+                        ("offsets_hint", lambda: lvgpu.batch_hint(arena, o, ln, hint, out=out, workspace=ws)),
+                        ("offsets_hint_aligned",
+                         lambda: lvgpu.batch_hint(arena, o, ln, hint_al, out=out, workspace=ws))):
             p50, avg = _event_times(torch, fn, max(20, min(args.steps, 100)), max(10, min(args.warmup, 50)))
             fn()
             kern = lvgpu.last_kernel()

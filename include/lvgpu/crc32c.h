@@ -90,11 +90,20 @@ int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, con
  * whole length sort and the join (the buffers are walked in index order) --
  * which the device-only call cannot know without a host sync.
  * The facts must be exact (max_len may be any upper bound of the lengths): a
- * hint that understates them gives wrong CRCs. */
+ * hint that understates them gives wrong CRCs.
+ * A uniform batch whose buffers all start 16-byte aligned (uniform ==
+ * LV_HINT_UNIFORM | LV_HINT_ALIGNED16; SST blocks of a fixed size, pages) and
+ * whose length is a multiple of 1 KiB runs on the kernels of
+ * lv_crc32c_batch_strided with each buffer's start read from d_off: no sort,
+ * no join, the long-buffer split of the strided API (the library checks that
+ * d_arena is 16-byte aligned and otherwise ignores the bit). */
+#define LV_HINT_UNIFORM 1u
+#define LV_HINT_ALIGNED16 2u
 typedef struct lv_batch_hint {
     uint64_t total_bytes; /* sum of d_len[i] */
     uint32_t max_len;     /* an upper bound of every d_len[i] */
-    uint32_t uniform;     /* nonzero: every d_len[i] == max_len (then total_bytes == n * max_len) */
+    uint32_t uniform;     /* nonzero: every d_len[i] == max_len (then total_bytes == n * max_len); bit
+                             LV_HINT_ALIGNED16: also every d_arena + d_off[i] is 16-byte aligned */
 } lv_batch_hint;
 
 /* lv_crc32c_batch_device(_ws) with an optional hint (NULL = no hint) and an
@@ -108,7 +117,10 @@ int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, c
  * `cus` compute units, launches the long-buffer join (the decision
  * lv_crc32c_batch_device_hint makes on the host), 0 if it is left out.  A
  * sorted batch (> 1,024 buffers, not uniform-and-unsplittable) always
- * launches it: that launch also puts the CRCs back in buffer order. */
+ * launches it: that launch also puts the CRCs back in buffer order.  With
+ * LV_HINT_ALIGNED16 (an aligned d_arena assumed) and whole-KiB lengths, the
+ * join is the strided API's, launched when a split's pieces are not joined
+ * inside the walk. */
 int lv_crc32c_hint_needs_join(const lv_batch_hint *hint, size_t n, uint32_t cus);
 
 /* Fixed-stride form for table blocks: buffer i is

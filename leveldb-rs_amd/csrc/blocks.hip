@@ -66,7 +66,13 @@ __device__ __forceinline__ void fuse_pieces(const Params &P, const uint32_t *fm,
     if (v < P.n && k == 0) P.out[v >> P.pshift] = final_crc(P, acc);
 }
 static_assert(kFuseMax * 33 <= kWaves * 64, "fused combine matrices fit g_oidx");
-template <int G, bool SEEDED, bool PIECES = false, bool FUSE = false>
+// GATHER: the offsets API with an aligned uniform hint (lv_batch_hint,
+// LV_HINT_ALIGNED16) -- block k starts at base + off[k] instead of base +
+// k * stride, every start 16-B aligned and every block blen bytes, so the
+// walk is the strided one.  A wave needs the next round's offset when it
+// leaves a block; it loads the offset of the block after that at every step
+// (as it does the seed), so no batch load waits on an offset load.
+template <int G, bool SEEDED, bool PIECES = false, bool FUSE = false, bool GATHER = false>
 __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint32_t nb,
                                                                  const uint4 *__restrict__ image) {
     static_assert(!FUSE || (PIECES && G == 16), "fused combine: pieces of the G = 16 kernel");
@@ -83,11 +89,19 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     // has a block; groups past the end are masked.
     const uint64_t wblk0 = (static_cast<uint64_t>(blockIdx.x) * kW + wave) * kGroups;
     const uint64_t pmask = (1ull << P.pshift) - 1;
-    auto block_ptr = [&](uint64_t k) {
+    // the start of block k's block (of piece k's block) relative to base
+    auto block_off = [&](uint64_t k) -> uint64_t {
         const uint64_t kk = k < P.n ? k : 0;
-        if constexpr (PIECES) return P.base + (kk >> P.pshift) * P.stride + (kk & pmask) * P.plen + 16u * gl;
-        return P.base + kk * P.stride + 16u * gl;
+        const uint64_t b = PIECES ? kk >> P.pshift : kk;
+        if constexpr (GATHER) return P.off[b];
+        return b * P.stride;
     };
+    auto block_at = [&](uint64_t k, uint64_t bo) {
+        const uint64_t kk = k < P.n ? k : 0;
+        if constexpr (PIECES) return P.base + bo + (kk & pmask) * P.plen + 16u * gl;
+        return P.base + bo + 16u * gl;
+    };
+    auto block_ptr = [&](uint64_t k) { return block_at(k, block_off(k)); };
     // the word xored into lane 0's first word of block k: ~seed (0 -> ~0)
     // for a whole block or a first piece, 0 for a later piece (raw R(0, .))
     auto seed_ld = [&](uint64_t k) -> uint32_t {
@@ -103,6 +117,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     // The first batch (and seed) is requested before the table image is
     // staged, so its HBM latency overlaps the staging.
     uint64_t ptr = block_ptr(blk);
+    uint64_t o1 = GATHER ? block_off(blk + gstride) : 0;  // GATHER: the next round's block offset
+    uint64_t o2 = o1;                                      // ... and the one after it, in flight
     uint32_t s0 = kVarS0 ? seed_ld(blk) : 0xffffffffu;
     uint32_t s0n = s0;
     uint4 slot0[U], slot1[U];
@@ -179,10 +195,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     auto step = [&](uint64_t r, uint32_t j, uint4(&cur)[U], uint4(&nxt)[U]) {
         const bool lastj = j + 1 == nb;
         const bool more = !lastj || r + 1 < rounds;
-        const uint64_t nptr = lastj ? block_ptr(blk + gstride) : ptr + kBatch;
+        if constexpr (GATHER) o2 = block_off(blk + 2 * gstride);
+        const uint64_t nptr = lastj ? (GATHER ? block_at(blk + gstride, o1) : block_ptr(blk + gstride)) : ptr + kBatch;
         // no next batch: a dummy read of the arena's first row, the same lines
-        // for every wave (L2 hits)
-        const uint64_t lptr = more ? nptr : P.base + 16u * gl;
+        // for every wave (L2 hits); GATHER rereads this batch (the caller's
+        // arena pointer need not be readable)
+        const uint64_t lptr = more ? nptr : GATHER ? ptr : P.base + 16u * gl;
         if constexpr (kVarS0) s0n = seed_ld(blk + gstride);
 #pragma unroll
         for (uint32_t i = 0; i < U; ++i) nxt[i] = load16(lptr + kRow * i);
@@ -208,6 +226,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
             }
             blk += gstride;
             if constexpr (kVarS0) s0 = s0n;
+            if constexpr (GATHER) o1 = o2;
         }
         ptr = nptr;
     };
@@ -396,16 +415,16 @@ int pick_block_gi(uint64_t base, uint64_t stride, uint64_t blen, int forced, uin
     return -1;
 }
 
-template <int G>
-void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, uint32_t blen,
-                     uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t s) {
+template <int G, bool GATHER>
+void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, const uint64_t *off,
+                     uint32_t blen, uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t s) {
     const uint64_t groups_per_wg = static_cast<uint64_t>(lvk::kWaves) * (64 / G);
     uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
     if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
     if (grid == 0) grid = 1;
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(base);
-    P.off = nullptr;
+    P.off = off;
     P.len = nullptr;
     P.seed = seed;
     P.out = out;
@@ -416,24 +435,114 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
     P.ent = nullptr;
     P.sseed = nullptr;
     const uint32_t nb = static_cast<uint32_t>(blen / (16ull * G * lvk::U));
-    static const std::string name = "crc32c_blocks_kernel<" + std::to_string(G) + ">";
+    static const std::string name = "crc32c_blocks_kernel<" + std::to_string(G) + (GATHER ? ",gather>" : ">");
     g_kernel = name.c_str();
     if (seed)
-        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G, true>), dim3(static_cast<uint32_t>(grid)),
-                           dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
+        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G, true, false, false, GATHER>),
+                           dim3(static_cast<uint32_t>(grid)), dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
     else
-        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G, false>), dim3(static_cast<uint32_t>(grid)),
-                           dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
+        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<G, false, false, false, GATHER>),
+                           dim3(static_cast<uint32_t>(grid)), dim3(lvk::kThreads), 0, s, P, nb, c.image[gi]);
 }
 
-void launch_blocks(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, uint32_t blen,
+template <bool GATHER>
+void launch_blocks(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, const uint64_t *off, uint32_t blen,
                    uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t s) {
     switch (gi) {
-        case 0: launch_blocks_g<1>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
-        case 1: launch_blocks_g<4>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
-        case 2: launch_blocks_g<16>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
-        default: launch_blocks_g<64>(c, gi, base, stride, blen, n, seed, out, flags, s); break;
+        case 0: launch_blocks_g<1, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
+        case 1: launch_blocks_g<4, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
+        case 2: launch_blocks_g<16, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
+        default: launch_blocks_g<64, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
     }
+}
+
+// The long-block split: the piece walk (the fused join when the pieces fill
+// one round of <= kFuseMax per block) and, unfused, the join launch.
+template <bool GATHER>
+void launch_pieces(DevCtx &c, uint32_t ps, const uint32_t *mats, const uint32_t *tabs, const uint8_t *base,
+                   uint64_t stride, const uint64_t *off, uint32_t blen, uint64_t n, const uint32_t *seed,
+                   uint32_t *out, uint32_t flags, hipStream_t hs, uint32_t *scr) {
+    const uint64_t nv = n << ps, plen = blen >> ps;
+    const uint32_t nb = static_cast<uint32_t>(plen / (16ull * 16 * lvk::U));
+    lvk::Params P{};
+    P.base = reinterpret_cast<uint64_t>(base);
+    P.off = off;
+    P.seed = seed;
+    P.n = nv;
+    P.stride = stride;
+    P.blen = static_cast<uint32_t>(plen);
+    P.flags = flags;
+    P.plen = plen;
+    P.pshift = ps;
+    P.mats = mats;
+    if (!scr) {  // one round of the grid: each workgroup joins its own blocks' pieces
+        P.out = out;
+        const dim3 grid(static_cast<uint32_t>((nv + 63) / 64));
+        if (seed)
+            hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, true, true, true, GATHER>), grid, dim3(lvk::kThreads), 0,
+                               hs, P, nb, c.image[2]);
+        else
+            hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true, true, GATHER>), grid, dim3(lvk::kThreads),
+                               0, hs, P, nb, c.image[2]);
+        g_kernel = GATHER ? "crc32c_blocks_kernel<16,pieces,fused,gather>" : "crc32c_blocks_kernel<16,pieces,fused>";
+        return;
+    }
+    P.out = scr;
+    const uint64_t grid = std::min<uint64_t>(c.cus, (nv + 63) / 64);
+    if (seed)
+        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, true, true, false, GATHER>), dim3(static_cast<uint32_t>(grid)),
+                           dim3(lvk::kThreads), 0, hs, P, nb, c.image[2]);
+    else
+        hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true, false, GATHER>),
+                           dim3(static_cast<uint32_t>(grid)), dim3(lvk::kThreads), 0, hs, P, nb, c.image[2]);
+    if (ps >= 11) {  // > 1,024 pieces per block: a workgroup per block
+        hipLaunchKernelGGL(lvk::combine_pieces_wg_kernel, dim3(static_cast<uint32_t>(n)), dim3(1024), 0, hs, P.out,
+                           1u << ps, tabs, out, flags);
+        g_kernel = GATHER ? "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_wg_kernel"
+                          : "crc32c_blocks_kernel<16,pieces>+combine_pieces_wg_kernel";
+    } else {
+        hipLaunchKernelGGL(lvk::combine_pieces_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(1024, (n + 3) / 4))),
+                           dim3(256), 0, hs, P.out, n, 1u << ps, mats, out, flags);
+        g_kernel = GATHER ? "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_kernel"
+                          : "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel";
+    }
+}
+
+UniformPlan uniform_plan(int cus, uint64_t base, uint64_t stride, uint32_t blen, uint64_t n, int gi) {
+    UniformPlan pl{};
+    pl.ps = pick_split(base, stride, blen, n, gi, cus);
+    pl.bgi = -1;
+    if (pl.ps > 0) {
+        const uint64_t nv = n << pl.ps;
+        const bool fused = (1u << pl.ps) <= lvk::kFuseMax && nv <= 64ull * static_cast<uint64_t>(cus);
+        pl.scratch = fused ? 0 : nv * 4;
+    } else {
+        pl.bgi = pick_block_gi(base, stride, blen, gi, n, cus);
+    }
+    return pl;
+}
+
+int launch_uniform(DevCtx &c, const UniformPlan &pl, const uint8_t *base, uint64_t stride, const uint64_t *off,
+                   uint32_t blen, uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t hs,
+                   uint8_t *scr) {
+    if (pl.ps > 0) {
+        const uint64_t plen = blen >> pl.ps;
+        const uint32_t *mats = nullptr, *tabs = nullptr;
+        if (int rc = piece_mats(c, plen, &mats)) return rc;
+        if (pl.scratch && pl.ps >= 11)
+            if (int rc = piece_tabs(c, plen, &tabs)) return rc;
+        uint32_t *s32 = pl.scratch ? reinterpret_cast<uint32_t *>(scr) : nullptr;
+        if (off)
+            launch_pieces<true>(c, pl.ps, mats, tabs, base, stride, off, blen, n, seed, out, flags, hs, s32);
+        else
+            launch_pieces<false>(c, pl.ps, mats, tabs, base, stride, off, blen, n, seed, out, flags, hs, s32);
+        return 0;
+    }
+    if (off)
+        launch_blocks<true>(c, pl.bgi, base, stride, off, blen, n, seed, out, flags, hs);
+    else
+        launch_blocks<false>(c, pl.bgi, base, stride, off, blen, n, seed, out, flags, hs);
+    return 0;
 }
 
 }  // namespace lvh
@@ -452,77 +561,19 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
     if (int rc = current_ctx(&c)) return rc;
     const int gi = forced_gi(flags);
     hipStream_t hs = static_cast<hipStream_t>(stream);
-    const uint32_t ps = pick_split(reinterpret_cast<uint64_t>(d_base), stride, block_len, n, gi, c->cus);
-    if (ps > 0) {
-        const uint64_t nv = static_cast<uint64_t>(n) << ps, plen = block_len >> ps;
-        const uint32_t *mats = nullptr;
-        if (int rc = piece_mats(*c, plen, &mats)) return rc;
-        const uint32_t nb = static_cast<uint32_t>(plen / (16ull * 16 * lvk::U));
-        if ((1u << ps) <= lvk::kFuseMax && nv <= 64ull * static_cast<uint64_t>(c->cus)) {
-            // one round of the grid: each workgroup joins its own blocks' pieces
-            lvk::Params P{};
-            P.base = reinterpret_cast<uint64_t>(d_base);
-            P.seed = d_seed;
-            P.out = d_out;
-            P.n = nv;
-            P.stride = stride;
-            P.blen = static_cast<uint32_t>(plen);
-            P.flags = flags;
-            P.plen = plen;
-            P.pshift = ps;
-            P.mats = mats;
-            const dim3 grid(static_cast<uint32_t>((nv + 63) / 64));
-            if (d_seed)
-                hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, true, true, true>), grid, dim3(lvk::kThreads), 0, hs,
-                                   P, nb, c->image[2]);
-            else
-                hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true, true>), grid, dim3(lvk::kThreads), 0,
-                                   hs, P, nb, c->image[2]);
-            g_kernel = "crc32c_blocks_kernel<16,pieces,fused>";
-            return check_launch();
-        }
+    const UniformPlan pl = uniform_plan(c->cus, reinterpret_cast<uint64_t>(d_base), stride, block_len, n, gi);
+    if (pl.applies()) {
+        // aligned whole-batch blocks: the uniform-block kernel, or its split
         uint8_t *scr = nullptr;
         std::unique_lock<std::mutex> ws_lk;  // held through both launches
-        if (int rc = stream_ws_bytes(*c, hs, nv * 4, &scr, &ws_lk)) return rc;
-        lvk::Params P{};
-        P.base = reinterpret_cast<uint64_t>(d_base);
-        P.seed = d_seed;
-        P.out = reinterpret_cast<uint32_t *>(scr);
-        P.n = nv;
-        P.stride = stride;
-        P.blen = static_cast<uint32_t>(plen);
-        P.plen = plen;
-        P.pshift = ps;
-        const uint64_t grid = std::min<uint64_t>(c->cus, (nv + 63) / 64);
-        if (d_seed)
-            hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, true, true>), dim3(static_cast<uint32_t>(grid)),
-                               dim3(lvk::kThreads), 0, hs, P, nb, c->image[2]);
-        else
-            hipLaunchKernelGGL((lvk::crc32c_blocks_kernel<16, false, true>), dim3(static_cast<uint32_t>(grid)),
-                               dim3(lvk::kThreads), 0, hs, P, nb, c->image[2]);
-        const uint32_t *tabs = nullptr;
-        if (int rc = piece_tabs(*c, plen, &tabs)) return rc;
-        if (ps >= 11) {  // > 1,024 pieces per block: a workgroup per block
-            hipLaunchKernelGGL(lvk::combine_pieces_wg_kernel, dim3(static_cast<uint32_t>(n)), dim3(1024), 0, hs, P.out,
-                               1u << ps, tabs, d_out, flags);
-            g_kernel = "crc32c_blocks_kernel<16,pieces>+combine_pieces_wg_kernel";
-        } else {
-            hipLaunchKernelGGL(lvk::combine_pieces_kernel,
-                               dim3(static_cast<uint32_t>(std::min<uint64_t>(1024, (n + 3) / 4))), dim3(256), 0, hs,
-                               P.out, static_cast<uint64_t>(n), 1u << ps, mats, d_out, flags);
-            g_kernel = "crc32c_blocks_kernel<16,pieces>+combine_pieces_kernel";
-        }
-        return check_launch();
-    }
-    // Aligned whole-batch blocks take the uniform-block kernel.
-    const int bgi = pick_block_gi(reinterpret_cast<uint64_t>(d_base), stride, block_len, gi, n, c->cus);
-    if (bgi >= 0) {
-        launch_blocks(*c, bgi, d_base, stride, block_len, n, d_seed, d_out, flags,
-                      static_cast<hipStream_t>(stream));
+        if (pl.scratch)
+            if (int rc = stream_ws_bytes(*c, hs, pl.scratch, &scr, &ws_lk)) return rc;
+        if (int rc = launch_uniform(*c, pl, d_base, stride, nullptr, block_len, n, d_seed, d_out, flags, hs, scr))
+            return rc;
         return check_launch();
     }
     launch_g<true>(*c, gi >= 0 ? gi : pick_gi(block_len), d_base, nullptr, nullptr, stride, block_len, d_seed,
-                   d_out, n, flags, static_cast<hipStream_t>(stream));
+                   d_out, n, flags, hs);
     return check_launch();
 }
 

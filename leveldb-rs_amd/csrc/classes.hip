@@ -601,6 +601,12 @@ static uint32_t host_split_rule(uint32_t L, uint64_t total, uint32_t *p) {
 // workgroup's static rounds of the fused kernel, which joins those itself
 // (the same unit layout crc32c_fused_small_kernel computes on the device).
 bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
+    if ((h.uniform & LV_HINT_ALIGNED16) && h.max_len) {
+        // (an aligned arena) the strided API's kernels: a join launch
+        // (combine_pieces_*) only for a split whose pieces do not join in the walk
+        const UniformPlan pl = uniform_plan(static_cast<int>(cus), 0, 0, h.max_len, n, -1);
+        if (pl.applies()) return pl.scratch != 0;
+    }
     uint32_t p = 0;
     const bool nosplit = host_split_rule(h.max_len, h.total_bytes, &p) == 0;  // monotone: nothing splits
     // > kFusedMax buffers: the sorted path's join launch also unsorts the
@@ -706,9 +712,23 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
         if (ws_bytes < sort_ws_bytes(n)) return set_err(LV_ERR_INVALID, "workspace too small");
         if (reinterpret_cast<uintptr_t>(d_ws) % 16) return set_err(LV_ERR_INVALID, "workspace must be 16-byte aligned");
         // no initialisation: every workspace word the sort reads, it wrote first
-    } else if (int rc = stream_ws(*c, s, n, &d_ws, &ws_lk)) {
-        return rc;
     }
+    if (hint && (hint->uniform & LV_HINT_ALIGNED16) && hint->max_len &&
+        reinterpret_cast<uintptr_t>(d_arena) % 16 == 0) {
+        // aligned uniform buffers: the strided API's kernels with each start
+        // read from d_off (no sort, no class kernel, no unsort)
+        const UniformPlan pl = uniform_plan(c->cus, 0, 0, hint->max_len, n, -1);
+        if (pl.applies() && (!d_ws || ws_bytes >= pl.scratch)) {
+            uint8_t *scr = d_ws;
+            if (pl.scratch && !scr)
+                if (int rc = stream_ws_bytes(*c, s, pl.scratch, &scr, &ws_lk)) return rc;
+            if (int rc = launch_uniform(*c, pl, d_arena, 0, d_off, hint->max_len, n, d_seed, d_out, flags, s, scr))
+                return rc;
+            return check_launch();
+        }
+    }
+    if (!d_ws)
+        if (int rc = stream_ws(*c, s, n, &d_ws, &ws_lk)) return rc;
     if (hint && hint->uniform && n > lvk::kFusedMax) {
         uint32_t p = 0;
         if (host_split_rule(hint->max_len, hint->total_bytes, &p) == 0) {

@@ -498,9 +498,18 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
         hint.max_len = std::max(hint.max_len, h_len[i]);
     }
     for (size_t i = 0; i < n && hint.uniform; ++i) hint.uniform = h_len[i] == hint.max_len;
-    const bool join = hint_needs_join(hint, n, static_cast<uint32_t>(c->cus));
-    if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s, join))
+    bool aligned = hint.uniform && hint.max_len && reinterpret_cast<uintptr_t>(c->d_arena) % 16 == 0;
+    for (size_t i = 0; i < n && aligned; ++i) aligned = h_off[i] % 16 == 0;
+    const UniformPlan pl = aligned ? uniform_plan(c->cus, 0, 0, hint.max_len, n, -1) : UniformPlan{0, -1, 0};
+    if (pl.applies() && pl.scratch <= sort_ws_bytes(n)) {
+        // aligned uniform blocks (LV_HINT_ALIGNED16): the strided API's kernels
+        if (int rc = launch_uniform(*c, pl, c->d_arena, 0, d_off, hint.max_len, n, h_seed ? d_seed : nullptr, d_out,
+                                    flags, s, ws))
+            return rc;
+    } else if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s,
+                                      hint_needs_join(hint, n, static_cast<uint32_t>(c->cus)))) {
         return rc;
+    }
     if (int rc = check_launch()) return rc;
     LV_HIP(hipMemcpyAsync(c->h_meta, d_out, n * 4, hipMemcpyDeviceToHost, s));
     counters().d2h += n * 4;

@@ -155,5 +155,21 @@ void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const ui
 void launch_group(const DevCtx &c, bool strided, int gi, const uint8_t *arena, const uint64_t *off,
                   const uint32_t *len, uint64_t stride, uint32_t blen, const uint32_t *seed, uint32_t *out, uint64_t n,
                   uint32_t flags, hipStream_t s);
+// The uniform-block kernels (blocks.hip) for n blocks of blen bytes, 16-B
+// aligned: the long-block split (ps > 0; `scratch` bytes of piece registers
+// unless the pieces join inside the walk) or crc32c_blocks_kernel with group
+// size kGs[bgi]; neither when the blocks are not whole 1 KiB batches.
+struct UniformPlan {
+    uint32_t ps;
+    int bgi;
+    uint64_t scratch;
+    bool applies() const { return ps > 0 || bgi >= 0; }
+};
+UniformPlan uniform_plan(int cus, uint64_t base, uint64_t stride, uint32_t blen, uint64_t n, int gi);
+// Launches a plan that applies: block k at base + off[k] (off != null, the
+// offsets API with an aligned uniform hint) or base + k * stride.
+int launch_uniform(DevCtx &c, const UniformPlan &pl, const uint8_t *base, uint64_t stride, const uint64_t *off,
+                   uint32_t blen, uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t hs,
+                   uint8_t *scr);
 
 }  // namespace lvh

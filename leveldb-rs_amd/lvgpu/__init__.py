@@ -97,6 +97,8 @@ def lib() -> ctypes.CDLL:
     L.lv_crc32c_batch_strided.restype = ctypes.c_int
     L.lv_crc32c_batch_device_hint.restype = ctypes.c_int
     L.lv_crc32c_batch_device_hint.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, vp, sz, vp]
+    L.lv_crc32c_hint_needs_join.restype = ctypes.c_int
+    L.lv_crc32c_hint_needs_join.argtypes = [vp, sz, u32]
     L.lv_crc32c_batch_strided.argtypes = [vp, u64, u32, sz, vp, vp, u32, vp]
     L.lv_crc32c_batch_host.restype = ctypes.c_int
     L.lv_crc32c_batch_host.argtypes = [vp, sz, vp, vp, vp, vp, sz, u32, ctypes.c_int]
@@ -247,12 +249,22 @@ class BatchHint(ctypes.Structure):
     _fields_ = [("total_bytes", ctypes.c_uint64), ("max_len", ctypes.c_uint32), ("uniform", ctypes.c_uint32)]
 
 
-def hint_for(lengths) -> BatchHint:
-    """The exact hint of a host-side length list (numpy-convertible)."""
+HINT_UNIFORM = 1     # LV_HINT_UNIFORM
+HINT_ALIGNED16 = 2   # LV_HINT_ALIGNED16
+
+
+def hint_for(lengths, offsets=None) -> BatchHint:
+    """The exact hint of a host-side length list (numpy-convertible); with the
+    host-side offsets too, a uniform batch whose offsets are all multiples of
+    16 also gets LV_HINT_ALIGNED16 (the library checks the arena's own
+    alignment)."""
     import numpy as np
     ln = np.asarray(lengths, dtype=np.uint64)
     mx = int(ln.max()) if ln.size else 0
-    return BatchHint(int(ln.sum()), mx, int(ln.size > 0 and bool((ln == mx).all())))
+    uniform = int(ln.size > 0 and bool((ln == mx).all()))
+    if uniform and offsets is not None and bool((np.asarray(offsets, dtype=np.uint64) % 16 == 0).all()):
+        uniform |= HINT_ALIGNED16
+    return BatchHint(int(ln.sum()), mx, uniform)
 
 
 def batch_hint(arena, off, length, hint: BatchHint, seed=None, out=None, masked=False, workspace=None,

@@ -293,3 +293,57 @@ def test_hint_join_decision_matches_the_device_layout():
         got = L.lv_crc32c_hint_needs_join(ctypes.addressof(h), n, 256)
         assert bool(got) == (n > 1024 or _split_rule(max(lens), sum(lens))[0] > 0)
         assert bool(got) >= _needs_join(lens, 256)  # never leaves out a join the device needs
+
+
+def _uniform_plan(n, blen, cus):
+    """Replica of lvh::uniform_plan (blocks.hip: pick_split, pick_block_gi,
+    the fused-join rule) for a 16-B aligned uniform batch: (pieces log2,
+    group size or None, scratch bytes)."""
+    want = 4 * cus * 16
+    ps = 0
+    while (n << ps) < want and ps < 12:
+        s2 = 2 << ps
+        if blen % s2 or (blen // s2) % 1024 or blen // s2 < 4096:
+            break
+        ps += 1
+    if ps:
+        nv = n << ps
+        fused = (1 << ps) <= 16 and nv <= 64 * cus
+        return ps, None, 0 if fused else nv * 4
+    if blen == 0:
+        return 0, None, 0
+    fits = lambda g: blen % (16 * g * 4) == 0
+    if n < want and fits(64):
+        return 0, 64, 0
+    return 0, next((g for g in (16, 4, 1) if fits(g)), None), 0
+
+
+def test_aligned_hint_join_decision():
+    """LV_HINT_ALIGNED16: a uniform batch of whole 1 KiB batches runs on the
+    strided API's kernels, whose join (combine_pieces_*) runs only for a split
+    whose pieces are not joined in the walk; other lengths keep the unaligned
+    decision."""
+    import random
+    L = lvgpu.lib()
+    cases = [(1024, 65536, 0), (1, 16 << 20, 1), (16, 1 << 20, 1), (20000, 4096, 0), (2000, 8192, 0),
+             (5000, 4000, 0), (1100, 160 << 10, 1), (600, 1000, 0)]
+    for n, size, want in cases:
+        h = lvgpu.BatchHint(n * size, size, lvgpu.HINT_UNIFORM | lvgpu.HINT_ALIGNED16)
+        assert L.lv_crc32c_hint_needs_join(ctypes.addressof(h), n, 256) == want, (n, size)
+    rng = random.Random(808)
+    for _ in range(400):
+        n = rng.randrange(1, 40000)
+        size = rng.choice([1024, 2048, 4096, 8192, 65536, 1 << 20, 3 << 20, 16 << 20, 5000, 40000])
+        cus = rng.choice([64, 80, 256, 304])
+        h = lvgpu.BatchHint(n * size, size, 3)
+        ps, g, scratch = _uniform_plan(n, size, cus)
+        got = L.lv_crc32c_hint_needs_join(ctypes.addressof(h), n, cus)
+        if ps or g:
+            assert got == int(scratch > 0), (n, size, cus)
+        else:
+            h1 = lvgpu.BatchHint(n * size, size, 1)
+            assert got == L.lv_crc32c_hint_needs_join(ctypes.addressof(h1), n, cus), (n, size, cus)
+    # hint_for sets the bit only for uniform lengths at 16-B multiples
+    assert lvgpu.hint_for([4096] * 3, [0, 4096, 8192]).uniform == 3
+    assert lvgpu.hint_for([4096] * 3, [0, 4104, 8192]).uniform == 1
+    assert lvgpu.hint_for([4096, 10], [0, 4096]).uniform == 0

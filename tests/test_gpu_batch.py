@@ -551,6 +551,27 @@ def test_host_api_long_buffers(gpu):
     assert np.array_equal(lvgpu.batch_host(arena, offs, lens, None), want)
 
 
+@pytest.mark.parametrize("L,n", [(4096, 5000), (65536, 300), (1024, 70)])
+def test_host_api_aligned_uniform_blocks(gpu, L, n):
+    """lv_crc32c_batch_host passes its own LV_HINT_ALIGNED16 fact: uniform
+    blocks at shuffled 16-B multiples run on the strided API's kernels
+    (gathering their starts); one misaligned offset sends the same batch
+    through the length sort.  Bit-exact vs the oracle both ways."""
+    rng = np.random.default_rng(L + n)
+    starts = np.cumsum(rng.integers(0, 3, n) * 16 + L) - L
+    offs = rng.permutation(starts).astype(np.uint64)
+    lens = np.full(n, L, dtype=np.uint32)
+    arena = rng.integers(0, 256, size=int(starts[-1]) + L + 32, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = oracle_batch(arena, offs, lens, seeds, True)
+    assert np.array_equal(lvgpu.batch_host(arena, offs, lens, seeds, masked=True), want)
+    assert "gather" in lvgpu.last_kernel(), lvgpu.last_kernel()
+    offs[n // 2] += 1
+    want = oracle_batch(arena, offs, lens, seeds, True)
+    assert np.array_equal(lvgpu.batch_host(arena, offs, lens, seeds, masked=True), want)
+    assert "gather" not in lvgpu.last_kernel()
+
+
 def test_two_threads_same_stream(torch_dev, arena):
     """Two host threads call the offsets API on the SAME stream (the default
     one) with different batch sizes: the library's per-stream sort workspace
@@ -977,6 +998,70 @@ def test_offsets_api_with_hint(torch_dev, case, seeded):
     torch.cuda.synchronize()
     assert np.array_equal(out2.cpu().numpy().view(np.uint32), want)
     assert np.array_equal(out3.cpu().numpy().view(np.uint32), want)
+
+
+ALIGNED_HINT_CASES = {
+    # name: (n, length, kernel substring with LV_HINT_ALIGNED16)
+    "20000x4KiB": (20000, 4096, "crc32c_blocks_kernel<16,gather>"),
+    "3000x1KiB": (3000, 1024, "crc32c_blocks_kernel<16,gather>"),
+    "40x4KiB_g64": (40, 4096, "crc32c_blocks_kernel<64,gather>"),
+    "1024x64KiB": (1024, 65536, "crc32c_blocks_kernel<16,pieces,fused,gather>"),
+    "2000x8KiB": (2000, 8192, "crc32c_blocks_kernel<16,pieces,fused,gather>"),
+    "16x1MiB": (16, 1 << 20, "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_kernel"),
+    "1x16MiB": (1, 16 << 20, "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_wg_kernel"),
+    "5000x4000B": (5000, 4000, "crc32c_classes_kernel"),  # not whole 1 KiB batches: the identity list
+    "600x1000B": (600, 1000, "crc32c_fused_small_kernel"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(ALIGNED_HINT_CASES))
+@pytest.mark.parametrize("seeded", [False, True])
+def test_offsets_api_with_aligned_hint(torch_dev, case, seeded):
+    """LV_HINT_ALIGNED16: a uniform batch of 16-B aligned buffers whose
+    length is whole 1 KiB batches runs on the strided API's kernels
+    (crc32c_blocks_kernel, its long-block split and joins) with each buffer's
+    start read from d_off.  Offsets are shuffled with gaps, so the walk must
+    gather; CRCs bit-exact vs the oracle with the library's and a caller's
+    workspace, the join query agrees with the launch, and a misaligned arena
+    ignores the bit."""
+    torch, dev = torch_dev
+    n, L, kern = ALIGNED_HINT_CASES[case]
+    rng = np.random.default_rng(sum(map(ord, case)) * 104729 + seeded)
+    gaps = rng.integers(0, 4, n) * 16
+    Lp = -(-L // 16) * 16
+    starts = np.cumsum(gaps + Lp) - Lp  # aligned, in arena order
+    offs = rng.permutation(starts).astype(np.uint64)
+    lens = np.full(n, L, dtype=np.uint32)
+    size = int(starts[-1]) + L + 64
+    arena = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    want = oracle_batch(arena, offs, lens, seeds, True)
+    a = torch.frombuffer(bytearray(arena), dtype=torch.uint8).to(dev)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    hint = lvgpu.hint_for(lens, offs)
+    assert hint.uniform == lvgpu.HINT_UNIFORM | lvgpu.HINT_ALIGNED16
+    out = lvgpu.batch_hint(a, o, ln, hint, seed=sd, masked=True)
+    k1 = lvgpu.last_kernel()
+    ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
+    out2 = lvgpu.batch_hint(a, o, ln, hint, seed=sd, masked=True, workspace=ws)
+    k2 = lvgpu.last_kernel()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(out2.cpu().numpy().view(np.uint32), want)
+    assert k1 == k2 and k1.startswith(kern), k1
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    joined = "combine" in k1
+    assert lvgpu.lib().lv_crc32c_hint_needs_join(ctypes.addressof(hint), n, cus) == int(joined)
+    # the same offsets against an arena 8 bytes off 16-B alignment: the bit is ignored
+    a8 = torch.empty(size + 8, dtype=torch.uint8, device=dev)[8:]
+    a8.copy_(a)
+    out3 = lvgpu.batch_hint(a8, o, ln, hint, seed=sd, masked=True)
+    k3 = lvgpu.last_kernel()
+    torch.cuda.synchronize()
+    assert np.array_equal(out3.cpu().numpy().view(np.uint32), want)
+    assert "gather" not in k3, k3
 
 
 def test_hint_rejects_inconsistent_uniform(torch_dev):
