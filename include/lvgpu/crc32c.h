@@ -89,14 +89,20 @@ int lv_crc32c_batch_device_ws(const uint8_t *d_arena, const uint64_t *d_off, con
  * joined inside the walk; for larger uniform batches that cannot split, the
  * whole length sort and the join (the buffers are walked in index order) --
  * which the device-only call cannot know without a host sync.
- * The facts must be exact (max_len may be any upper bound of the lengths): a
- * hint that understates them gives wrong CRCs.
+ * The facts must be exact (max_len may be any upper bound of the lengths).
+ * The kernels check them where they read what the facts describe (every
+ * offset and length on the aligned path, every length on the identity and
+ * small-batch paths, the total on the small-batch path) and record a
+ * violation for lv_crc32c_batch_check instead of failing silently; a call
+ * whose hint was violated leaves its CRCs undefined.
  * A uniform batch whose buffers all start 16-byte aligned (uniform ==
  * LV_HINT_UNIFORM | LV_HINT_ALIGNED16; SST blocks of a fixed size, pages) and
  * whose length is a multiple of 1 KiB runs on the kernels of
  * lv_crc32c_batch_strided with each buffer's start read from d_off: no sort,
  * no join, the long-buffer split of the strided API (the library checks that
- * d_arena is 16-byte aligned and otherwise ignores the bit). */
+ * d_arena is 16-byte aligned and otherwise ignores the bit).  `uniform` must
+ * be 0, LV_HINT_UNIFORM or LV_HINT_UNIFORM | LV_HINT_ALIGNED16; any other
+ * value is LV_ERR_INVALID. */
 #define LV_HINT_UNIFORM 1u
 #define LV_HINT_ALIGNED16 2u
 typedef struct lv_batch_hint {
@@ -112,6 +118,22 @@ int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, c
                                 const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
                                 const lv_batch_hint *hint, void *d_workspace, size_t workspace_bytes,
                                 void *stream);
+
+/* Hint violations found on the device (bits of lv_crc32c_batch_check's
+ * *violations). */
+#define LV_HINT_ERR_MISALIGNED 0x1u /* LV_HINT_ALIGNED16: d_off[i] % 16 != 0          */
+#define LV_HINT_ERR_NOT_UNIFORM 0x2u /* LV_HINT_UNIFORM: d_len[i] != max_len          */
+#define LV_HINT_ERR_LONGER 0x4u /* d_len[i] > max_len                                  */
+#define LV_HINT_ERR_TOTAL 0x8u /* sum of d_len[i] != total_bytes                      */
+#define LV_ERR_HINT (-4) /* a batch hint contradicted the device-side lengths/offsets */
+
+/* Stream-ordered check of the hints of every lv_crc32c_batch_device_hint call
+ * enqueued on `stream` (on the calling thread's current device) since the last
+ * check: waits for the stream, then returns LV_OK, or LV_ERR_HINT with the
+ * violated facts in *violations (may be NULL) and lv_last_error naming them;
+ * the record is cleared.  Not needed after lv_crc32c_batch_host (its hint is
+ * derived from the host arrays). */
+int lv_crc32c_batch_check(void *stream, uint32_t *violations);
 
 /* Debug query: 1 if a batch of n buffers with these facts, on a device with
  * `cus` compute units, launches the long-buffer join (the decision

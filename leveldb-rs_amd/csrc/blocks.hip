@@ -71,7 +71,12 @@ static_assert(kFuseMax * 33 <= kWaves * 64, "fused combine matrices fit g_oidx")
 // k * stride, every start 16-B aligned and every block blen bytes, so the
 // walk is the strided one.  A wave needs the next round's offset when it
 // leaves a block; it loads the offset of the block after that at every step
-// (as it does the seed), so no batch load waits on an offset load.
+// (as it does the seed), so no batch load waits on an offset load.  The
+// block's length is loaded beside its offset; where the offset is consumed
+// both are checked against the hint (a misaligned offset or a length other
+// than the hint's max_len is recorded in P.herr, lv_crc32c_batch_check), and
+// the address uses the offset rounded down to 16 B, so a lying hint costs
+// wrong CRCs it reports, never an unaligned or wider read.
 template <int G, bool SEEDED, bool PIECES = false, bool FUSE = false, bool GATHER = false>
 __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint32_t nb,
                                                                  const uint4 *__restrict__ image) {
@@ -96,8 +101,13 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         if constexpr (GATHER) return P.off[b];
         return b * P.stride;
     };
+    auto report = [&](uint32_t bad) {
+        if constexpr (GATHER)
+            if (bad && P.herr) atomicOr(P.herr, bad);
+    };
     auto block_at = [&](uint64_t k, uint64_t bo) {
         const uint64_t kk = k < P.n ? k : 0;
+        if constexpr (GATHER) bo &= ~static_cast<uint64_t>(15);
         if constexpr (PIECES) return P.base + bo + (kk & pmask) * P.plen + 16u * gl;
         return P.base + bo + 16u * gl;
     };
@@ -116,7 +126,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
 
     // The first batch (and seed) is requested before the table image is
     // staged, so its HBM latency overlaps the staging.
-    uint64_t ptr = block_ptr(blk);
+    const uint64_t o0 = block_off(blk);                    // this round's block offset
+    uint64_t ptr = block_at(blk, o0);
     uint64_t o1 = GATHER ? block_off(blk + gstride) : 0;  // GATHER: the next round's block offset
     uint64_t o2 = o1;                                      // ... and the one after it, in flight
     uint32_t s0 = kVarS0 ? seed_ld(blk) : 0xffffffffu;
@@ -124,6 +135,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
     uint4 slot0[U], slot1[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) slot0[i] = load16(ptr + kRow * i);
+    // GATHER with a hint to check: every length, a grid-strided share per
+    // thread (the walk itself never reads one).  The first four are requested
+    // here and arrive under the table staging's round trip; more (> 4 x 1,024
+    // blocks per workgroup) after it.
+    const uint64_t nblk = PIECES ? (P.n >> P.pshift) : P.n;
+    const uint64_t lstr = static_cast<uint64_t>(gridDim.x) * kThreads;
+    const uint64_t lb0 = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+    uint32_t lq[4] = {0, 0, 0, 0};
+    const bool lcheck = GATHER && P.herr;
+    if (lcheck) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint64_t b = lb0 + i * lstr;
+            lq[i] = b < nblk ? P.len[b] ^ P.hlen : 0u;
+        }
+    }
     uint32_t *const fm = &g_oidx[0][0];  // FUSE: matrix j at word 33 j (distinct banks per lane)
     if constexpr (FUSE) {
         const uint32_t nw = (1u << P.pshift) * 32u;
@@ -132,6 +159,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
 #if !LVK_EXP_NOSTAGE
     stage_tables(image);
 #endif
+    uint32_t lbad = lq[0] | lq[1] | lq[2] | lq[3];
+    if (lcheck)
+        for (uint64_t b = lb0 + 4 * lstr; b < nblk; b += lstr) lbad |= P.len[b] ^ P.hlen;
+    // GATHER: the first block's offset and this thread's share of the lengths
+    // (later offsets are checked as the walk consumes them)
+    if constexpr (GATHER) report(((o0 & 15u) ? LV_HINT_ERR_MISALIGNED : 0u) | (lbad ? LV_HINT_ERR_NOT_UNIFORM : 0u));
     if (wblk0 >= P.n) {
         if constexpr (FUSE) fuse_pieces(P, fm, g_ocrc, lane, wave);  // the barrier is workgroup-wide
         return;
@@ -226,7 +259,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
             }
             blk += gstride;
             if constexpr (kVarS0) s0 = s0n;
-            if constexpr (GATHER) o1 = o2;
+            if constexpr (GATHER) {
+                if (o1 & 15u) report(LV_HINT_ERR_MISALIGNED);  // the block walked next (o1 was consumed above)
+                o1 = o2;
+            }
         }
         ptr = nptr;
     };
@@ -417,7 +453,8 @@ int pick_block_gi(uint64_t base, uint64_t stride, uint64_t blen, int forced, uin
 
 template <int G, bool GATHER>
 void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, const uint64_t *off,
-                     uint32_t blen, uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t s) {
+                     const uint32_t *len, const HintCheck *hc, uint32_t blen, uint64_t n, const uint32_t *seed,
+                     uint32_t *out, uint32_t flags, hipStream_t s) {
     const uint64_t groups_per_wg = static_cast<uint64_t>(lvk::kWaves) * (64 / G);
     uint64_t grid = (n + groups_per_wg - 1) / groups_per_wg;
     if (grid > static_cast<uint64_t>(c.cus)) grid = c.cus;
@@ -425,7 +462,7 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(base);
     P.off = off;
-    P.len = nullptr;
+    P.len = len;
     P.seed = seed;
     P.out = out;
     P.n = n;
@@ -434,6 +471,7 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
     P.flags = flags;
     P.ent = nullptr;
     P.sseed = nullptr;
+    set_hint(P, hc, blen);
     const uint32_t nb = static_cast<uint32_t>(blen / (16ull * G * lvk::U));
     static const std::string name = "crc32c_blocks_kernel<" + std::to_string(G) + (GATHER ? ",gather>" : ">");
     g_kernel = name.c_str();
@@ -446,13 +484,14 @@ void launch_blocks_g(const DevCtx &c, int gi, const uint8_t *base, uint64_t stri
 }
 
 template <bool GATHER>
-void launch_blocks(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, const uint64_t *off, uint32_t blen,
-                   uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t s) {
+void launch_blocks(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride, const uint64_t *off,
+                   const uint32_t *len, const HintCheck *hc, uint32_t blen, uint64_t n, const uint32_t *seed,
+                   uint32_t *out, uint32_t flags, hipStream_t s) {
     switch (gi) {
-        case 0: launch_blocks_g<1, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
-        case 1: launch_blocks_g<4, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
-        case 2: launch_blocks_g<16, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
-        default: launch_blocks_g<64, GATHER>(c, gi, base, stride, off, blen, n, seed, out, flags, s); break;
+        case 0: launch_blocks_g<1, GATHER>(c, gi, base, stride, off, len, hc, blen, n, seed, out, flags, s); break;
+        case 1: launch_blocks_g<4, GATHER>(c, gi, base, stride, off, len, hc, blen, n, seed, out, flags, s); break;
+        case 2: launch_blocks_g<16, GATHER>(c, gi, base, stride, off, len, hc, blen, n, seed, out, flags, s); break;
+        default: launch_blocks_g<64, GATHER>(c, gi, base, stride, off, len, hc, blen, n, seed, out, flags, s); break;
     }
 }
 
@@ -460,13 +499,14 @@ void launch_blocks(const DevCtx &c, int gi, const uint8_t *base, uint64_t stride
 // one round of <= kFuseMax per block) and, unfused, the join launch.
 template <bool GATHER>
 void launch_pieces(DevCtx &c, uint32_t ps, const uint32_t *mats, const uint32_t *tabs, const uint8_t *base,
-                   uint64_t stride, const uint64_t *off, uint32_t blen, uint64_t n, const uint32_t *seed,
-                   uint32_t *out, uint32_t flags, hipStream_t hs, uint32_t *scr) {
+                   uint64_t stride, const uint64_t *off, const uint32_t *len, const HintCheck *hc, uint32_t blen,
+                   uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t hs, uint32_t *scr) {
     const uint64_t nv = n << ps, plen = blen >> ps;
     const uint32_t nb = static_cast<uint32_t>(plen / (16ull * 16 * lvk::U));
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(base);
     P.off = off;
+    P.len = len;
     P.seed = seed;
     P.n = nv;
     P.stride = stride;
@@ -475,6 +515,7 @@ void launch_pieces(DevCtx &c, uint32_t ps, const uint32_t *mats, const uint32_t 
     P.plen = plen;
     P.pshift = ps;
     P.mats = mats;
+    set_hint(P, hc, blen);
     if (!scr) {  // one round of the grid: each workgroup joins its own blocks' pieces
         P.out = out;
         const dim3 grid(static_cast<uint32_t>((nv + 63) / 64));
@@ -523,8 +564,8 @@ UniformPlan uniform_plan(int cus, uint64_t base, uint64_t stride, uint32_t blen,
 }
 
 int launch_uniform(DevCtx &c, const UniformPlan &pl, const uint8_t *base, uint64_t stride, const uint64_t *off,
-                   uint32_t blen, uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t hs,
-                   uint8_t *scr) {
+                   const uint32_t *len, const HintCheck *hc, uint32_t blen, uint64_t n, const uint32_t *seed,
+                   uint32_t *out, uint32_t flags, hipStream_t hs, uint8_t *scr) {
     if (pl.ps > 0) {
         const uint64_t plen = blen >> pl.ps;
         const uint32_t *mats = nullptr, *tabs = nullptr;
@@ -533,15 +574,16 @@ int launch_uniform(DevCtx &c, const UniformPlan &pl, const uint8_t *base, uint64
             if (int rc = piece_tabs(c, plen, &tabs)) return rc;
         uint32_t *s32 = pl.scratch ? reinterpret_cast<uint32_t *>(scr) : nullptr;
         if (off)
-            launch_pieces<true>(c, pl.ps, mats, tabs, base, stride, off, blen, n, seed, out, flags, hs, s32);
+            launch_pieces<true>(c, pl.ps, mats, tabs, base, stride, off, len, hc, blen, n, seed, out, flags, hs, s32);
         else
-            launch_pieces<false>(c, pl.ps, mats, tabs, base, stride, off, blen, n, seed, out, flags, hs, s32);
+            launch_pieces<false>(c, pl.ps, mats, tabs, base, stride, off, len, hc, blen, n, seed, out, flags, hs,
+                                 s32);
         return 0;
     }
     if (off)
-        launch_blocks<true>(c, pl.bgi, base, stride, off, blen, n, seed, out, flags, hs);
+        launch_blocks<true>(c, pl.bgi, base, stride, off, len, hc, blen, n, seed, out, flags, hs);
     else
-        launch_blocks<false>(c, pl.bgi, base, stride, off, blen, n, seed, out, flags, hs);
+        launch_blocks<false>(c, pl.bgi, base, stride, off, len, hc, blen, n, seed, out, flags, hs);
     return 0;
 }
 
@@ -568,7 +610,8 @@ int lv_crc32c_batch_strided(const uint8_t *d_base, uint64_t stride, uint32_t blo
         std::unique_lock<std::mutex> ws_lk;  // held through both launches
         if (pl.scratch)
             if (int rc = stream_ws_bytes(*c, hs, pl.scratch, &scr, &ws_lk)) return rc;
-        if (int rc = launch_uniform(*c, pl, d_base, stride, nullptr, block_len, n, d_seed, d_out, flags, hs, scr))
+        if (int rc = launch_uniform(*c, pl, d_base, stride, nullptr, nullptr, nullptr, block_len, n, d_seed, d_out,
+                                    flags, hs, scr))
             return rc;
         return check_launch();
     }

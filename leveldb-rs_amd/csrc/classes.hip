@@ -128,6 +128,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     }
 }
 
+// The hinted identity path's check (lv_crc32c_batch_device_hint, a uniform
+// batch walked in index order with no sort): every length must be the
+// hint's.  A launch of its own: the same check inside the class kernel, at
+// its start or its end, moved the seeded walk's register allocation into
+// spills with reloads in the round loops.
+__global__ __launch_bounds__(256) void hint_len_kernel(const uint32_t *__restrict__ len, uint64_t n, uint32_t hlen,
+                                                       uint32_t *__restrict__ err) {
+    const uint64_t str = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    uint32_t bad = 0;
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (; i + 3 * str < n; i += 4 * str)  // four loads in flight per thread
+        bad |= (len[i] ^ hlen) | (len[i + str] ^ hlen) | (len[i + 2 * str] ^ hlen) | (len[i + 3 * str] ^ hlen);
+    for (; i < n; i += str) bad |= len[i] ^ hlen;
+    if (bad) atomicOr(err, LV_HINT_ERR_NOT_UNIFORM);
+}
+
 // Joins the pieces of the offsets API's split long buffers (sort_scatter,
 // split_wave): long record {buffer, first piece slot, m, p}, pieces of
 // P = 2^p bytes aligned to the buffer end; piece 0's register is
@@ -459,6 +475,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, 
     __syncthreads();
     uint64_t total = 0;
     for (uint32_t k = 0; k < kWaves; ++k) total += (static_cast<uint64_t>(sc[2 * k + 1]) << 32) | sc[2 * k];
+    if (P.herr && blockIdx.x == 0) {
+        // the host left out the join on the hint's word: check it against
+        // the lengths (one workgroup reports)
+        uint32_t bad = 0;
+        if (t < nbuf) bad |= P.huni ? (Lt != P.hlen ? LV_HINT_ERR_NOT_UNIFORM : 0u) : (Lt > P.hlen ? LV_HINT_ERR_LONGER : 0u);
+        if (t == 0 && total != P.htotal) bad |= LV_HINT_ERR_TOTAL;
+        if (bad) atomicOr(P.herr, bad);
+    }
     uint32_t p = 0;
     const uint32_t m = t < nbuf ? split_rule(Lt, total, &p, kFusedPieceLog2, kFusedMaxPieces) : 0u;
     const uint32_t units = t < nbuf ? (m ? m : 1u) : 0u;
@@ -631,7 +655,8 @@ bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
 // Length-sorted launch of the offsets API, no host sync: the sort (one or
 // three launches), the persistent class kernel, the long-buffer join.
 int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join) {
+                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join,
+                  const HintCheck *hc) {
     uint32_t *ws = reinterpret_cast<uint32_t *>(ws_bytes);
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(arena);
@@ -651,6 +676,10 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
         longs = reinterpret_cast<uint4 *>(ws_bytes + lay.longs);
         P.part = reinterpret_cast<uint32_t *>(ws_bytes + lay.part);
         P.tabs = c.base_tabs;
+        // the hint decided whether the join runs: the kernel checks its facts
+        // against the lengths it reads (the sorted path below always joins,
+        // so no fact of the hint changes what it computes)
+        set_hint(P, hc, 0);
         g_kernel = join ? "crc32c_fused_small_kernel+combine_long_kernel" : "crc32c_fused_small_kernel";
         if (seed)
             hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<true>, dim3(static_cast<uint32_t>(c.cus)),
@@ -713,6 +742,16 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
         if (reinterpret_cast<uintptr_t>(d_ws) % 16) return set_err(LV_ERR_INVALID, "workspace must be 16-byte aligned");
         // no initialisation: every workspace word the sort reads, it wrote first
     }
+    // the hint's facts travel to the kernels that read what they describe
+    HintCheck hcv{nullptr, 0, 0, 0};
+    const HintCheck *hc = nullptr;
+    if (hint) {
+        if (int rc = stream_err(*c, s, &hcv.err)) return rc;
+        hcv.total = hint->total_bytes;
+        hcv.len = hint->max_len;
+        hcv.uniform = hint->uniform;
+        hc = &hcv;
+    }
     if (hint && (hint->uniform & LV_HINT_ALIGNED16) && hint->max_len &&
         reinterpret_cast<uintptr_t>(d_arena) % 16 == 0) {
         // aligned uniform buffers: the strided API's kernels with each start
@@ -722,10 +761,20 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
             uint8_t *scr = d_ws;
             if (pl.scratch && !scr)
                 if (int rc = stream_ws_bytes(*c, s, pl.scratch, &scr, &ws_lk)) return rc;
-            if (int rc = launch_uniform(*c, pl, d_arena, 0, d_off, hint->max_len, n, d_seed, d_out, flags, s, scr))
+            if (int rc = launch_uniform(*c, pl, d_arena, 0, d_off, d_len, hc, hint->max_len, n, d_seed, d_out, flags,
+                                        s, scr))
                 return rc;
             return check_launch();
         }
+    }
+    // Past this point the aligned path did not run (a misaligned arena, a
+    // length that is not whole batches, a short caller workspace): the join
+    // decision below must not assume it did.
+    lv_batch_hint h2{};
+    if (hint) {
+        h2 = *hint;
+        h2.uniform &= ~LV_HINT_ALIGNED16;
+        hint = &h2;
     }
     if (!d_ws)
         if (int rc = stream_ws(*c, s, n, &d_ws, &ws_lk)) return rc;
@@ -745,13 +794,16 @@ static int batch_device_impl(const uint8_t *d_arena, const uint64_t *d_off, cons
             P.flags = flags;
             const uint32_t L = hint->max_len;
             P.hident = 1u + (L <= 256u ? 0u : L <= 2048u ? 1u : L <= 32768u ? 2u : 3u);  // 1 + lvk::len_class(L)
-            g_kernel = "crc32c_classes_kernel";
+            g_kernel = "hint_len_kernel+crc32c_classes_kernel";
+            const uint64_t lg = std::min<uint64_t>(4ull * static_cast<uint64_t>(c->cus), (n + 1023) / 1024);
+            hipLaunchKernelGGL(lvk::hint_len_kernel, dim3(static_cast<uint32_t>(lg)), dim3(256), 0, s, d_len,
+                               static_cast<uint64_t>(n), L, hcv.err);
             launch_classes(*c, d_seed != nullptr, P, reinterpret_cast<const uint32_t *>(d_ws), s);
             return check_launch();
         }
     }
     const bool join = hint ? hint_needs_join(*hint, n, static_cast<uint32_t>(c->cus)) : true;
-    if (int rc = launch_binned(*c, d_ws, d_arena, d_off, d_len, d_seed, d_out, n, flags, s, join)) return rc;
+    if (int rc = launch_binned(*c, d_ws, d_arena, d_off, d_len, d_seed, d_out, n, flags, s, join, hc)) return rc;
     return check_launch();
 }
 
@@ -772,6 +824,9 @@ int lv_crc32c_batch_device_hint(const uint8_t *d_arena, const uint64_t *d_off, c
                                 const uint32_t *d_seed, uint32_t *d_out, size_t n, uint32_t flags,
                                 const lv_batch_hint *hint, void *d_workspace, size_t workspace_bytes, void *stream) {
     if (hint) {
+        if (hint->uniform != 0 && hint->uniform != LV_HINT_UNIFORM &&
+            hint->uniform != (LV_HINT_UNIFORM | LV_HINT_ALIGNED16))
+            return set_err(LV_ERR_INVALID, "hint: uniform must be 0, LV_HINT_UNIFORM or LV_HINT_UNIFORM | LV_HINT_ALIGNED16");
         if (hint->uniform && hint->total_bytes != static_cast<uint64_t>(n) * hint->max_len)
             return set_err(LV_ERR_INVALID, "uniform hint: total_bytes != n * max_len");
         if (n && hint->max_len == 0 && hint->total_bytes != 0)

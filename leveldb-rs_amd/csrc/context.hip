@@ -201,14 +201,19 @@ int forced_gi(uint32_t flags) {
 // The library-owned workspace of (device, stream), grown on demand (the sort
 // needs no initialised state).  Returns with the workspace's lock held in
 // `lk`; the caller keeps it until its last launch has been enqueued.
-int stream_ws_bytes(DevCtx &c, hipStream_t s, size_t need, uint8_t **out, std::unique_lock<std::mutex> *lk) {
-    StreamWs *w = nullptr;
-    {
-        std::lock_guard<std::mutex> mk(c.ws_m);
-        auto &slot = c.ws[s];
-        if (!slot) slot.reset(new StreamWs);
-        w = slot.get();
+static StreamWs *find_ws(DevCtx &c, hipStream_t s, bool create) {
+    std::lock_guard<std::mutex> mk(c.ws_m);
+    if (!create) {
+        auto it = c.ws.find(s);
+        return it == c.ws.end() ? nullptr : it->second.get();
     }
+    auto &slot = c.ws[s];
+    if (!slot) slot.reset(new StreamWs);
+    return slot.get();
+}
+
+int stream_ws_bytes(DevCtx &c, hipStream_t s, size_t need, uint8_t **out, std::unique_lock<std::mutex> *lk) {
+    StreamWs *w = find_ws(c, s, true);
     *lk = std::unique_lock<std::mutex>(w->m);
     if (w->cap < need) {
         if (w->p) LV_HIP(hipFree(w->p));
@@ -224,6 +229,44 @@ int stream_ws_bytes(DevCtx &c, hipStream_t s, size_t need, uint8_t **out, std::u
 
 int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_lock<std::mutex> *lk) {
     return stream_ws_bytes(c, s, sort_ws_bytes(n), out, lk);
+}
+
+// The stream's hint-violation word (zeroed on the stream before first use).
+int stream_err(DevCtx &c, hipStream_t s, uint32_t **out) {
+    StreamWs *w = find_ws(c, s, true);
+    std::lock_guard<std::mutex> lk(w->em);
+    if (!w->err) {
+        LV_HIP(hipHostMalloc(reinterpret_cast<void **>(&w->herr), 4, hipHostMallocDefault));
+        LV_HIP(hipMalloc(&w->err, 4));
+        counters().allocs += 2;
+        LV_HIP(hipMemsetAsync(w->err, 0, 4, s));
+    }
+    *out = w->err;
+    return 0;
+}
+
+// lv_crc32c_batch_check: read and clear the stream's violation word.
+int check_hints(hipStream_t s, uint32_t *violations) {
+    if (violations) *violations = 0;
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    StreamWs *w = find_ws(*c, s, false);
+    if (!w) return LV_OK;  // no hinted call on this stream yet
+    std::lock_guard<std::mutex> lk(w->em);
+    if (!w->err) return LV_OK;
+    LV_HIP(hipMemcpyAsync(w->herr, w->err, 4, hipMemcpyDeviceToHost, s));
+    LV_HIP(hipStreamSynchronize(s));
+    const uint32_t v = *w->herr;
+    if (!v) return LV_OK;
+    LV_HIP(hipMemsetAsync(w->err, 0, 4, s));  // ordered before the stream's next calls
+    if (violations) *violations = v;
+    std::string msg = "batch hint violated on the device:";
+    if (v & LV_HINT_ERR_MISALIGNED) msg += " an offset is not 16-byte aligned (LV_HINT_ALIGNED16);";
+    if (v & LV_HINT_ERR_NOT_UNIFORM) msg += " a length differs from max_len (LV_HINT_UNIFORM);";
+    if (v & LV_HINT_ERR_LONGER) msg += " a length exceeds max_len;";
+    if (v & LV_HINT_ERR_TOTAL) msg += " the lengths do not sum to total_bytes;";
+    msg += " the CRCs of the call(s) are undefined";
+    return set_err(LV_ERR_HINT, msg);
 }
 
 // Shift_{j plen} (j < 64) and Shift_{64 plen} as 65 GF(2) matrices of 32
@@ -306,6 +349,11 @@ int lv_device_counters(int device, uint64_t *out, size_t n) {
     return LV_OK;
 }
 
+int lv_crc32c_batch_check(void *stream, uint32_t *violations) {
+    g_err.clear();
+    return check_hints(static_cast<hipStream_t>(stream), violations);
+}
+
 int lv_device_init(void) {
     DevCtx *c = nullptr;
     return current_ctx(&c);
@@ -386,6 +434,9 @@ void pinned_free(uint8_t *p) {
 
 void count_h2d(uint64_t bytes) { counters().h2d += bytes; }
 void count_d2h(uint64_t bytes) { counters().d2h += bytes; }
+void count_alloc(int device) {
+    if (device >= 0 && device < 64) g_count[device].allocs++;
+}
 
 int host_scratch(HostPath *hp, int slot, size_t bytes, uint8_t **d) {
     (void)hp;  // the lock it holds is the device's host_m
@@ -503,8 +554,8 @@ int lv_crc32c_batch_host(const uint8_t *h_arena, size_t arena_bytes, const uint6
     const UniformPlan pl = aligned ? uniform_plan(c->cus, 0, 0, hint.max_len, n, -1) : UniformPlan{0, -1, 0};
     if (pl.applies() && pl.scratch <= sort_ws_bytes(n)) {
         // aligned uniform blocks (LV_HINT_ALIGNED16): the strided API's kernels
-        if (int rc = launch_uniform(*c, pl, c->d_arena, 0, d_off, hint.max_len, n, h_seed ? d_seed : nullptr, d_out,
-                                    flags, s, ws))
+        if (int rc = launch_uniform(*c, pl, c->d_arena, 0, d_off, d_len, nullptr, hint.max_len, n,
+                                    h_seed ? d_seed : nullptr, d_out, flags, s, ws))
             return rc;
     } else if (int rc = launch_binned(*c, ws, c->d_arena, d_off, d_len, h_seed ? d_seed : nullptr, d_out, n, flags, s,
                                       hint_needs_join(hint, n, static_cast<uint32_t>(c->cus)))) {

@@ -19,8 +19,12 @@
 // pageable memory, which the upload then staged again: two copies).  It is
 // done in chunks of kPackChunk bytes so the copy never holds a range's whole
 // payload; a chunk's pack is not overlapped with the previous chunk's upload.
+// The page-locked pack buffer is cached per device for the process's life
+// (round 5, ADVICE r04: pinning up to kPackChunk per call cost a
+// hipHostMalloc and an implicitly synchronising hipHostFree every time).
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -53,17 +57,19 @@ constexpr double kPackRatio = 1.5;
 constexpr uint64_t kPackSlack = 1ull << 20;
 constexpr uint64_t kPackChunk = 256ull << 20;
 
-// Page-locked pack buffer, freed on every return path.
+// Page-locked pack buffer of one device, grown on demand and kept (never
+// freed: a static destructor would run after the HIP runtime's teardown).
 struct Pinned {
+    std::mutex m;  // one packed range at a time per device
     uint8_t *p = nullptr;
     size_t cap = 0;
-    ~Pinned() { lvgpu_internal::pinned_free(p); }
-    int reserve(size_t bytes) {
+    int reserve(size_t bytes, int device) {
         if (cap >= bytes) return LV_OK;
         lvgpu_internal::pinned_free(p);
         p = nullptr;
         cap = 0;
         if (int rc = lvgpu_internal::pinned_alloc(bytes, &p)) return rc;
+        lvgpu_internal::count_alloc(device);
         cap = bytes;
         return LV_OK;
     }
@@ -73,9 +79,15 @@ struct Pinned {
 // (a lone longer buffer is its own sub-range and ships from the arena as
 // is), each packed into one reused page-locked buffer: host memory stays
 // bounded by the chunk however large the range's payload is.
+Pinned &pack_buffer(int device) {
+    static Pinned *bufs = new Pinned[64];  // lv_crc32c_batch_multi_devices checks 0 <= device < 64
+    return bufs[device];
+}
+
 int packed_ranges(const uint8_t *arena, const uint64_t *off, const uint32_t *len, const uint32_t *seed,
                   uint32_t *out, size_t cnt, uint32_t flags, int device) {
-    Pinned packed;
+    Pinned &packed = pack_buffer(device);
+    std::lock_guard<std::mutex> lk(packed.m);
     std::vector<uint64_t> poff;
     for (size_t lo = 0; lo < cnt;) {
         if (len[lo] >= kPackChunk) {
@@ -89,7 +101,7 @@ int packed_ranges(const uint8_t *arena, const uint64_t *off, const uint32_t *len
         size_t hi = lo;
         uint64_t bytes = 0;
         while (hi < cnt && len[hi] < kPackChunk && bytes + len[hi] <= kPackChunk) bytes += len[hi++];
-        if (int rc = packed.reserve(bytes ? bytes : 1)) return rc;  // non-null even for all-empty buffers
+        if (int rc = packed.reserve(bytes ? bytes : 1, device)) return rc;  // non-null even for all-empty buffers
         poff.resize(hi - lo);
         uint64_t pos = 0;
         for (size_t k = lo; k < hi; ++k) {
@@ -116,6 +128,8 @@ int lv_crc32c_batch_multi_devices(const uint8_t *h_arena, size_t arena_bytes, co
     if (n == 0) return LV_OK;
     if (!h_arena || !h_off || !h_len || !h_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null host pointer");
     if (!devices || ndev <= 0) return lvgpu_internal::set_error(LV_ERR_INVALID, "no devices");
+    for (int r = 0; r < ndev; ++r)
+        if (devices[r] < 0 || devices[r] >= 64) return lvgpu_internal::set_error(LV_ERR_INVALID, "device out of range");
     for (size_t i = 0; i < n; ++i)
         if (h_off[i] > arena_bytes || h_len[i] > arena_bytes - h_off[i])
             return lvgpu_internal::set_error(LV_ERR_INVALID, "buffer outside arena");

@@ -55,4 +55,6 @@ void pinned_free(uint8_t *p);
 // context.hip (current device).
 void count_h2d(uint64_t bytes);
 void count_d2h(uint64_t bytes);
+// ... and an allocation the host path made for `device` (any thread).
+void count_alloc(int device);
 }

@@ -54,6 +54,11 @@ struct StreamWs {
     std::mutex m;
     uint8_t *p = nullptr;
     size_t cap = 0;
+    // hint violations of this stream's calls (lv_crc32c_batch_check): a device
+    // word and a pinned host word to read it into, made once under em
+    std::mutex em;
+    uint32_t *err = nullptr;
+    uint32_t *herr = nullptr;
 };
 
 struct DevCtx {
@@ -130,6 +135,25 @@ int stream_ws(DevCtx &c, hipStream_t s, uint64_t n, uint8_t **out, std::unique_l
 int piece_mats(DevCtx &c, uint64_t plen, const uint32_t **out);
 int piece_tabs(DevCtx &c, uint64_t plen, const uint32_t **out);
 
+// The facts of a caller's lv_batch_hint, for the kernels' checks (err: the
+// stream's violation word, lv_crc32c_batch_check); null = nothing to check.
+struct HintCheck {
+    uint32_t *err;
+    uint64_t total;
+    uint32_t len;
+    uint32_t uniform;
+};
+inline void set_hint(lvk::Params &P, const HintCheck *hc, uint32_t dflt_len) {
+    P.herr = hc ? hc->err : nullptr;
+    P.htotal = hc ? hc->total : 0;
+    P.hlen = hc ? hc->len : dflt_len;
+    P.huni = hc ? hc->uniform : 0;
+}
+// The violation word of (device, stream), allocated and zeroed on first use.
+int stream_err(DevCtx &c, hipStream_t s, uint32_t **out);
+// Reads and clears the current device's violation word of stream s.
+int check_hints(hipStream_t s, uint32_t *violations);
+
 // ---- launchers ----
 // The length sort of the offsets API (sort.hip) for n > 1,024 buffers:
 // histogram + column scan + scatter.  Fills P.ent,
@@ -145,7 +169,8 @@ void launch_sort_scan(uint32_t *M, uint32_t wgs, uint32_t *ws, uint64_t *wgb, hi
 // join = false leaves out the join launch (the caller proved it empty with
 // hint_needs_join).
 int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join = true);
+                  const uint32_t *seed, uint32_t *out, uint64_t n, uint32_t flags, hipStream_t s, bool join = true,
+                  const HintCheck *hc = nullptr);
 // Whether a batch with these host-side facts needs the long-buffer join
 // (lv_crc32c_batch_device_hint; classes.hip).
 bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus);
@@ -167,9 +192,10 @@ struct UniformPlan {
 };
 UniformPlan uniform_plan(int cus, uint64_t base, uint64_t stride, uint32_t blen, uint64_t n, int gi);
 // Launches a plan that applies: block k at base + off[k] (off != null, the
-// offsets API with an aligned uniform hint) or base + k * stride.
+// offsets API with an aligned uniform hint; len = the device lengths, checked
+// against hc when it is not null) or base + k * stride.
 int launch_uniform(DevCtx &c, const UniformPlan &pl, const uint8_t *base, uint64_t stride, const uint64_t *off,
-                   uint32_t blen, uint64_t n, const uint32_t *seed, uint32_t *out, uint32_t flags, hipStream_t hs,
-                   uint8_t *scr);
+                   const uint32_t *len, const HintCheck *hc, uint32_t blen, uint64_t n, const uint32_t *seed,
+                   uint32_t *out, uint32_t flags, hipStream_t hs, uint8_t *scr);
 
 }  // namespace lvh

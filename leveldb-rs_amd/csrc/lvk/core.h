@@ -325,6 +325,13 @@ struct Params {
     // buffers can split is one sort key in index order, known on the host --
     // no sort runs; hident = 1 + its length class (0: the sort's ranges)
     uint32_t hident;
+    // The hint's facts, checked where a kernel reads what they describe
+    // (lv_crc32c_batch_check): violations are or-ed into *herr as
+    // LV_HINT_ERR_* bits.  herr null: no hint to check (hlen / htotal unused).
+    uint32_t *herr;
+    uint64_t htotal;  // the hint's total_bytes
+    uint32_t hlen;    // the hint's max_len
+    uint32_t huni;    // the hint's uniform word
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of

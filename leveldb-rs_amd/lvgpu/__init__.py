@@ -97,6 +97,8 @@ def lib() -> ctypes.CDLL:
     L.lv_crc32c_batch_strided.restype = ctypes.c_int
     L.lv_crc32c_batch_device_hint.restype = ctypes.c_int
     L.lv_crc32c_batch_device_hint.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, vp, sz, vp]
+    L.lv_crc32c_batch_check.restype = ctypes.c_int
+    L.lv_crc32c_batch_check.argtypes = [vp, vp]
     L.lv_crc32c_hint_needs_join.restype = ctypes.c_int
     L.lv_crc32c_hint_needs_join.argtypes = [vp, sz, u32]
     L.lv_crc32c_batch_strided.argtypes = [vp, u64, u32, sz, vp, vp, u32, vp]
@@ -283,6 +285,32 @@ def batch_hint(arena, off, length, hint: BatchHint, seed=None, out=None, masked=
         ctypes.byref(hint) if hint is not None else None, _dev_ptr(workspace, "workspace"),
         workspace.numel() if workspace is not None else 0, _stream_ptr(stream)))
     return out
+
+
+HINT_ERR_MISALIGNED = 0x1   # LV_HINT_ERR_MISALIGNED
+HINT_ERR_NOT_UNIFORM = 0x2  # LV_HINT_ERR_NOT_UNIFORM
+HINT_ERR_LONGER = 0x4       # LV_HINT_ERR_LONGER
+HINT_ERR_TOTAL = 0x8        # LV_HINT_ERR_TOTAL
+ERR_HINT = -4               # LV_ERR_HINT
+
+
+class HintViolation(LvError):
+    """A batch hint contradicted the device-side offsets/lengths
+    (lv_crc32c_batch_check); `violations` holds the LV_HINT_ERR_* bits."""
+
+    def __init__(self, msg, violations):
+        super().__init__(msg)
+        self.violations = violations
+
+
+def batch_check(stream=None) -> None:
+    """Wait for `stream` and raise HintViolation if a hinted batch call on it
+    (since the last check) was given facts its device arrays contradict."""
+    v = ctypes.c_uint32(0)
+    rc = lib().lv_crc32c_batch_check(_stream_ptr(stream), ctypes.byref(v))
+    if rc == ERR_HINT:
+        raise HintViolation(f"lvgpu error {rc}: {lib().lv_last_error().decode()}", int(v.value))
+    _check(rc)
 
 
 def batch_strided(base, stride: int, block_len: int, n: int, seed=None, out=None, masked=False, stream=None,

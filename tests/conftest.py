@@ -50,12 +50,25 @@ def kat_bytes(k):
     return bytes([k["fill"]["byte"]]) * k["fill"]["n"]
 
 
+def gpu_selected(config) -> bool:
+    """True when the run selects the gpu marker (`-m gpu`, `-m "gpu and ..."`):
+    a GPU run, where a missing device is a failure, not a skip."""
+    expr = (config.getoption("markexpr", default="") or "").replace("(", " ").replace(")", " ").split()
+    return any(tok == "gpu" and (i == 0 or expr[i - 1] != "not") for i, tok in enumerate(expr))
+
+
 @pytest.fixture(scope="session")
-def gpu():
-    """Skip unless a GPU is visible; on a GPU box, the HIP library must load."""
+def gpu(request):
+    """The GPU every `gpu` test runs on.  Under `-m gpu` a missing device
+    FAILS the test (a GPU run that executes nothing must not look green);
+    otherwise (a plain `pytest` on a CPU host) the test is skipped.  On a GPU
+    box the HIP library must load."""
     import torch
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        msg = "no GPU visible (torch.cuda.is_available() is False)"
+        if gpu_selected(request.config):
+            pytest.fail(msg + " in a run that selects -m gpu", pytrace=False)
+        pytest.skip(msg)
     import lvgpu
     lvgpu.device_init()
     return torch.device("cuda:0")

@@ -327,6 +327,11 @@ def test_batch_multi_ships_each_device_its_buffers(gpu):
         moved = lvgpu.device_counters(0)["h2d"] - before["h2d"]
         assert np.array_equal(got, want), devs
         assert moved <= payload + 16 * n, (devs, moved, payload)
+    # the page-locked pack buffer is cached per device: a repeat allocates nothing
+    before = lvgpu.device_counters(0)
+    got = lvgpu.batch_multi(arena, offs, lens, None, devices=[0, 0])
+    assert np.array_equal(got, want)
+    assert lvgpu.device_counters(0)["allocs"] == before["allocs"]
     # in index order and byte-packed: one span per range, no pack needed
     packed_offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
     want2 = np.zeros(n, dtype=np.uint32)
@@ -1071,3 +1076,122 @@ def test_hint_rejects_inconsistent_uniform(torch_dev):
     ln = torch.full((2,), 8, dtype=torch.int32, device=dev)
     with pytest.raises(lvgpu.LvError):
         lvgpu.batch_hint(a, o, ln, lvgpu.BatchHint(17, 8, 1))
+
+
+def test_hint_rejects_unknown_uniform_bits(torch_dev):
+    """`uniform` is 0, LV_HINT_UNIFORM or LV_HINT_UNIFORM |
+    LV_HINT_ALIGNED16; ALIGNED16 alone or unknown bits are LV_ERR_INVALID."""
+    torch, dev = torch_dev
+    a = torch.zeros(64, dtype=torch.uint8, device=dev)
+    o = torch.zeros(2, dtype=torch.int64, device=dev)
+    ln = torch.full((2,), 16, dtype=torch.int32, device=dev)
+    for bad in (lvgpu.HINT_ALIGNED16, 4, 5, 0x80000001):
+        with pytest.raises(lvgpu.LvError):
+            lvgpu.batch_hint(a, o, ln, lvgpu.BatchHint(32, 16, bad))
+
+
+def _hint_case(torch, dev, rng, n, L, aligned, seeded=False, slack=1 << 16):
+    """n buffers of L bytes at (16-B aligned if `aligned`) shuffled offsets in
+    an arena with `slack` bytes after the last one."""
+    Lp = -(-L // 16) * 16 + (0 if aligned else 3)
+    starts = np.arange(n, dtype=np.uint64) * Lp
+    offs = rng.permutation(starts).astype(np.uint64)
+    arena = rng.integers(0, 256, int(starts[-1]) + L + slack, dtype=np.uint8).tobytes()
+    a = torch.frombuffer(bytearray(arena), dtype=torch.uint8).to(dev)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if seeded else None
+    sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+    return arena, a, offs, seeds, sd
+
+
+# name: (n, L, aligned hint, how the device arrays contradict the hint, bits, kernel)
+HINT_LIE_CASES = {
+    "gather_misaligned_offset": (3000, 4096, True, "misalign", lvgpu.HINT_ERR_MISALIGNED,
+                                 "crc32c_blocks_kernel<16,gather>"),
+    "gather_understated_max_len": (3000, 4096, True, "longer", lvgpu.HINT_ERR_NOT_UNIFORM,
+                                   "crc32c_blocks_kernel<16,gather>"),
+    "gather_pieces_misaligned": (1024, 65536, True, "misalign", lvgpu.HINT_ERR_MISALIGNED,
+                                 "crc32c_blocks_kernel<16,pieces,fused,gather>"),
+    "gather_pieces_shorter": (16, 1 << 20, True, "shorter", lvgpu.HINT_ERR_NOT_UNIFORM,
+                              "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_kernel"),
+    "identity_understated": (5000, 4000, False, "longer", lvgpu.HINT_ERR_NOT_UNIFORM,
+                             "hint_len_kernel+crc32c_classes_kernel"),
+    "fused_uniform_shorter": (600, 1000, False, "shorter", lvgpu.HINT_ERR_NOT_UNIFORM, "crc32c_fused_small_kernel"),
+    "fused_understated_max": (600, 1000, False, "nonuniform_longer",
+                              lvgpu.HINT_ERR_LONGER | lvgpu.HINT_ERR_TOTAL, "crc32c_fused_small_kernel"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(HINT_LIE_CASES))
+def test_wrong_hint_is_reported(torch_dev, case):
+    """a hint the device arrays contradict is reported by
+    lv_crc32c_batch_check (LV_ERR_HINT with the violated facts), not answered
+    with silently wrong CRCs; the same arrays with an exact hint check clean,
+    and the record clears after a check."""
+    torch, dev = torch_dev
+    n, L, aligned, lie, bits, kern = HINT_LIE_CASES[case]
+    rng = np.random.default_rng(sum(map(ord, case)))
+    arena, a, offs, seeds, sd = _hint_case(torch, dev, rng, n, L, aligned)
+    lens = np.full(n, L, dtype=np.uint32)
+    hint = lvgpu.hint_for(lens, offs if aligned else None)
+    assert hint.uniform == (3 if aligned else 1)
+    lvgpu.batch_check()  # nothing recorded on this stream yet (or cleared)
+    # the exact hint: CRCs right, no violation
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = lvgpu.batch_hint(a, o, ln, hint, masked=True)
+    assert lvgpu.last_kernel().startswith(kern), lvgpu.last_kernel()
+    lvgpu.batch_check()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle_batch(arena, offs, lens, None, True))
+    # now the device arrays contradict the (unchanged) hint
+    k = int(rng.integers(0, n))
+    offs2, lens2 = offs.copy(), lens.copy()
+    if lie == "misalign":
+        offs2[k] += 8
+    elif lie == "longer":
+        lens2[k] = L + 5
+    elif lie == "shorter":
+        lens2[k] = L - 16
+    elif lie == "nonuniform_longer":  # a non-uniform hint whose max_len is understated
+        lens2[: n // 2] = L // 2
+        hint = lvgpu.hint_for(lens2)
+        lens2[k] = L + 1
+    o2 = torch.from_numpy(offs2.astype(np.int64)).to(dev)
+    ln2 = torch.from_numpy(lens2.view(np.int32)).to(dev)
+    lvgpu.batch_hint(a, o2, ln2, hint, masked=True)
+    with pytest.raises(lvgpu.HintViolation) as ei:
+        lvgpu.batch_check()
+    assert ei.value.violations == bits, (hex(ei.value.violations), lvgpu.last_kernel())
+    lvgpu.batch_check()  # the record was cleared
+    # a caller workspace takes the same checks
+    ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
+    lvgpu.batch_hint(a, o2, ln2, hint, masked=True, workspace=ws)
+    with pytest.raises(lvgpu.HintViolation):
+        lvgpu.batch_check()
+
+
+@pytest.mark.parametrize("n,L", [(64, 17 << 10), (200, 20 << 10), (1024, 64 << 10)])
+def test_aligned_hint_on_misaligned_arena_joins(torch_dev, n, L):
+    """with LV_HINT_ALIGNED16 but an arena pointer off
+    16-B alignment the library ignores the bit -- and its join decision must
+    not assume the aligned path ran.  64 x 17 KiB and 200 x 20 KiB split into
+    pieces that straddle workgroups on any CU count, so the fused walk needs
+    combine_long_kernel; CRCs bit-exact vs the oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(n * 31 + L)
+    arena, a, offs, _, _ = _hint_case(torch, dev, rng, n, L, True, slack=64)
+    lens = np.full(n, L, dtype=np.uint32)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    hint = lvgpu.hint_for(lens, offs)
+    assert hint.uniform == 3
+    a8 = torch.empty(a.numel() + 8, dtype=torch.uint8, device=dev)[8:]
+    a8.copy_(a)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    out = lvgpu.batch_hint(a8, o, ln, hint, seed=sd, masked=True)
+    kern = lvgpu.last_kernel()
+    lvgpu.batch_check()
+    assert "gather" not in kern, kern
+    if (n, L) != (1024, 64 << 10):
+        assert "combine_long_kernel" in kern, kern
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle_batch(arena, offs, lens, seeds, True))
