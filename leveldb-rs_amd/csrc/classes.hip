@@ -382,6 +382,7 @@ template <bool SEEDED>
 struct FusedUnits {
     static constexpr uint32_t kFlush = 16;
     static constexpr bool kAlMid = true;
+    static constexpr bool kPlainMerge = false;
     static constexpr bool kOneRound = LVK_FUSED_ONE_ROUND;  // sorted_stream: a one-round wave loads all batches at once
     // wait-count modes 1 / 2 (walk.h) measured 0.7-1.3 / 0.5-0.9 us slower on
     // the few-long-buffer calls (profiles/r04/new_ab/, mode2_ab/): masked

@@ -174,6 +174,13 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
 // Whether a batch with these host-side facts needs the long-buffer join
 // (lv_crc32c_batch_device_hint; classes.hip).
 bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus);
+// The one-launch device WAL scan (wal_pipe.hip): workspace bytes, whether a
+// log of `bytes` takes it on this device, and the launch (a memset of its
+// count granules, then wal_pipe_kernel).
+size_t wal_pipe_ws_bytes(uint64_t bytes, uint64_t cap);
+bool wal_pipe_applies(const DevCtx &c, uint64_t bytes);
+int launch_wal_pipe(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
+                    uint32_t *d_info, uint64_t cap, uint64_t *d_count, uint8_t *ws, hipStream_t s);
 // The persistent class kernel over a sorted list (classes.hip).
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s);
 // One group-size kernel over a batch, offsets or strided (blocks.hip).

@@ -46,6 +46,7 @@
     defined(LVK_HASH_LDS_ALL) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
+    defined(LVK_WAL_LOCAL) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -146,6 +147,9 @@
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8
+#endif
+#ifndef LVK_WAL_LOCAL  // WAL scan: one persistent launch, each workgroup frames, sorts and walks its own blocks
+#define LVK_WAL_LOCAL 1
 #endif
 #ifndef LVK_WAL_UNSORT  // WAL scan: CRCs stored by sorted position, then written in log order (wal_unsort)
 #define LVK_WAL_UNSORT 1

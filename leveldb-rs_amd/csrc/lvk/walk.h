@@ -305,7 +305,11 @@ __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint3
 // (In the depth-2 form W2(W1(h0)^h1) ^ (W1(h2)^h3).)  `rot` (wave-uniform)
 // is false when every group of the wave ends at lane 15 (e.g. aligned table
 // blocks): no early lanes, no rotation.
-template <uint32_t NU>
+// PLAIN: W1 / W2 from the plain combine tables 4 / 5 (Shift_256 / Shift_512)
+// instead of region B's Latin copies -- for a kernel that keeps region B's
+// 64 KiB of LDS for itself (wal_pipe_kernel; round 1 measured the plain
+// merge neutral on the class kernel).
+template <uint32_t NU, bool PLAIN = false>
 __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a3p, const Lut &L, const RGeo &q,
                                              uint32_t gl, uint32_t lane, bool rot) {
     const AGeo g = al_geo(q);
@@ -316,6 +320,11 @@ __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a
 #pragma unroll
         for (uint32_t i = 0; i < NU; ++i) X ^= A[i];
         return X;
+    } else if constexpr (PLAIN) {
+        static_assert(NU == 4, "plain merge: four rows per batch");
+        const uint32_t x01 = comb_shift(early ? a3p : A[0], 4) ^ (early ? A[0] : A[1]);
+        const uint32_t x23 = comb_shift(early ? A[1] : A[2], 4) ^ (early ? A[2] : A[3]);
+        X = comb_shift(x01, 5) ^ x23;
     } else if constexpr (NU == 4) {
         const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
         const uint32_t x23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
@@ -395,6 +404,7 @@ template <bool SEEDED>
 struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
+    static constexpr bool kPlainMerge = false;  // merge_al: region B's Latin tables
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
     static constexpr uint32_t kExact = LVK_WALK_EXACT;  // sorted_stream: wait-count mode (below)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
@@ -522,7 +532,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             if (nbw > 1u) fold_j(v1, 1);
             if (nbw > 2u) fold_j(v2, 2);
             if (nbw > 3u) fold_j(v3, 3);
-            uint32_t X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
+            uint32_t X = merge_al<NU, Src::kPlainMerge>(A, a3p, L, q, gl, lane, rot);
             X = finish_raw(q, X, tail, gl, L);
             if (gl == 0) src.stage(P, wave, grp, q, X, tr);
             __builtin_amdgcn_wave_barrier();
@@ -574,7 +584,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         }
         uint32_t X;
         if constexpr (AL)
-            X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
+            X = merge_al<NU, Src::kPlainMerge>(A, a3p, L, q, gl, lane, rot);
         else
             X = merge_group<G, W1K, W2K>(A, L);
         X = finish_raw(q, X, tail, gl, L);

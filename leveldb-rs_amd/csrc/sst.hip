@@ -45,6 +45,7 @@ struct TableUnits {
     // crc_out 32 slots of four words
     static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
+    static constexpr bool kPlainMerge = false;
     static constexpr bool kOneRound = false;
     // Wait-count mode (walk.h sorted_stream): verify runs mode 2 (every load
     // unconditional within its path: 0.703 -> 0.723 against the session-start

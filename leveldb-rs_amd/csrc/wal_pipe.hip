@@ -1,0 +1,613 @@
+// The device WAL scan in ONE persistent launch (round 5; lv_wal_scan_device,
+// the reader side of SURVEY 8f row 1: log_reader.rs:271-364).
+//
+// Round 4's scan ran five launches: the header chains of every 32 KiB block
+// (wal_hist, ~22 us: dependent HBM misses, most of the chip idle), a column
+// scan, a scatter into one global length sort, the class kernel (174 us) and
+// an unsort.  The chains were ~17 % of the call and ran before any CRC.
+//
+// Here workgroup w owns a contiguous range of blocks (~4 MiB of a 1 GiB log
+// on 256 CUs) and does everything for it:
+//   1. every thread reads the first header of one block (one round trip,
+//      under the table staging): each block's first record is known at once
+//      -- 59 % of the bench log's bytes (a FIRST / MIDDLE fragment fills its
+//      block);
+//   2. the first records of > 2 KiB units are counting-sorted in LDS (longest
+//      first) and 14-16 waves start checksumming them ("phase A") with the
+//      class kernel's G = 16 aligned-row walk;
+//   3. meanwhile one or two framer waves walk the rest of every block's chain
+//      (as read_physical_record frames it, log_reader.rs:271-331), caching
+//      headers and counting sort keys -- hidden under phase A;
+//   4. the last framer wave publishes the workgroup's record count (an 8-B
+//      {tag, count} granule, agent-scope sc1 store), reads every other
+//      workgroup's (a bounded relaxed poll: the counts of the workgroups before
+//      it give its base in the log-order output, all of them the total for
+//      the capacity check), writes hdr_off / info of its records in log order
+//      and counting-sorts the rest of its records into ent[base, ...) by
+//      (class, batches) -- the same key as the global sort -- then raises an
+//      LDS flag;
+//   5. the waves walk that local list (classes 2, 1, 0 with G = 16, 4, 1),
+//      CRCs staged in LDS by record index, and the workgroup writes its CRCs
+//      in log order at the end.
+// No cross-workgroup data moves but the 8-B counts (one grid-wide granule
+// array, zeroed by a memset before the launch).  A per-workgroup sort of
+// ~700 records keeps rounds as uniform as the global sort did (simulated:
+// 0.99 of the batch-count efficiency of the global sort).
+// LDS: the image without region B (the aligned walk's merge reads the plain
+// combine tables 4 / 5 instead, merge_al<PLAIN>), so region B's 64 KiB hold
+// the workgroup's block tables, key histograms and the CRC staging.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../include/lvgpu/wal.h"
+#include "lvh.h"
+#include "lvk/walk.h"
+
+namespace lvk {
+
+constexpr uint32_t kPipeBlockSize = 32768;  // log_format.rs:63
+constexpr uint32_t kPipeHeader = 7;         // log_format.rs:66
+constexpr uint32_t kPipeMaxBlocks = 1024;   // blocks per workgroup (the LDS block tables)
+constexpr uint32_t kPipeCache = 64;         // headers per block in the global header cache
+constexpr uint32_t kPipeAMin = 2049;        // phase A: first records of class-2 units (> 2 KiB)
+
+// Region B carve-out (word offsets into g_lds).
+constexpr uint32_t kPB = kRegionB / 4;
+constexpr uint32_t kPCnt = kPB;                          // records per block
+constexpr uint32_t kPPre = kPCnt + kPipeMaxBlocks;       // exclusive prefix of kPCnt
+constexpr uint32_t kPRecA = kPPre + kPipeMaxBlocks;      // first record: len | type << 16 | status << 24, ~0 none
+constexpr uint32_t kPCrcA = kPRecA + kPipeMaxBlocks;     // phase-A CRCs by block
+constexpr uint32_t kPSortA = kPCrcA + kPipeMaxBlocks;    // phase-A list: block indices, longest first
+constexpr uint32_t kPHist = kPSortA + kPipeMaxBlocks;    // phase-B key counts, then cursors
+constexpr uint32_t kPHistA = kPHist + kKeys;             // phase-A bucket counts, then cursors
+constexpr uint32_t kPCtl = kPHistA + 64;                 // control words (below)
+constexpr uint32_t kPStage = kPCtl + 64;                 // CRCs by local record index
+constexpr uint32_t kPStageN = kPB + 16384 - kPStage;     // records whose CRC is staged (10,880)
+enum : uint32_t {
+    kCPoolA,    // round counters of the four lists
+    kCPool16,
+    kCPool4,
+    kCPool1,
+    kCNA,       // phase-A entries
+    kCN16,      // phase-B entries per group size
+    kCN4,
+    kCN1,
+    kCReady,    // phase-B list written (ent[], hdr_off, info)
+    kCAbort,    // write nothing: the records exceed cap, or a count never arrived
+    kCFramed,   // framer waves done
+    kCBaseLo,   // this workgroup's first record in log order
+    kCBaseHi,
+    kCCount,    // this workgroup's records
+};
+static_assert(kPStage + kPStageN == kPB + 16384, "carve-out fits region B");
+
+struct WalPipe {
+    const uint8_t *log;
+    uint64_t size, nblocks;
+    uint64_t *gran;  // one {tag 1 | count} granule per workgroup, zeroed before the launch
+    uint64_t *hc;    // header cache: kPipeCache per block (pos | len << 16 | type << 32)
+    uint4 *ent;      // phase-B sorted entries {unit addr lo, hi, unit length, record index}
+    uint64_t *hdr_off;
+    uint32_t *crc, *info;
+    uint64_t *count;
+    uint64_t cap;
+    uint32_t *err;  // set when a workgroup's count never arrived (bounded poll)
+};
+
+__device__ __forceinline__ uint32_t &pctl(uint32_t k) { return g_lds[kPCtl + k]; }
+
+// Phase A: the sorted first records, geometry from LDS (no memory load).
+struct PipeFirst {
+    static constexpr uint32_t kFlush = 16;
+    static constexpr bool kAlMid = true;
+    static constexpr bool kOneRound = false;
+    static constexpr uint32_t kExact = LVK_WALK_EXACT;
+    static constexpr bool kPlainMerge = true;  // region B is the carve-out
+    uint64_t blk0;  // address of the workgroup's first block
+    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
+        const bool valid = e < P.n;
+        const uint32_t i = static_cast<uint32_t>(valid ? e : P.n - 1);
+        const uint32_t bl = g_lds[kPSortA + i];
+        const uint32_t r = g_lds[kPRecA + bl];
+        RGeo q;
+        q.a = blk0 + static_cast<uint64_t>(bl) * kPipeBlockSize + 6u;  // [type || payload], log_reader.rs:336
+        q.len = (r & 0xffffu) + 1u;
+        q.seed = 0;
+        q.bid = valid ? bl : 0xffffffffu;
+        q.aux = 0;
+        return q;
+    }
+    __device__ __forceinline__ uint2 trailer(const RGeo &, uint32_t) const { return make_uint2(0, 0); }
+    __device__ __forceinline__ void stage(const Params &, uint32_t, uint32_t, const RGeo &q, uint32_t X,
+                                          uint2) const {
+        if (q.bid != 0xffffffffu) g_lds[kPCrcA + q.bid] = ~X;
+    }
+    __device__ __forceinline__ void flush(const Params &, uint32_t, uint32_t, uint32_t) const {}
+};
+
+// Phase B: the workgroup's sorted rest, entries in ent[] (written by its own
+// builder wave: same CU, after an LDS flag).  CRCs by record index: the LDS
+// staging, or (a workgroup with more records) straight to the output in the
+// flush, every kFlush rounds like the class kernel's stores.
+struct PipeRest {
+    static constexpr uint32_t kFlush = 16;
+    static constexpr bool kAlMid = true;
+    static constexpr bool kOneRound = false;
+    static constexpr uint32_t kExact = LVK_WALK_EXACT;
+    static constexpr bool kPlainMerge = true;
+    const uint4 *ent;
+    uint64_t logbase;
+    uint32_t *crc;  // d_crc + the workgroup's base
+    __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
+        const bool valid = e < P.n;
+        const uint64_t ec = valid ? e : P.n - 1;
+        const uint4 v = ent[ec];
+        RGeo q;
+        q.a = v.z ? logbase + ((static_cast<uint64_t>(v.y) << 32) | v.x) : logbase;
+        q.len = v.z;
+        q.seed = 0;
+        q.bid = valid ? v.w : 0xffffffffu;
+        q.aux = 0;
+        return q;
+    }
+    __device__ __forceinline__ uint2 trailer(const RGeo &, uint32_t) const { return make_uint2(0, 0); }
+    __device__ __forceinline__ void stage(const Params &, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
+                                          uint2) const {
+        g_oidx[wave][slot] = q.bid;
+        g_ocrc[wave][slot] = ~X;
+    }
+    __device__ __forceinline__ void flush(const Params &, uint32_t wave, uint32_t lane, uint32_t nslots) const {
+        const uint32_t li = g_oidx[wave][lane], c = g_ocrc[wave][lane];
+        if (lane >= nslots || li == 0xffffffffu) return;
+        if (li < kPStageN)
+            g_lds[kPStage + li] = c;
+        else
+            crc[li] = c;
+    }
+};
+
+// Region A and the combine tables of the G = 16 image (region B stays the
+// carve-out): every thread issues its loads before its first LDS store.
+__device__ __forceinline__ void stage_tables_ab(const uint4 *__restrict__ image) {
+    constexpr int kA = kRegionB / 16, kC0 = kComb / 16, kC = (kImageWords * 4 - kComb) / 16;  // uint4 counts
+    constexpr int kN = kA + kC;
+    constexpr int kPer = (kN + kThreads - 1) / kThreads;
+    uint4 *l4 = reinterpret_cast<uint4 *>(g_lds);
+    g_u32x4 *src = reinterpret_cast<g_u32x4 *>(reinterpret_cast<uint64_t>(image));
+    u32x4 r[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = threadIdx.x + k * kThreads;
+        const int s = i < kA ? i : kC0 + (i - kA);
+        if (i < kN) r[k] = src[s];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = threadIdx.x + k * kThreads;
+        const int s = i < kA ? i : kC0 + (i - kA);
+        if (i < kN) l4[s] = to_uint4(r[k]);
+    }
+}
+
+// A record header at in-block position pos: status and unit length
+// (log_reader.rs:305-331).
+__device__ __forceinline__ uint32_t pipe_status(uint32_t len, uint32_t type, uint32_t blen, uint32_t pos) {
+    if (kPipeHeader + len > blen - pos) return LV_WAL_REC_BAD_LENGTH;  // log_reader.rs:312-324
+    if (type == 0 && len == 0) return LV_WAL_REC_ZERO;                 // log_reader.rs:326-331
+    return LV_WAL_REC_OK;
+}
+
+// Sort-key walk order: class 2 (longest first), class 1, class 0, then the
+// (empty: units <= 32,762 B) class 3.
+__device__ __forceinline__ uint32_t pipe_order_key(uint32_t o) {
+    return o < 64u ? 128u + o : o < 128u ? o : o < 192u ? o - 128u : o;
+}
+
+__global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uint4 *__restrict__ image) {
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t grid = gridDim.x, w = blockIdx.x;
+    const uint64_t lo = a.nblocks * w / grid, hi = a.nblocks * (w + 1) / grid;
+    const uint32_t nblk = static_cast<uint32_t>(hi - lo);  // <= kPipeMaxBlocks (host)
+    const uint64_t blk0 = reinterpret_cast<uint64_t>(a.log) + lo * kPipeBlockSize;
+    const uint8_t *const log = a.log;
+
+    // ---- 1. the first header of every block (under the table staging) ----
+    uint32_t w1 = 0, blen1 = 0;
+    if (t < nblk) {
+        const uint64_t start = (lo + t) * kPipeBlockSize;
+        blen1 = static_cast<uint32_t>(a.size - start < kPipeBlockSize ? a.size - start : kPipeBlockSize);
+        // header bytes 4..6 (length, type) in the aligned dword at +4 (an
+        // aligned dword never crosses a page: its 4th byte may lie past a
+        // 7-byte last block)
+        if (blen1 >= kPipeHeader) w1 = *reinterpret_cast<const uint32_t *>(log + start + 4);
+    }
+    for (uint32_t k = t; k < kKeys + 64 + 64; k += kThreads) g_lds[kPHist + k] = 0;  // hist, histA, ctl
+    stage_tables_ab(image);
+    __syncthreads();
+    if (t < nblk) {
+        uint32_t r = 0xffffffffu;
+        if (blen1 >= kPipeHeader) {
+            const uint32_t len = w1 & 0xffffu, type = (w1 >> 16) & 0xffu;
+            const uint32_t st = pipe_status(len, type, blen1, 0);
+            r = len | (type << 16) | (st << 24);
+            const uint32_t ulen = st == LV_WAL_REC_OK ? len + 1u : 0u;
+            if (ulen >= kPipeAMin)
+                atomicAdd(&g_lds[kPHistA + (sort_key(ulen) & 63u)], 1u);
+            else
+                atomicAdd(&g_lds[kPHist + sort_key(ulen)], 1u);
+        }
+        g_lds[kPRecA + t] = r;
+    }
+    __syncthreads();
+    if (wave == 0) {  // bucket starts of phase A (64 buckets, longest first)
+        const uint32_t c = g_lds[kPHistA + lane];
+        uint32_t inc = c;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(inc, d);
+            if (lane >= d) inc += x;
+        }
+        g_lds[kPHistA + lane] = inc - c;
+        if (lane == 63) pctl(kCNA) = inc;
+    }
+    __syncthreads();
+    if (t < nblk) {
+        const uint32_t r = g_lds[kPRecA + t];
+        if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK && (r & 0xffffu) + 1u >= kPipeAMin) {
+            const uint32_t slot = atomicAdd(&g_lds[kPHistA + (sort_key((r & 0xffffu) + 1u) & 63u)], 1u);
+            g_lds[kPSortA + slot] = t;
+        }
+    }
+    __syncthreads();
+    // (values read from LDS are wave-uniform: readfirstlane keeps them in
+    // scalar registers, where the walk's list bounds and pointers belong)
+    auto uni = [](uint32_t v) { return __builtin_amdgcn_readfirstlane(v); };
+    const uint32_t nA = uni(pctl(kCNA));
+    const Lut L = make_lut(lane);
+    auto pool = [&](uint32_t word) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&g_lds[kPCtl + word], 1u);
+        return static_cast<uint64_t>(__shfl(k, 0));
+    };
+    auto nextA = [&]() { return pool(kCPoolA); };
+    auto walk_first = [&]() {
+        Params P{};
+        P.n = nA;
+        sorted_stream<16>(P, PipeFirst{blk0}, lane, L, nextA(), nextA);
+    };
+
+    // ---- 2. framer waves: the rest of every chain; the others: phase A ----
+    const uint32_t nframers = nblk > 64u ? 2u : 1u;
+    if (wave < nframers) {
+        const uint32_t fl = wave * 64u + lane;
+        for (uint32_t b0 = 0; b0 < nblk; b0 += 64u * nframers) {  // wave-uniform
+            const uint32_t bl = b0 + fl;
+            const uint64_t start = (lo + bl) * kPipeBlockSize;
+            uint32_t blen = 0, pos = 0, cnt = 0;
+            bool active = false;
+            if (bl < nblk) {
+                blen = static_cast<uint32_t>(a.size - start < kPipeBlockSize ? a.size - start : kPipeBlockSize);
+                const uint32_t r = g_lds[kPRecA + bl];
+                cnt = r == 0xffffffffu ? 0u : 1u;
+                if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK) {
+                    pos = kPipeHeader + (r & 0xffffu);
+                    active = blen - pos >= kPipeHeader;
+                }
+            }
+            // the header's length / type: the two aligned dwords around
+            // bytes pos + 4 .. pos + 6 (the second clamped to the block's last)
+            const uint8_t *const blk = log + start;
+            const uint32_t lastd = blen ? (blen - 1u) & ~3u : 0u;
+            uint32_t wlo = 0, whi = 0, wsh = 0;
+            auto issue = [&](uint32_t p, bool on) {
+                const uint32_t pr = p + 4u, ar = pr & ~3u;
+                wsh = pr & 3u;
+                if (on) {
+                    wlo = *reinterpret_cast<const uint32_t *>(blk + ar);
+                    whi = *reinterpret_cast<const uint32_t *>(blk + (ar + 4u < lastd ? ar + 4u : lastd));
+                }
+            };
+            issue(pos, active);
+            while (__any(active)) {  // wave-uniform: the longest chain of the wave
+                const uint32_t hw = __builtin_amdgcn_alignbyte(whi, wlo, wsh);  // bytes pos + 4 .. pos + 7
+                const uint32_t len = hw & 0xffffu, type = (hw >> 16) & 0xffu;
+                const bool ok = kPipeHeader + len <= blen - pos && (type | len) != 0u;
+                const uint32_t npos = pos + kPipeHeader + len;
+                const bool nact = active && ok && blen - npos >= kPipeHeader;
+                issue(npos, nact);  // the next header's loads before this record's store
+                if (active) {
+                    if (cnt < kPipeCache)
+                        a.hc[(lo + bl) * kPipeCache + cnt] =
+                            pos | (static_cast<uint64_t>(len) << 16) | (static_cast<uint64_t>(type) << 32);
+                    __hip_atomic_fetch_add(&g_lds[kPHist + sort_key(ok ? len + 1u : 0u)], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ++cnt;
+                }
+                pos = npos;
+                active = nact;
+            }
+            if (bl < nblk) g_lds[kPCnt + bl] = cnt;
+        }
+        // the header cache and this wave's LDS writes are complete before the
+        // count that elects the builder
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        uint32_t done = 0;
+        if (lane == 0)
+            done = __hip_atomic_fetch_add(&pctl(kCFramed), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        done = __shfl(done, 0);
+        if (done + 1u == nframers) {
+            // ---- 3. the builder: counts, base, hdr_off / info, the phase-B list ----
+            uint32_t run = 0;
+            for (uint32_t b0 = 0; b0 < nblk; b0 += 64u) {  // exclusive prefix of the block counts
+                const uint32_t bl = b0 + lane;
+                const uint32_t c = bl < nblk ? g_lds[kPCnt + bl] : 0u;
+                uint32_t inc = c;
+#pragma unroll
+                for (uint32_t d = 1; d < 64; d <<= 1) {
+                    const uint32_t x = __shfl_up(inc, d);
+                    if (lane >= d) inc += x;
+                }
+                if (bl < nblk) g_lds[kPPre + bl] = run + inc - c;
+                run += __shfl(inc, 63);
+            }
+            const uint32_t count_w = run;
+            // (global address space: an agent-scope sc1 store / load, never flat)
+            typedef __attribute__((address_space(1))) uint64_t gu64;
+            gu64 *const gran = reinterpret_cast<gu64 *>(reinterpret_cast<uint64_t>(a.gran));
+            if (lane == 0) __hip_atomic_store(gran + w, (1ull << 32) | count_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // every workgroup's count (bounded poll: ~0.2 s of s_memrealtime at 100 MHz)
+            uint64_t base = 0, total = 0;
+            bool timeout = false;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t j0 = 0; j0 < grid; j0 += 64u) {  // wave-uniform
+                const uint32_t j = j0 + lane;
+                uint64_t v = 0;
+                for (;;) {
+                    if (j < grid) v = __hip_atomic_load(gran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(j >= grid || (v >> 32) == 1u)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+                        timeout = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                const uint64_t c = j < grid ? (v & 0xffffffffull) : 0u;
+                base += j < w ? c : 0u;
+                total += c;
+            }
+#pragma unroll
+            for (int k = 32; k >= 1; k >>= 1) {
+                base += __shfl_xor(base, k);
+                total += __shfl_xor(total, k);
+            }
+            const bool abort = timeout || total > a.cap;
+            if (w == 0 && lane == 0) *a.count = timeout ? ~0ull : total;
+            if (timeout && lane == 0) atomicOr(a.err, 1u);
+            if (!abort) {
+                // phase-B key starts in walk order (class 2, 1, 0)
+                uint32_t c4[4], inc4 = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    c4[i] = g_lds[kPHist + pipe_order_key(4u * lane + i)];
+                    inc4 += c4[i];
+                }
+                uint32_t inc = inc4;
+#pragma unroll
+                for (uint32_t d = 1; d < 64; d <<= 1) {
+                    const uint32_t x = __shfl_up(inc, d);
+                    if (lane >= d) inc += x;
+                }
+                uint32_t s = inc - inc4;
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    g_lds[kPHist + pipe_order_key(4u * lane + i)] = s;
+                    s += c4[i];
+                }
+                // lanes 0-15 hold class 2, 16-31 class 1, 32-47 class 0
+                const uint32_t e16 = __shfl(inc, 15), e4 = __shfl(inc, 31), e1 = __shfl(inc, 47);
+                const uint32_t tot = __shfl(inc, 63);
+                (void)tot;
+                if (lane == 0) {
+                    pctl(kCN16) = e16;  // (class 3 is empty: a unit is at most 32,762 B)
+                    pctl(kCN4) = e4 - e16;
+                    pctl(kCN1) = e1 - e4;
+                    pctl(kCBaseLo) = static_cast<uint32_t>(base);
+                    pctl(kCBaseHi) = static_cast<uint32_t>(base >> 32);
+                    pctl(kCCount) = count_w;
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint64_t *const hdr = a.hdr_off + base;
+                uint32_t *const info = a.info + base;
+                uint4 *const ent = a.ent + base;
+                const uint64_t lb = lo * kPipeBlockSize;
+                // records in log order: record q is record k = q - pre[bl] of
+                // the last block bl with pre[bl] <= q
+                for (uint32_t q0 = 0; q0 < count_w; q0 += 64u) {  // wave-uniform
+                    const uint32_t q = q0 + lane;
+                    uint32_t bl = 0;
+                    for (uint32_t step = kPipeMaxBlocks / 2; step >= 1; step >>= 1)
+                        if (bl + step < nblk && g_lds[kPPre + bl + step] <= q) bl += step;
+                    const uint32_t k = q - g_lds[kPPre + bl];
+                    const bool rec = q < count_w && k < kPipeCache;
+                    const uint64_t start = lb + static_cast<uint64_t>(bl) * kPipeBlockSize;
+                    const uint32_t blen =
+                        static_cast<uint32_t>(a.size - start < kPipeBlockSize ? a.size - start : kPipeBlockSize);
+                    uint32_t pos = 0, len = 0, type = 0;
+                    if (rec) {
+                        if (k == 0) {
+                            const uint32_t r = g_lds[kPRecA + bl];
+                            len = r & 0xffffu;
+                            type = (r >> 16) & 0xffu;
+                        } else {
+                            const uint64_t h = a.hc[(lo + bl) * kPipeCache + k];
+                            pos = static_cast<uint32_t>(h) & 0xffffu;
+                            len = static_cast<uint32_t>(h >> 16) & 0xffffu;
+                            type = static_cast<uint32_t>(h >> 32) & 0xffu;
+                        }
+                    }
+                    const uint32_t st = pipe_status(len, type, blen, pos);
+                    const uint32_t ulen = st == LV_WAL_REC_OK ? len + 1u : 0u;
+                    const bool inb = rec && !(k == 0 && ulen >= kPipeAMin);  // phase A walks the others
+                    const uint32_t slot = wave_claim(&g_lds[kPHist], sort_key(ulen), inb, lane);
+                    if (rec) {
+                        hdr[q] = start + pos;
+                        info[q] = type | (st << 8) | (len << 16);
+                    }
+                    if (inb) {
+                        const uint64_t ua = start + pos + 6u;  // [type || payload], log_reader.rs:336
+                        ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), ulen, q);
+                    }
+                }
+                // blocks of more than kPipeCache records walk on from the last
+                // cached header (one lane per block; a 32 KiB block holds more
+                // than 64 records only when they are a few bytes long)
+                for (uint32_t b0 = 0; b0 < nblk; b0 += 64u) {  // wave-uniform
+                    const uint32_t bl = b0 + lane;
+                    const uint32_t c = bl < nblk ? g_lds[kPCnt + bl] : 0u;
+                    bool active = c > kPipeCache;
+                    const uint64_t start = lb + static_cast<uint64_t>(bl) * kPipeBlockSize;
+                    const uint32_t blen =
+                        active ? static_cast<uint32_t>(a.size - start < kPipeBlockSize ? a.size - start : kPipeBlockSize)
+                               : 0u;
+                    uint32_t pos = 0, q = 0;
+                    if (active) {
+                        const uint64_t h = a.hc[(lo + bl) * kPipeCache + kPipeCache - 1];
+                        pos = (static_cast<uint32_t>(h) & 0xffffu) + kPipeHeader + (static_cast<uint32_t>(h >> 16) & 0xffffu);
+                        q = g_lds[kPPre + bl] + kPipeCache;
+                    }
+                    while (__any(active)) {
+                        uint32_t len = 0, type = 0, st = 0;
+                        if (active) {
+                            const uint64_t hb = start + pos + 4u;
+                            uint32_t b4 = log[hb], b5 = log[hb + 1], b6 = log[hb + 2];
+                            len = b4 | (b5 << 8);
+                            type = b6;
+                            st = pipe_status(len, type, blen, pos);
+                        }
+                        const uint32_t ulen = st == LV_WAL_REC_OK ? len + 1u : 0u;
+                        const uint32_t slot = wave_claim(&g_lds[kPHist], sort_key(ulen), active, lane);
+                        if (active) {
+                            hdr[q] = start + pos;
+                            info[q] = type | (st << 8) | (len << 16);
+                            const uint64_t ua = start + pos + 6u;
+                            ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), ulen, q);
+                            ++q;
+                            pos += kPipeHeader + len;
+                            active = st == LV_WAL_REC_OK && blen - pos >= kPipeHeader;
+                        }
+                    }
+                }
+            } else if (lane == 0) {
+                pctl(kCAbort) = 1u;
+                pctl(kCN16) = 0u;
+                pctl(kCN4) = 0u;
+                pctl(kCN1) = 0u;
+            }
+            // the entries are in memory before the flag (same CU: the walkers'
+            // loads of them follow the flag)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&pctl(kCReady), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+
+    // ---- 4. every wave: phase A, then (after the flag) the phase-B lists ----
+    walk_first();
+    while (__hip_atomic_load(&pctl(kCReady), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(16);
+    const bool abort = uni(pctl(kCAbort)) != 0u;
+    const uint64_t base = (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo));
+    const uint32_t n16 = uni(pctl(kCN16)), n4 = uni(pctl(kCN4)), n1 = uni(pctl(kCN1));
+    if (!abort) {
+        const PipeRest r16{a.ent + base, reinterpret_cast<uint64_t>(log), a.crc + base};
+        const PipeRest r4{a.ent + base + n16, reinterpret_cast<uint64_t>(log), a.crc + base};
+        const PipeRest r1{a.ent + base + n16 + n4, reinterpret_cast<uint64_t>(log), a.crc + base};
+        Params P{};
+        auto next16 = [&]() { return pool(kCPool16); };
+        auto next4 = [&]() { return pool(kCPool4); };
+        auto next1 = [&]() { return pool(kCPool1); };
+        P.n = n16;
+        sorted_stream<16>(P, r16, lane, L, next16(), next16);
+        P.n = n4;
+        sorted_stream<4>(P, r4, lane, L, next4(), next4);
+        P.n = n1;
+        sorted_stream<1>(P, r1, lane, L, next1(), next1);
+    }
+    __syncthreads();
+    if (abort) return;
+    // ---- 5. the workgroup's CRCs in log order ----
+    const uint32_t count_w = uni(pctl(kCCount));
+    uint32_t *const crc = a.crc + base;
+    for (uint32_t bl = t; bl < nblk; bl += kThreads) {  // phase A's CRCs to their record index
+        const uint32_t r = g_lds[kPRecA + bl];
+        if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK && (r & 0xffffu) + 1u >= kPipeAMin) {
+            const uint32_t li = g_lds[kPPre + bl];
+            if (li < kPStageN)
+                g_lds[kPStage + li] = g_lds[kPCrcA + bl];
+            else
+                crc[li] = g_lds[kPCrcA + bl];
+        }
+    }
+    __syncthreads();
+    const uint32_t ns = count_w < kPStageN ? count_w : kPStageN;
+    for (uint32_t i = t; i < ns; i += kThreads) crc[i] = g_lds[kPStage + i];
+}
+
+}  // namespace lvk
+
+namespace lvh {
+
+// The one-launch scan's workspace: the count granules (zeroed before every
+// launch), the header cache, the phase-B entries.
+struct PipeWs {
+    size_t gran, hc, ent, err, total;
+};
+
+static PipeWs pipe_ws_layout(uint64_t nblocks, uint64_t cap) {
+    PipeWs w;
+    w.gran = 0;
+    w.err = al16(1024 * sizeof(uint64_t));
+    w.hc = w.err + 16;
+    w.ent = w.hc + al16(nblocks * lvk::kPipeCache * sizeof(uint64_t));
+    w.total = w.ent + al16(cap * sizeof(uint4));
+    return w;
+}
+
+size_t wal_pipe_ws_bytes(uint64_t bytes, uint64_t cap) {
+    const uint64_t nblocks = (bytes + lvk::kPipeBlockSize - 1) / lvk::kPipeBlockSize;
+    return pipe_ws_layout(nblocks, cap).total;
+}
+
+bool wal_pipe_applies(const DevCtx &c, uint64_t bytes) {
+    const uint64_t nblocks = (bytes + lvk::kPipeBlockSize - 1) / lvk::kPipeBlockSize;
+    const uint64_t grid = std::min<uint64_t>(static_cast<uint64_t>(c.cus), nblocks);
+    return LVK_WAL_LOCAL && nblocks > 0 && grid <= 1024 && (nblocks + grid - 1) / grid <= lvk::kPipeMaxBlocks;
+}
+
+int launch_wal_pipe(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
+                    uint32_t *d_info, uint64_t cap, uint64_t *d_count, uint8_t *ws, hipStream_t s) {
+    const uint64_t nblocks = (bytes + lvk::kPipeBlockSize - 1) / lvk::kPipeBlockSize;
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(c.cus), nblocks));
+    const PipeWs lay = pipe_ws_layout(nblocks, cap);
+    lvk::WalPipe a{};
+    a.log = d_log;
+    a.size = bytes;
+    a.nblocks = nblocks;
+    a.gran = reinterpret_cast<uint64_t *>(ws + lay.gran);
+    a.hc = reinterpret_cast<uint64_t *>(ws + lay.hc);
+    a.ent = reinterpret_cast<uint4 *>(ws + lay.ent);
+    a.hdr_off = d_hdr_off;
+    a.crc = d_crc;
+    a.info = d_info;
+    a.count = d_count;
+    a.cap = cap;
+    a.err = reinterpret_cast<uint32_t *>(ws + lay.err);
+    // the granules every workgroup polls start at zero in every call (a
+    // memset node under graph capture)
+    LV_HIP(hipMemsetAsync(ws + lay.gran, 0, al16(static_cast<size_t>(grid) * sizeof(uint64_t)), s));
+    hipLaunchKernelGGL(lvk::wal_pipe_kernel, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);
+    return 0;
+}
+
+}  // namespace lvh

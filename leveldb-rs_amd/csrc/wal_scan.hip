@@ -403,7 +403,20 @@ static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
     return w;
 }
 
-size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) { return wal_ws_layout(bytes, cap).total; }
+static thread_local int g_wal_path = 0;  // lv_wal_scan_set_path
+
+int lv_wal_scan_set_path(int path) {
+    if (path < 0 || path > 2) return set_err(LV_ERR_INVALID, "path must be 0, 1 or 2");
+    const int prev = g_wal_path;
+    g_wal_path = path;
+    return prev;
+}
+
+size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) {
+    // either path's layout fits (the one-launch scan's, wal_pipe.hip, or the
+    // five-launch one's below)
+    return std::max<size_t>(wal_ws_layout(bytes, cap).total, wal_pipe_ws_bytes(bytes, cap));
+}
 
 int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
                        size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream) {
@@ -416,7 +429,7 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     if (bytes / lvk::kWalHeader >= 0xffffffffull || cap > 0xffffffffull)
         return set_err(LV_ERR_INVALID, "log too large for one scan");
     const WalWs lay = wal_ws_layout(bytes, cap);
-    if (workspace_bytes < lay.total) return set_err(LV_ERR_INVALID, "workspace too small");
+    if (workspace_bytes < lv_wal_scan_workspace_bytes(bytes, cap)) return set_err(LV_ERR_INVALID, "workspace too small");
     DevCtx *c = nullptr;
     if (int rc = current_ctx(&c)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -426,6 +439,15 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
         return LV_OK;
     }
     uint8_t *wb = static_cast<uint8_t *>(d_workspace);
+    const bool pipe = wal_pipe_applies(*c, bytes);
+    if (g_wal_path == 1 && !pipe) return set_err(LV_ERR_INVALID, "the one-launch scan does not apply to this log");
+    if (pipe && g_wal_path != 2) {
+        // one launch: every workgroup frames, sorts and checksums its own
+        // blocks (wal_pipe.hip)
+        if (int rc = launch_wal_pipe(*c, d_log, bytes, d_hdr_off, d_crc, d_info, cap, d_count, wb, s)) return rc;
+        g_kernel = "wal_pipe_kernel";
+        return check_launch();
+    }
     uint32_t *ws = reinterpret_cast<uint32_t *>(wb);
     uint32_t *M = reinterpret_cast<uint32_t *>(wb + lay.m);
     uint64_t *wgrec = reinterpret_cast<uint64_t *>(wb + lay.wgrec);

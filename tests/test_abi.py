@@ -108,8 +108,9 @@ def test_argument_checks_before_any_device_call():
     assert W.lv_wal_scan_device(fake, 64, fake, fake, fake, 8, fake, fake, need - 1, None) == -1
     assert b"workspace" in L.lv_last_error()
     # the workspace grows with the capacity: a 16-B entry, the CRC by sorted
-    # position and the sorted position per record
-    assert W.lv_wal_scan_workspace_bytes(64, 1008) - need == 1000 * 24
+    # position and the sorted position per record (the five-launch layout,
+    # which bounds the one-launch scan's at this size)
+    assert W.lv_wal_scan_workspace_bytes(64, 2008) - W.lv_wal_scan_workspace_bytes(64, 1008) == 1000 * 24
     # kernel-choice query: empty on a thread that has launched nothing
     import threading
     seen = []

@@ -952,7 +952,7 @@ def _hint_kernel(n, hint, join):
     if n <= 1024:
         return "crc32c_fused_small_kernel" + ("+combine_long_kernel" if join else "")
     if hint.uniform and not join:
-        return "crc32c_classes_kernel"  # a host-known identity list: no sort
+        return "hint_len_kernel+crc32c_classes_kernel"  # a host-known identity list: no sort (lengths checked)
     return "sort+crc32c_classes_kernel" + ("+combine_long_kernel" if join else "")
 
 

@@ -92,7 +92,7 @@ def test_offsets_api_random_sweep(torch_dev, trial):
         join = bool(L.lv_crc32c_hint_needs_join(ctypes.addressof(hint), n,
                                                 torch.cuda.get_device_properties(dev).multi_processor_count))
     if hinted and n > 1024 and hint.uniform and not join:
-        base = "crc32c_classes_kernel"  # host-known identity list: no sort
+        base = "hint_len_kernel+crc32c_classes_kernel"  # host-known identity list: no sort
     assert kern == base + ("+combine_long_kernel" if join else ""), (kern, hinted)
     got = out.cpu().numpy().view(np.uint32)
     want = oracle_batch(arena.cpu().numpy().tobytes(), offs, lens, seeds, masked)
