@@ -39,6 +39,17 @@ typedef struct lv_wal_scan lv_wal_scan;
  * the GPU, CRCs every record and copies the results back.  Returns NULL on
  * error (lv_last_error()).  Records are in log order. */
 lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int device);
+/* The same scan, pipelined against its reader: returns at once, while a
+ * worker thread scans the log in 32 MiB block-aligned chunks (upload, device
+ * scan, results back).  A reader over this scan (lv_wal_reader_new) waits only
+ * for the chunk holding the next header it reaches, so replaying chunk k
+ * overlaps the scan of chunk k + 1; the accessors below wait for the whole
+ * scan.  `log` must stay valid until lv_wal_scan_free.  NULL on an argument
+ * error; a scan error surfaces from the reader (< 0) or lv_wal_scan_wait. */
+lv_wal_scan *lv_wal_scan_host_pipelined(const uint8_t *log, size_t bytes, int device);
+/* Waits for a pipelined scan to finish: 0, or its error (lv_last_error).
+ * Immediate for any other scan. */
+int lv_wal_scan_wait(lv_wal_scan *scan);
 /* Device-resident scan of a log already in HBM (8-byte aligned), with no
  * host synchronisation: every 32 KiB block's header chain is walked inside
  * its workgroup's pass and every [type || payload] unit is checksummed: a
@@ -60,7 +71,8 @@ size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap);
 int lv_wal_scan_set_path(int path);
 int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
                        size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream);
-/* Number of physical records reached by the blocks' header chains. */
+/* Number of physical records reached by the blocks' header chains (a
+ * pipelined scan: waits for it; 0 if it failed). */
 size_t lv_wal_scan_count(const lv_wal_scan *scan);
 /* Header offsets (ascending), value([type||payload]) (0 unless status OK),
  * and info = type | status << 8 | payload_length << 16. */

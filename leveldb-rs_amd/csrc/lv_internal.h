@@ -1,16 +1,52 @@
 // Internal declarations shared by the product sources: the WAL scan object
 // (GPU scan + host reader) and the lv_last_error plumbing.
 #pragma once
+#include <condition_variable>
 #include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
+
+namespace lvgpu_internal {
+// One block-aligned chunk of a pipelined scan (offsets are log offsets).
+struct ScanChunk {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> crc, info;
+};
+// A scan still running (lv_wal_scan_host_pipelined): a worker thread scans
+// the log's chunks in order; readers wait for the chunk they need.
+struct ScanPipe {
+    uint64_t chunk_bytes = 0;
+    std::vector<ScanChunk> chunks;
+    std::mutex m;
+    std::condition_variable cv;
+    size_t ready = 0;  // chunks [0, ready) are complete (all of them once rc != 0)
+    int rc = 0;
+    std::string err;
+    std::thread worker;
+    bool flat = false;  // the scan's flat arrays were filled
+    // 0 once chunk k is complete, or the worker's error
+    int wait(size_t k) {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return ready > k || rc != 0; });
+        return ready > k ? 0 : rc;
+    }
+    ~ScanPipe() {
+        if (worker.joinable()) worker.join();
+    }
+};
+}  // namespace lvgpu_internal
 
 struct lv_wal_scan {
     std::vector<uint64_t> off;   // physical-record header offsets, ascending
     std::vector<uint32_t> crc;   // value([type || payload]) (0 unless status OK)
     std::vector<uint32_t> info;  // type | status << 8 | payload_length << 16
+    // lv_wal_scan_host_pipelined: the chunks still arriving (the flat arrays
+    // above are filled from them when first asked for), or null
+    std::unique_ptr<lvgpu_internal::ScanPipe> pipe;
 };
-
-#include <mutex>
 
 namespace lvgpu_internal {
 int set_error(int code, const char *msg);  // lv_last_error plumbing (context.hip)
@@ -29,6 +65,12 @@ struct DeviceGuard {
     int set(int device);  // LV status; the first call saves the current device
     ~DeviceGuard();
 };
+
+// Scan of log[0, bytes) on `device` into `out` (offsets += base): the body of
+// lv_wal_scan_host, one chunk of a pipelined scan (wal_scan.hip).
+int scan_host_range(const uint8_t *log, size_t bytes, uint64_t base, int device, ScanChunk *out);
+// Waits for a pipelined scan and fills its flat arrays (no-op otherwise).
+int scan_flatten(lv_wal_scan *scan);
 
 // Host-memory path of one device (context.hip): holds the device's
 // host-path lock while alive.  host_upload copies `bytes` of host memory into

@@ -47,6 +47,7 @@
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
     defined(LVK_WAL_LOCAL) || \
+    defined(LVK_WAL_PIPE_TRACE) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -150,6 +151,9 @@
 #endif
 #ifndef LVK_WAL_LOCAL  // WAL scan: one persistent launch, each workgroup frames, sorts and walks its own blocks
 #define LVK_WAL_LOCAL 1
+#endif
+#ifndef LVK_WAL_PIPE_TRACE  // timing only: wal_pipe_kernel writes s_memrealtime stamps per workgroup to its workspace
+#define LVK_WAL_PIPE_TRACE 0
 #endif
 #ifndef LVK_WAL_UNSORT  // WAL scan: CRCs stored by sorted position, then written in log order (wal_unsort)
 #define LVK_WAL_UNSORT 1

@@ -33,10 +33,16 @@ uint32_t decode_fixed_32(const uint8_t *p) {  // coding.rs:70-77
 // ---------------------------------------------------------------------------
 extern "C" {
 
-size_t lv_wal_scan_count(const lv_wal_scan *scan) { return scan ? scan->off.size() : 0; }
-const uint64_t *lv_wal_scan_offsets(const lv_wal_scan *scan) { return scan ? scan->off.data() : nullptr; }
-const uint32_t *lv_wal_scan_crcs(const lv_wal_scan *scan) { return scan ? scan->crc.data() : nullptr; }
-const uint32_t *lv_wal_scan_info(const lv_wal_scan *scan) { return scan ? scan->info.data() : nullptr; }
+// (A pipelined scan fills its flat arrays on the first accessor call.)
+static const lv_wal_scan *flat(const lv_wal_scan *scan) {
+    if (scan && scan->pipe && lvgpu_internal::scan_flatten(const_cast<lv_wal_scan *>(scan))) return nullptr;
+    return scan;
+}
+size_t lv_wal_scan_count(const lv_wal_scan *scan) { return (scan = flat(scan)) ? scan->off.size() : 0; }
+const uint64_t *lv_wal_scan_offsets(const lv_wal_scan *scan) { return (scan = flat(scan)) ? scan->off.data() : nullptr; }
+const uint32_t *lv_wal_scan_crcs(const lv_wal_scan *scan) { return (scan = flat(scan)) ? scan->crc.data() : nullptr; }
+const uint32_t *lv_wal_scan_info(const lv_wal_scan *scan) { return (scan = flat(scan)) ? scan->info.data() : nullptr; }
+int lv_wal_scan_wait(lv_wal_scan *scan) { return lvgpu_internal::scan_flatten(scan); }
 
 lv_wal_scan *lv_wal_scan_from_arrays(const uint64_t *offsets, const uint32_t *crcs, const uint32_t *info,
                                      size_t n) {
@@ -80,6 +86,16 @@ struct lv_wal_reader {
     uint64_t initial_offset;
     bool resyncing;
     size_t cursor = 0;  // scan index hint (reads advance monotonically)
+    size_t pchunk = 0;  // a pipelined scan: the chunk `cursor` indexes
+    // info / crc of a find() result
+    uint32_t info_at(long i) const {
+        if (scan->pipe) return scan->pipe->chunks[i >> 40].info[i & ((1l << 40) - 1)];
+        return scan->info[i];
+    }
+    uint32_t crc_at(long i) const {
+        if (scan->pipe) return scan->pipe->chunks[i >> 40].crc[i & ((1l << 40) - 1)];
+        return scan->crc[i];
+    }
     bool failed = false;
     std::vector<uint8_t> scratch;
 
@@ -88,8 +104,25 @@ struct lv_wal_reader {
         if (reporter && end_of_buffer_offset >= blen + bytes + initial_offset) reporter(ctx, bytes, reason);
     }
 
-    // Scan entry for the header at log offset `hdr`, or -1.
+    // Scan entry for the header at log offset `hdr`, or -1.  A pipelined
+    // scan: the entry within its chunk (waiting for the chunk), as (chunk <<
+    // 40) | index, read back by entry().
     long find(uint64_t hdr) {
+        if (scan->pipe) {  // (the chunk arrays stay valid after a flatten)
+            lvgpu_internal::ScanPipe &p = *scan->pipe;
+            const size_t k = static_cast<size_t>(hdr / p.chunk_bytes);
+            if (k >= p.chunks.size() || p.wait(k)) {
+                if (k < p.chunks.size() && p.rc) lvgpu_internal::set_error(p.rc, ("WAL scan: " + p.err).c_str());
+                return -1;
+            }
+            const auto &off = p.chunks[k].off;
+            if (k == pchunk && cursor < off.size() && off[cursor] == hdr) return static_cast<long>((k << 40) | cursor);
+            auto it = std::lower_bound(off.begin(), off.end(), hdr);
+            if (it == off.end() || *it != hdr) return -1;
+            pchunk = k;
+            cursor = static_cast<size_t>(it - off.begin());
+            return static_cast<long>((k << 40) | cursor);
+        }
         const auto &off = scan->off;
         if (cursor < off.size() && off[cursor] == hdr) return static_cast<long>(cursor);
         auto it = std::lower_bound(off.begin(), off.end(), hdr);
@@ -151,12 +184,12 @@ struct lv_wal_reader {
             }
             if (checksum) {
                 const long i = find(buf);
-                if (i < 0 || ((scan->info[i] >> 8) & 0xffu) != LV_WAL_REC_OK) {
+                if (i < 0 || ((info_at(i) >> 8) & 0xffu) != LV_WAL_REC_OK) {
                     failed = true;
                     return kEof;
                 }
                 const uint32_t expected = lv_crc32c_unmask(decode_fixed_32(h));
-                if (expected != scan->crc[i]) {
+                if (expected != crc_at(i)) {
                     const uint64_t drop = blen;
                     blen = 0;
                     report_drop(drop, "checksum mismatch");
@@ -183,7 +216,8 @@ struct lv_wal_reader {
             uint64_t frag = 0, flen = 0;
             const int rt = read_physical_record(&frag, &flen);
             if (failed) {
-                lvgpu_internal::set_error(LV_ERR_INVALID, "WAL scan does not cover a header the reader reached");
+                if (!(scan->pipe && scan->pipe->rc))
+                    lvgpu_internal::set_error(LV_ERR_INVALID, "WAL scan does not cover a header the reader reached");
                 return -1;
             }
             const uint64_t fsize = (rt == kEof || rt == kBadRecord) ? 0 : flen;

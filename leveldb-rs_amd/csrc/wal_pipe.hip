@@ -79,6 +79,7 @@ enum : uint32_t {
     kCBaseLo,   // this workgroup's first record in log order
     kCBaseHi,
     kCCount,    // this workgroup's records
+    kCDense,    // the phase-B list is in ent[base, ...) (more records than the local slice holds)
 };
 static_assert(kPStage + kPStageN == kPB + 16384, "carve-out fits region B");
 
@@ -87,13 +88,28 @@ struct WalPipe {
     uint64_t size, nblocks;
     uint64_t *gran;  // one {tag 1 | count} granule per workgroup, zeroed before the launch
     uint64_t *hc;    // header cache: kPipeCache per block (pos | len << 16 | type << 32)
-    uint4 *ent;      // phase-B sorted entries {unit addr lo, hi, unit length, record index}
+    uint4 *ent;      // a dense workgroup's phase-B entries (8 B each) from its base on
+    uint64_t *lst;   // phase-B entries of the other workgroups: kPipeCache per block of each
     uint64_t *hdr_off;
     uint32_t *crc, *info;
     uint64_t *count;
     uint64_t cap;
     uint32_t *err;  // set when a workgroup's count never arrived (bounded poll)
+    uint64_t *trace;  // LVK_WAL_PIPE_TRACE: kPipeTrace s_memrealtime stamps per workgroup
 };
+
+// Timing variant (LVK_WAL_PIPE_TRACE): stamps of the phases per workgroup.
+constexpr uint32_t kPipeTrace = 64;
+#if LVK_WAL_PIPE_TRACE
+#define PTRACE(slot)                                                                                   \
+    do {                                                                                               \
+        if ((threadIdx.x & 63u) == 0) a.trace[blockIdx.x * kPipeTrace + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PTRACE(slot) \
+    do {             \
+    } while (0)
+#endif
 
 __device__ __forceinline__ uint32_t &pctl(uint32_t k) { return g_lds[kPCtl + k]; }
 
@@ -126,28 +142,31 @@ struct PipeFirst {
     __device__ __forceinline__ void flush(const Params &, uint32_t, uint32_t, uint32_t) const {}
 };
 
-// Phase B: the workgroup's sorted rest, entries in ent[] (written by its own
-// builder wave: same CU, after an LDS flag).  CRCs by record index: the LDS
-// staging, or (a workgroup with more records) straight to the output in the
-// flush, every kFlush rounds like the class kernel's stores.
+// Phase B: the workgroup's sorted rest.  An entry is 8 bytes: record index
+// (23 bits) | unit length << 23 (15 bits) | the unit's offset from the
+// workgroup's first block << 38 -- in the workgroup's slice of the workspace
+// (written by its own builder wave: same CU, loaded after an LDS flag), or
+// for a dense workgroup in ent[base, ...).  CRCs by record index: the LDS
+// staging, or (a dense workgroup's records past it) straight to the output
+// in the flush, every kFlush rounds like the class kernel's stores.
 struct PipeRest {
     static constexpr uint32_t kFlush = 16;
     static constexpr bool kAlMid = true;
     static constexpr bool kOneRound = false;
     static constexpr uint32_t kExact = LVK_WALK_EXACT;
     static constexpr bool kPlainMerge = true;
-    const uint4 *ent;
-    uint64_t logbase;
-    uint32_t *crc;  // d_crc + the workgroup's base
+    const uint64_t *lst;
+    uint64_t blk0;  // address of the workgroup's first block
+    uint32_t *crc;  // a dense workgroup: d_crc + its base
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
         const uint64_t ec = valid ? e : P.n - 1;
-        const uint4 v = ent[ec];
+        const uint64_t v = lst[ec];
         RGeo q;
-        q.a = v.z ? logbase + ((static_cast<uint64_t>(v.y) << 32) | v.x) : logbase;
-        q.len = v.z;
+        q.len = static_cast<uint32_t>(v >> 23) & 0x7fffu;
+        q.a = blk0 + (q.len ? (v >> 38) : 0u);
         q.seed = 0;
-        q.bid = valid ? v.w : 0xffffffffu;
+        q.bid = valid ? static_cast<uint32_t>(v) & 0x7fffffu : 0xffffffffu;
         q.aux = 0;
         return q;
     }
@@ -166,6 +185,35 @@ struct PipeRest {
             crc[li] = c;
     }
 };
+
+// The rest of a long chain through L2: one dword of every 128-B line of the
+// rest of each block still being walked, four blocks per round trip (wal_hist's
+// touch, wal_scan.hip: the bench log's longest chain is 54 records).
+constexpr uint32_t kPipeTouchHops = 16;
+__device__ __forceinline__ uint32_t pipe_touch(const uint8_t *blk, uint32_t pos, uint32_t blen, bool active,
+                                               uint32_t lane) {
+    uint64_t dm = __ballot(active);
+    uint32_t x = 0;
+    while (dm) {  // wave-uniform
+        uint32_t v[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int l0 = dm ? __ffsll(static_cast<long long>(dm)) - 1 : 0;
+            const bool on = dm != 0;
+            dm &= dm - 1;
+            const uint32_t p0 = __shfl(pos, l0), bl = on ? __shfl(blen, l0) : 0u;
+            const uint64_t b = __shfl(reinterpret_cast<uint64_t>(blk), l0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t o = (p0 & ~127u) + 128u * (lane + 64u * k);
+                v[g][k] = o < bl ? *reinterpret_cast<const uint32_t *>(b + o) : 0u;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) x ^= xor3(v[g][0], v[g][1], v[g][2]) ^ v[g][3];
+    }
+    return x;
+}
 
 // Region A and the combine tables of the G = 16 image (region B stays the
 // carve-out): every thread issues its loads before its first LDS store.
@@ -212,6 +260,7 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
     const uint32_t nblk = static_cast<uint32_t>(hi - lo);  // <= kPipeMaxBlocks (host)
     const uint64_t blk0 = reinterpret_cast<uint64_t>(a.log) + lo * kPipeBlockSize;
     const uint8_t *const log = a.log;
+    if (wave == 0) PTRACE(0);
 
     // ---- 1. the first header of every block (under the table staging) ----
     uint32_t w1 = 0, blen1 = 0;
@@ -261,6 +310,7 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
         }
     }
     __syncthreads();
+    if (wave == 0) PTRACE(1);
     // (values read from LDS are wave-uniform: readfirstlane keeps them in
     // scalar registers, where the walk's list bounds and pointers belong)
     auto uni = [](uint32_t v) { return __builtin_amdgcn_readfirstlane(v); };
@@ -282,10 +332,11 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
     const uint32_t nframers = nblk > 64u ? 2u : 1u;
     if (wave < nframers) {
         const uint32_t fl = wave * 64u + lane;
+        uint32_t touched = 0;
         for (uint32_t b0 = 0; b0 < nblk; b0 += 64u * nframers) {  // wave-uniform
             const uint32_t bl = b0 + fl;
             const uint64_t start = (lo + bl) * kPipeBlockSize;
-            uint32_t blen = 0, pos = 0, cnt = 0;
+            uint32_t blen = 0, pos = 0, cnt = 0, hops = 0;
             bool active = false;
             if (bl < nblk) {
                 blen = static_cast<uint32_t>(a.size - start < kPipeBlockSize ? a.size - start : kPipeBlockSize);
@@ -311,6 +362,11 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
             };
             issue(pos, active);
             while (__any(active)) {  // wave-uniform: the longest chain of the wave
+                // after kPipeTouchHops hops, the rest of each block still being
+                // walked is touched into L2 (one dword per 128-B line, four
+                // blocks per round trip), so the rest of a long chain of short
+                // records hops through L2 instead of HBM (as wal_hist does)
+                if (hops++ == kPipeTouchHops) touched ^= pipe_touch(blk, pos, blen, active, lane);
                 const uint32_t hw = __builtin_amdgcn_alignbyte(whi, wlo, wsh);  // bytes pos + 4 .. pos + 7
                 const uint32_t len = hw & 0xffffu, type = (hw >> 16) & 0xffu;
                 const bool ok = kPipeHeader + len <= blen - pos && (type | len) != 0u;
@@ -330,15 +386,17 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
             }
             if (bl < nblk) g_lds[kPCnt + bl] = cnt;
         }
+        asm volatile("" ::"v"(touched));  // the touches are kept
         // the header cache and this wave's LDS writes are complete before the
         // count that elects the builder
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        PTRACE(2 + wave);
         uint32_t done = 0;
         if (lane == 0)
             done = __hip_atomic_fetch_add(&pctl(kCFramed), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         done = __shfl(done, 0);
         if (done + 1u == nframers) {
-            // ---- 3. the builder: counts, base, hdr_off / info, the phase-B list ----
+            // ---- 3. the builder ----
             uint32_t run = 0;
             for (uint32_t b0 = 0; b0 < nblk; b0 += 64u) {  // exclusive prefix of the block counts
                 const uint32_t bl = b0 + lane;
@@ -353,40 +411,14 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                 run += __shfl(inc, 63);
             }
             const uint32_t count_w = run;
+            PTRACE(4);
             // (global address space: an agent-scope sc1 store / load, never flat)
             typedef __attribute__((address_space(1))) uint64_t gu64;
             gu64 *const gran = reinterpret_cast<gu64 *>(reinterpret_cast<uint64_t>(a.gran));
             if (lane == 0) __hip_atomic_store(gran + w, (1ull << 32) | count_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // every workgroup's count (bounded poll: ~0.2 s of s_memrealtime at 100 MHz)
-            uint64_t base = 0, total = 0;
-            bool timeout = false;
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t j0 = 0; j0 < grid; j0 += 64u) {  // wave-uniform
-                const uint32_t j = j0 + lane;
-                uint64_t v = 0;
-                for (;;) {
-                    if (j < grid) v = __hip_atomic_load(gran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__all(j >= grid || (v >> 32) == 1u)) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
-                        timeout = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(8);
-                }
-                const uint64_t c = j < grid ? (v & 0xffffffffull) : 0u;
-                base += j < w ? c : 0u;
-                total += c;
-            }
-#pragma unroll
-            for (int k = 32; k >= 1; k >>= 1) {
-                base += __shfl_xor(base, k);
-                total += __shfl_xor(total, k);
-            }
-            const bool abort = timeout || total > a.cap;
-            if (w == 0 && lane == 0) *a.count = timeout ? ~0ull : total;
-            if (timeout && lane == 0) atomicOr(a.err, 1u);
-            if (!abort) {
-                // phase-B key starts in walk order (class 2, 1, 0)
+            // phase-B key starts in walk order (class 2, 1, 0); lanes 0-15
+            // hold class 2, 16-31 class 1, 32-47 class 0 (48-63: class 3, empty)
+            {
                 uint32_t c4[4], inc4 = 0;
 #pragma unroll
                 for (uint32_t i = 0; i < 4; ++i) {
@@ -405,25 +437,37 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                     g_lds[kPHist + pipe_order_key(4u * lane + i)] = s;
                     s += c4[i];
                 }
-                // lanes 0-15 hold class 2, 16-31 class 1, 32-47 class 0
                 const uint32_t e16 = __shfl(inc, 15), e4 = __shfl(inc, 31), e1 = __shfl(inc, 47);
-                const uint32_t tot = __shfl(inc, 63);
-                (void)tot;
                 if (lane == 0) {
                     pctl(kCN16) = e16;  // (class 3 is empty: a unit is at most 32,762 B)
                     pctl(kCN4) = e4 - e16;
                     pctl(kCN1) = e1 - e4;
-                    pctl(kCBaseLo) = static_cast<uint32_t>(base);
-                    pctl(kCBaseHi) = static_cast<uint32_t>(base >> 32);
                     pctl(kCCount) = count_w;
                 }
-                __builtin_amdgcn_wave_barrier();
-                uint64_t *const hdr = a.hdr_off + base;
-                uint32_t *const info = a.info + base;
-                uint4 *const ent = a.ent + base;
-                const uint64_t lb = lo * kPipeBlockSize;
-                // records in log order: record q is record k = q - pre[bl] of
-                // the last block bl with pre[bl] <= q
+            }
+            // Every record of the workgroup in log order: record q is record
+            // k = q - pre[bl] of the last block bl with pre[bl] <= q.  LIST:
+            // its phase-B entry (claimed slot); OUT: hdr_off / info at base.
+            // Blocks of more than kPipeCache records walk on from the last
+            // cached header (one lane per block; rare: a 32 KiB block holds
+            // more than 64 records only when they are a few bytes long).
+            const uint64_t lb = lo * kPipeBlockSize;
+            auto emit = [&](uint64_t *list, uint64_t *hdr, uint32_t *info) {
+                auto one = [&](uint32_t q, uint32_t bl, uint32_t pos, uint32_t len, uint32_t type, uint32_t blen,
+                               bool rec, bool inb) {
+                    const uint32_t st = pipe_status(len, type, blen, pos);
+                    const uint32_t ulen = st == LV_WAL_REC_OK ? len + 1u : 0u;
+                    const uint32_t slot = list ? wave_claim(&g_lds[kPHist], sort_key(ulen), rec && inb, lane) : 0u;
+                    if (rec && hdr) {
+                        hdr[q] = lb + static_cast<uint64_t>(bl) * kPipeBlockSize + pos;
+                        info[q] = type | (st << 8) | (len << 16);
+                    }
+                    if (rec && inb && list) {
+                        const uint64_t ua = static_cast<uint64_t>(bl) * kPipeBlockSize + pos + 6u;  // [type || payload]
+                        list[slot] = q | (static_cast<uint64_t>(ulen) << 23) | (ua << 38);
+                    }
+                    return st;
+                };
                 for (uint32_t q0 = 0; q0 < count_w; q0 += 64u) {  // wave-uniform
                     const uint32_t q = q0 + lane;
                     uint32_t bl = 0;
@@ -447,22 +491,10 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                             type = static_cast<uint32_t>(h >> 32) & 0xffu;
                         }
                     }
-                    const uint32_t st = pipe_status(len, type, blen, pos);
-                    const uint32_t ulen = st == LV_WAL_REC_OK ? len + 1u : 0u;
-                    const bool inb = rec && !(k == 0 && ulen >= kPipeAMin);  // phase A walks the others
-                    const uint32_t slot = wave_claim(&g_lds[kPHist], sort_key(ulen), inb, lane);
-                    if (rec) {
-                        hdr[q] = start + pos;
-                        info[q] = type | (st << 8) | (len << 16);
-                    }
-                    if (inb) {
-                        const uint64_t ua = start + pos + 6u;  // [type || payload], log_reader.rs:336
-                        ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), ulen, q);
-                    }
+                    const bool firstA = k == 0 && pipe_status(len, type, blen, 0) == LV_WAL_REC_OK &&
+                                        len + 1u >= kPipeAMin;  // phase A walked it
+                    one(q, bl, pos, len, type, blen, rec, !firstA);
                 }
-                // blocks of more than kPipeCache records walk on from the last
-                // cached header (one lane per block; a 32 KiB block holds more
-                // than 64 records only when they are a few bytes long)
                 for (uint32_t b0 = 0; b0 < nblk; b0 += 64u) {  // wave-uniform
                     const uint32_t bl = b0 + lane;
                     const uint32_t c = bl < nblk ? g_lds[kPCnt + bl] : 0u;
@@ -478,51 +510,101 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                         q = g_lds[kPPre + bl] + kPipeCache;
                     }
                     while (__any(active)) {
-                        uint32_t len = 0, type = 0, st = 0;
+                        uint32_t len = 0, type = 0;
                         if (active) {
                             const uint64_t hb = start + pos + 4u;
-                            uint32_t b4 = log[hb], b5 = log[hb + 1], b6 = log[hb + 2];
-                            len = b4 | (b5 << 8);
-                            type = b6;
-                            st = pipe_status(len, type, blen, pos);
+                            len = static_cast<uint32_t>(log[hb]) | (static_cast<uint32_t>(log[hb + 1]) << 8);
+                            type = log[hb + 2];
                         }
-                        const uint32_t ulen = st == LV_WAL_REC_OK ? len + 1u : 0u;
-                        const uint32_t slot = wave_claim(&g_lds[kPHist], sort_key(ulen), active, lane);
+                        const uint32_t st = one(q, bl, pos, len, type, blen, active, true);
                         if (active) {
-                            hdr[q] = start + pos;
-                            info[q] = type | (st << 8) | (len << 16);
-                            const uint64_t ua = start + pos + 6u;
-                            ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), ulen, q);
                             ++q;
                             pos += kPipeHeader + len;
                             active = st == LV_WAL_REC_OK && blen - pos >= kPipeHeader;
                         }
                     }
                 }
-            } else if (lane == 0) {
-                pctl(kCAbort) = 1u;
-                pctl(kCN16) = 0u;
-                pctl(kCN4) = 0u;
-                pctl(kCN1) = 0u;
+            };
+            auto ready = [&]() {  // the list is in memory before the flag (same CU: walkers load after it)
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(&pctl(kCReady), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                PTRACE(6);
+            };
+            // Every workgroup's count (bounded poll, ~0.2 s of s_memrealtime
+            // at 100 MHz): this one's base in the log-order output and the
+            // total for the capacity check.
+            uint64_t base = 0, total = 0;
+            bool timeout = false;
+            auto lookback = [&]() {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (uint32_t j0 = 0; j0 < grid; j0 += 64u) {  // wave-uniform
+                    const uint32_t j = j0 + lane;
+                    uint64_t v = 0;
+                    for (;;) {
+                        if (j < grid) v = __hip_atomic_load(gran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (__all(j >= grid || (v >> 32) == 1u)) break;
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+                            timeout = true;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(8);
+                    }
+                    const uint64_t c = j < grid ? (v & 0xffffffffull) : 0u;
+                    base += j < w ? c : 0u;
+                    total += c;
+                }
+#pragma unroll
+                for (int k = 32; k >= 1; k >>= 1) {
+                    base += __shfl_xor(base, k);
+                    total += __shfl_xor(total, k);
+                }
+                PTRACE(5);
+                const bool abort = timeout || total > a.cap;
+                if (w == 0 && lane == 0) *a.count = timeout ? ~0ull : total;
+                if (timeout && lane == 0) atomicOr(a.err, 1u);
+                if (lane == 0) {
+                    pctl(kCBaseLo) = static_cast<uint32_t>(base);
+                    pctl(kCBaseHi) = static_cast<uint32_t>(base >> 32);
+                    pctl(kCAbort) = abort ? 1u : 0u;
+                }
+                return abort;
+            };
+            const bool local = count_w <= kPStageN && count_w <= kPipeCache * nblk;
+            if (local) {
+                // the list in this workgroup's slice of the workspace: ready
+                // as soon as the framing is done, before any other workgroup's
+                // count is known
+                emit(a.lst + lo * kPipeCache, nullptr, nullptr);
+                ready();
+                if (!lookback()) emit(nullptr, a.hdr_off + base, a.info + base);
+            } else {
+                // a dense workgroup: the list goes to ent[base, ...) (at most
+                // cap entries in all), so it waits for the base
+                if (!lookback())
+                    emit(reinterpret_cast<uint64_t *>(a.ent) + base, a.hdr_off + base, a.info + base);
+                else if (lane == 0)
+                    pctl(kCN16) = pctl(kCN4) = pctl(kCN1) = 0u;
+                if (lane == 0) pctl(kCDense) = 1u;
+                ready();
             }
-            // the entries are in memory before the flag (same CU: the walkers'
-            // loads of them follow the flag)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_store(&pctl(kCReady), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
 
     // ---- 4. every wave: phase A, then (after the flag) the phase-B lists ----
     walk_first();
+    PTRACE(8 + wave);
     while (__hip_atomic_load(&pctl(kCReady), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(16);
-    const bool abort = uni(pctl(kCAbort)) != 0u;
-    const uint64_t base = (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo));
-    const uint32_t n16 = uni(pctl(kCN16)), n4 = uni(pctl(kCN4)), n1 = uni(pctl(kCN1));
-    if (!abort) {
-        const PipeRest r16{a.ent + base, reinterpret_cast<uint64_t>(log), a.crc + base};
-        const PipeRest r4{a.ent + base + n16, reinterpret_cast<uint64_t>(log), a.crc + base};
-        const PipeRest r1{a.ent + base + n16 + n4, reinterpret_cast<uint64_t>(log), a.crc + base};
+    PTRACE(24 + wave);
+    {
+        const bool dense = uni(pctl(kCDense)) != 0u;
+        const uint32_t n16 = uni(pctl(kCN16)), n4 = uni(pctl(kCN4)), n1 = uni(pctl(kCN1));
+        const uint64_t base = dense ? (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo)) : 0u;
+        const uint64_t *const lst = dense ? reinterpret_cast<const uint64_t *>(a.ent) + base : a.lst + lo * kPipeCache;
+        uint32_t *const crcd = a.crc + base;  // dense: records past the LDS staging go straight out
+        const PipeRest r16{lst, blk0, crcd};
+        const PipeRest r4{lst + n16, blk0, crcd};
+        const PipeRest r1{lst + n16 + n4, blk0, crcd};
         Params P{};
         auto next16 = [&]() { return pool(kCPool16); };
         auto next4 = [&]() { return pool(kCPool4); };
@@ -534,9 +616,11 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
         P.n = n1;
         sorted_stream<1>(P, r1, lane, L, next1(), next1);
     }
+    PTRACE(40 + wave);
     __syncthreads();
-    if (abort) return;
+    if (uni(pctl(kCAbort))) return;
     // ---- 5. the workgroup's CRCs in log order ----
+    const uint64_t base = (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo));
     const uint32_t count_w = uni(pctl(kCCount));
     uint32_t *const crc = a.crc + base;
     for (uint32_t bl = t; bl < nblk; bl += kThreads) {  // phase A's CRCs to their record index
@@ -552,6 +636,7 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
     __syncthreads();
     const uint32_t ns = count_w < kPStageN ? count_w : kPStageN;
     for (uint32_t i = t; i < ns; i += kThreads) crc[i] = g_lds[kPStage + i];
+    if (wave == 0) PTRACE(56);
 }
 
 }  // namespace lvk
@@ -561,16 +646,19 @@ namespace lvh {
 // The one-launch scan's workspace: the count granules (zeroed before every
 // launch), the header cache, the phase-B entries.
 struct PipeWs {
-    size_t gran, hc, ent, err, total;
+    size_t gran, hc, lst, ent, err, total;
 };
 
 static PipeWs pipe_ws_layout(uint64_t nblocks, uint64_t cap) {
     PipeWs w;
     w.gran = 0;
     w.err = al16(1024 * sizeof(uint64_t));
-    w.hc = w.err + 16;
-    w.ent = w.hc + al16(nblocks * lvk::kPipeCache * sizeof(uint64_t));
-    w.total = w.ent + al16(cap * sizeof(uint4));
+    // (LVK_WAL_PIPE_TRACE: the stamps right after the error word, at byte
+    // 8,208 of the workspace: tools/wal_pipe_trace.py reads them there)
+    w.hc = w.err + 16 + (LVK_WAL_PIPE_TRACE ? 1024 * lvk::kPipeTrace * sizeof(uint64_t) : 0);
+    w.lst = w.hc + al16(nblocks * lvk::kPipeCache * sizeof(uint64_t));
+    w.ent = w.lst + al16(nblocks * lvk::kPipeCache * sizeof(uint64_t));
+    w.total = w.ent + al16(cap * sizeof(uint64_t));
     return w;
 }
 
@@ -597,12 +685,14 @@ int launch_wal_pipe(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint6
     a.gran = reinterpret_cast<uint64_t *>(ws + lay.gran);
     a.hc = reinterpret_cast<uint64_t *>(ws + lay.hc);
     a.ent = reinterpret_cast<uint4 *>(ws + lay.ent);
+    a.lst = reinterpret_cast<uint64_t *>(ws + lay.lst);
     a.hdr_off = d_hdr_off;
     a.crc = d_crc;
     a.info = d_info;
     a.count = d_count;
     a.cap = cap;
     a.err = reinterpret_cast<uint32_t *>(ws + lay.err);
+    a.trace = LVK_WAL_PIPE_TRACE ? reinterpret_cast<uint64_t *>(ws + lay.err + 16) : nullptr;
     // the granules every workgroup polls start at zero in every call (a
     // memset node under graph capture)
     LV_HIP(hipMemsetAsync(ws + lay.gran, 0, al16(static_cast<size_t>(grid) * sizeof(uint64_t)), s));

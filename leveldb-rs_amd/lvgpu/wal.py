@@ -32,6 +32,10 @@ def _bind():
     vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
     L.lv_wal_scan_host.restype = vp
     L.lv_wal_scan_host.argtypes = [vp, sz, ctypes.c_int]
+    L.lv_wal_scan_host_pipelined.restype = vp
+    L.lv_wal_scan_host_pipelined.argtypes = [vp, sz, ctypes.c_int]
+    L.lv_wal_scan_wait.restype = ctypes.c_int
+    L.lv_wal_scan_wait.argtypes = [vp]
     L.lv_wal_scan_count.restype = sz
     L.lv_wal_scan_count.argtypes = [vp]
     for f in ("lv_wal_scan_offsets", "lv_wal_scan_crcs", "lv_wal_scan_info"):
@@ -79,6 +83,23 @@ class Scan:
         if not h:
             _err("lv_wal_scan_host")
         return cls(h)
+
+    @classmethod
+    def host_pipelined(cls, log: bytes, device: int = 0) -> "Scan":
+        """lv_wal_scan_host_pipelined: returns at once; a Reader over it waits
+        only for the 32 MiB chunk holding its next header."""
+        L = _bind()
+        buf = ctypes.create_string_buffer(bytes(log), max(len(log), 1))
+        h = L.lv_wal_scan_host_pipelined(buf, len(log), device)
+        if not h:
+            _err("lv_wal_scan_host_pipelined")
+        s = cls(h)
+        s._buf = buf  # the worker reads the log until the scan is freed
+        return s
+
+    def wait(self) -> None:
+        if _bind().lv_wal_scan_wait(self._h):
+            _err("lv_wal_scan_wait")
 
     @classmethod
     def from_arrays(cls, offsets, crcs, info) -> "Scan":

@@ -1014,7 +1014,7 @@ ALIGNED_HINT_CASES = {
     "2000x8KiB": (2000, 8192, "crc32c_blocks_kernel<16,pieces,fused,gather>"),
     "16x1MiB": (16, 1 << 20, "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_kernel"),
     "1x16MiB": (1, 16 << 20, "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_wg_kernel"),
-    "5000x4000B": (5000, 4000, "crc32c_classes_kernel"),  # not whole 1 KiB batches: the identity list
+    "5000x4000B": (5000, 4000, "hint_len_kernel+crc32c_classes_kernel"),  # not whole 1 KiB batches: the identity list
     "600x1000B": (600, 1000, "crc32c_fused_small_kernel"),
 }
 

@@ -34,11 +34,11 @@ def _random_records(rng, n, maxlog=17):
 
 def _check_scan(log):
     import lvgpu.wal as LW
-    s = LW.Scan.host(log)
     o, c, i = W.scan_log(log)
-    assert s.offsets.tolist() == o
-    assert s.info.tolist() == i
-    assert s.crcs.tolist() == c
+    for s in (LW.Scan.host(log), LW.Scan.host_pipelined(log)):
+        assert s.offsets.tolist() == o
+        assert s.info.tolist() == i
+        assert s.crcs.tolist() == c
 
 
 def test_scan_small_logs(gpu):
@@ -92,6 +92,42 @@ def test_encode_empty_batch(gpu):
     empties = [b""] * 5
     for dest_length in (0, B - H - 2):
         assert LW.encode(empties, dest_length=dest_length) == _oracle_encode(empties, dest_length)
+
+
+def test_pipelined_scan_reader_over_chunks(gpu):
+    """lv_wal_scan_host_pipelined over a log of several 32 MiB chunks: the
+    Reader replays every record while later chunks are still being scanned
+    (it waits per chunk), with no reports; the finished scan's arrays equal
+    lv_wal_scan_host's.  Corrupted bytes in the second chunk are reported the
+    same way by both scans' readers."""
+    import lvgpu.wal as LW
+    rng = np.random.default_rng(41)
+    recs = _random_records(rng, 20000, maxlog=14)
+    log = LW.encode(recs)
+    assert len(log) > 2 * (32 << 20)
+    rep = W.ReportCollector()
+    r = LW.Reader(log, LW.Scan.host_pipelined(log), rep)
+    for want in recs:
+        assert r.read_record() == want
+    assert r.read_record() is None
+    assert rep.dropped_bytes == 0 and rep.message == ""
+    a, b = LW.Scan.host(log), LW.Scan.host_pipelined(log)
+    b.wait()
+    assert np.array_equal(a.offsets, b.offsets) and np.array_equal(a.crcs, b.crcs)
+    assert np.array_equal(a.info, b.info)
+    bad = bytearray(log)
+    for pos in rng.integers(33 << 20, 40 << 20, size=10):
+        bad[int(pos)] ^= 0x5A
+    bad = bytes(bad)
+    got = []
+    for scan in (LW.Scan.host(bad), LW.Scan.host_pipelined(bad)):
+        rep = W.ReportCollector()
+        rd = LW.Reader(bad, scan, rep)
+        n = 0
+        while rd.read_record() is not None:
+            n += 1
+        got.append((n, rep.dropped_bytes, rep.message))
+    assert got[0] == got[1] and got[0][1] > 0
 
 
 def test_encode_then_scan_then_read(gpu):

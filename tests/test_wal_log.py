@@ -19,7 +19,9 @@ B, H = W.BLOCK_SIZE, W.HEADER_SIZE
 
 
 class LogTest:
-    """log_writer.rs:268-443, over one of the three backends."""
+    """log_writer.rs:268-443, over one of the backends: the oracle, the native
+    reader over an oracle scan, the GPU (encode + lv_wal_scan_host), and the
+    GPU with the pipelined scan (lv_wal_scan_host_pipelined)."""
 
     def __init__(self, backend="oracle"):
         self.backend = backend
@@ -34,6 +36,7 @@ class LogTest:
         self.reader = None
         if backend == "oracle":
             self.reader = W.Reader(self.source, self.reporter, True, 0)
+        self.gpu = backend in ("gpu", "gpu_pipelined")
 
     # -- writer side --
     def _flush(self):
@@ -46,7 +49,7 @@ class LogTest:
 
     def write(self, msg):
         assert not self.reading
-        if self.backend == "gpu":
+        if self.gpu:
             self.pending.append(msg.encode())
         else:
             self.writer.add_record(msg.encode())
@@ -61,6 +64,8 @@ class LogTest:
         import lvgpu.wal as LW
         if self.backend == "gpu":
             scan = LW.Scan.host(log)
+        elif self.backend == "gpu_pipelined":  # the reader waits on the scan's chunks as it goes
+            scan = LW.Scan.host_pipelined(log)
         else:
             scan = LW.Scan.from_arrays(*W.scan_log(log))
         return LW.Reader(log, scan, self.reporter, True, initial_offset)
@@ -146,9 +151,10 @@ class LogTest:
         assert rd.read_record() is None
 
 
-@pytest.fixture(params=["oracle", "native", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.fixture(params=["oracle", "native", pytest.param("gpu", marks=pytest.mark.gpu),
+                        pytest.param("gpu_pipelined", marks=pytest.mark.gpu)])
 def LogTest_(request):
-    if request.param == "gpu":
+    if request.param in ("gpu", "gpu_pipelined"):
         request.getfixturevalue("gpu")
     return lambda: LogTest(request.param)
 
