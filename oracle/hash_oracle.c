@@ -4,7 +4,7 @@
  * CPU restatement of sunchao/leveldb-rs `src/util/hash.rs:20-51` (the
  * murmur-like hash behind the block cache's shard choice, `util/cache.rs:182`,
  * `:394-399`).  Checker for the batched GPU hash; the product never links it.
- * Pinned by the reference KATs `hash.rs:58-75` (tests/test_oracle_hash.py).
+ * Pinned by the reference KATs `hash.rs:58-75` (tests/test_hash.py).
  *
  * Overflow: `h += w` / `h += byte << k` are plain `+=` on u32 in the reference;
  * a release build (and upstream LevelDB's Hash) wraps, which is what the KATs
