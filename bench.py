@@ -1056,6 +1056,17 @@ def wal_bench(args):
     t_rec = R.lv_replay_recover(out.ctypes.data, out.size, 0, 5, ctypes.byref(nr), ctypes.byref(nb))
     if t_rec < 0 or nr.value != sizes.size or nb.value != int(sizes.sum()):
         raise SystemExit(f"pipelined recovery failed: {t_rec} s, {nr.value} records, {nb.value} bytes")
+    # its parts: the pipelined scan alone (to completion), and the Reader over
+    # a completed chunked scan
+    R.lv_replay_scan_pipelined.restype = ctypes.c_double
+    R.lv_replay_scan_pipelined.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+    t_pscan = R.lv_replay_scan_pipelined(out.ctypes.data, out.size, 0, 5)
+    psc = LW.Scan.host_pipelined(log)
+    psc.wait()
+    t_pread = R.lv_replay_reader(out.ctypes.data, out.size, psc._h, 5, ctypes.byref(nr), ctypes.byref(nb))
+    del psc
+    if t_pscan < 0 or t_pread < 0:
+        raise SystemExit(f"pipelined scan parts failed: {t_pscan}, {t_pread}")
     cpu = wal_cpu_baseline(out, args.cpu_seconds, int(o.size)) if args.cpu_seconds > 0 else None
     gib = out.size / 2**30
     print(json.dumps({"metric": "WAL group-commit encode and whole-log verify, host memory end to end",
@@ -1079,7 +1090,9 @@ def wal_bench(args):
                                              "records": int(nr.value),
                                              "note": "lv_wal_scan_host_pipelined + the Reader loop + free, one C "
                                                      "loop (tools/host_replay.c), best of 5: the Reader replays "
-                                                     "32 MiB chunk k while chunk k + 1 is uploaded and scanned"},
+                                                     "32 MiB chunk k while chunk k + 1 is uploaded and scanned",
+                                             "parts_ms": {"pipelined_scan_alone": round(t_pscan * 1e3, 2),
+                                                          "reader_over_finished_chunks": round(t_pread * 1e3, 2)}},
                       "cpu_baseline": cpu,
                       "data": "synthetic: Random(301).skewed(17) record sizes, random payload"}), flush=True)
 

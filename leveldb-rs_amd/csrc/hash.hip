@@ -54,6 +54,12 @@
 #include "lv_internal.h"
 #include "lvk/knobs.h"
 
+#if LVK_HASH_KPL == 2
+#define LVH_HASH_KERNEL lvh::hash_kernel2
+#else
+#define LVH_HASH_KERNEL lvh::hash_kernel
+#endif
+
 namespace lvh {
 
 constexpr uint32_t kM = 0xc6a4a793u;  // hash.rs:23
@@ -98,6 +104,63 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
         v = o > v ? o : v;
     }
     return v;
+}
+
+// hash.rs:25-48 of one key of any length read straight from memory
+// (dword-aligned reads, funnel-shifted by the key's misalignment, never a
+// dword past its last byte); h arrives as seed ^ (kM * L).
+__device__ __forceinline__ uint32_t key_from_mem(const uint8_t *__restrict__ base, uint64_t o, uint32_t L,
+                                                 uint32_t h) {
+    const uint32_t bs = static_cast<uint32_t>(o & 3u);
+    const uint32_t nw = L >> 2;
+    const uint32_t ndw = (bs + L + 3) >> 2;
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
+    uint32_t cur = d[0];
+    uint32_t k = 0;
+    // The first 4 quads (keys up to ~64 B: cache keys) are requested
+    // together, so a key costs one memory latency rather than one per
+    // quad; the loop below continues for longer keys.
+    constexpr uint32_t kPre = 4;
+    u32x4a4 pre[kPre];
+#pragma unroll
+    for (uint32_t m = 0; m < kPre; ++m)
+        if (4 * m + 4 <= nw && 4 * m + 4 < ndw) pre[m] = *reinterpret_cast<const u32x4a4 *>(d + 4 * m + 1);
+#pragma unroll
+    for (uint32_t m = 0; m < kPre; ++m) {
+        if (!(k + 4 <= nw && k + 4 < ndw)) break;
+        const u32x4a4 v = pre[m];
+        h = mix(h, funnel(v.x, cur, bs));
+        h = mix(h, funnel(v.y, v.x, bs));
+        h = mix(h, funnel(v.z, v.y, bs));
+        h = mix(h, funnel(v.w, v.z, bs));
+        cur = v.w;
+        k += 4;
+    }
+    // 4 words per step from d[k+1 .. k+4], all inside the buffer's dwords
+    for (; k + 4 <= nw && k + 4 < ndw; k += 4) {
+        const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + k + 1);
+        h = mix(h, funnel(v.x, cur, bs));
+        h = mix(h, funnel(v.y, v.x, bs));
+        h = mix(h, funnel(v.z, v.y, bs));
+        h = mix(h, funnel(v.w, v.z, bs));
+        cur = v.w;
+    }
+    for (; k < nw; ++k) {
+        const uint32_t hi = k + 1 < ndw ? d[k + 1] : 0u;
+        h = mix(h, funnel(hi, cur, bs));
+        cur = hi;
+    }
+    const uint32_t diff = L - 4 * nw;          // hash.rs:38-48
+    if (diff) {
+        const uint32_t hi = nw + 1 < ndw ? d[nw + 1] : 0u;
+        const uint32_t t = funnel(hi, cur, bs);
+        if (diff >= 3) h += ((t >> 16) & 0xffu) << 16;
+        if (diff >= 2) h += ((t >> 8) & 0xffu) << 8;
+        h += t & 0xffu;
+        h *= kM;
+        h ^= h >> 24;
+    }
+    return h;
 }
 
 // Hash of this lane's key of one wave-set of 64 keys (metadata already
@@ -230,52 +293,7 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
             h ^= h >> 24;
         }
     } else if (valid && L) {
-        const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
-        uint32_t cur = d[0];
-        uint32_t k = 0;
-        // The first 4 quads (keys up to ~64 B: cache keys) are requested
-        // together, so a key costs one memory latency rather than one per
-        // quad; the loop below continues for longer keys.
-        constexpr uint32_t kPre = 4;
-        u32x4a4 pre[kPre];
-#pragma unroll
-        for (uint32_t m = 0; m < kPre; ++m)
-            if (4 * m + 4 <= nw && 4 * m + 4 < ndw) pre[m] = *reinterpret_cast<const u32x4a4 *>(d + 4 * m + 1);
-#pragma unroll
-        for (uint32_t m = 0; m < kPre; ++m) {
-            if (!(k + 4 <= nw && k + 4 < ndw)) break;
-            const u32x4a4 v = pre[m];
-            h = mix(h, funnel(v.x, cur, bs));
-            h = mix(h, funnel(v.y, v.x, bs));
-            h = mix(h, funnel(v.z, v.y, bs));
-            h = mix(h, funnel(v.w, v.z, bs));
-            cur = v.w;
-            k += 4;
-        }
-        // 4 words per step from d[k+1 .. k+4], all inside the buffer's dwords
-        for (; k + 4 <= nw && k + 4 < ndw; k += 4) {
-            const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + k + 1);
-            h = mix(h, funnel(v.x, cur, bs));
-            h = mix(h, funnel(v.y, v.x, bs));
-            h = mix(h, funnel(v.z, v.y, bs));
-            h = mix(h, funnel(v.w, v.z, bs));
-            cur = v.w;
-        }
-        for (; k < nw; ++k) {
-            const uint32_t hi = k + 1 < ndw ? d[k + 1] : 0u;
-            h = mix(h, funnel(hi, cur, bs));
-            cur = hi;
-        }
-        const uint32_t diff = L - 4 * nw;          // hash.rs:38-48
-        if (diff) {
-            const uint32_t hi = nw + 1 < ndw ? d[nw + 1] : 0u;
-            const uint32_t t = funnel(hi, cur, bs);
-            if (diff >= 3) h += ((t >> 16) & 0xffu) << 16;
-            if (diff >= 2) h += ((t >> 8) & 0xffu) << 8;
-            h += t & 0xffu;
-            h *= kM;
-            h ^= h >> 24;
-        }
+        h = key_from_mem(base, o, L, h);
     }
     return h;
 }
@@ -398,8 +416,144 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     }
 }
 
+// ---- two keys per lane (LVK_HASH_KPL == 2) ----
+// A wave hashes sets of 128 keys: lane l owns keys 128 s + l and 128 s + 64 +
+// l, both halves' metadata requested one set ahead (every lane, clamped), the
+// set's span staged through LDS once, and the two keys' chains run in one
+// loop so their exec-mask steps and the per-set wave work (span, ballots,
+// staging, stores) are paid once per 128 keys instead of per 64.  A stage of
+// kSpan2 bytes per wave (LDS: 4 x (kSpan2 + 80) B per workgroup).
+constexpr uint32_t kSpan2 = LVK_HASH_SPAN2;
+constexpr uint32_t kCh2 = (kSpan2 / 16 + 63) / 64;
+static_assert(kSpan2 % 16 == 0, "stage of whole granules");
+
+// hash.rs:25-48 for K keys whose windows (<= kFastDw dwords from the key's
+// aligned-down start) lie in LDS at sd[k]; on[k] false leaves h[k] alone.
+template <uint32_t K>
+__device__ __forceinline__ void chains_staged(const uint32_t *const (&sd)[K], const uint32_t (&bs)[K],
+                                              const uint32_t (&L)[K], const bool (&on)[K], uint32_t (&h)[K]) {
+    uint32_t w[K][kFastDw + 1];
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) {
+#pragma unroll
+        for (uint32_t j = 0; j < kFastDw; ++j) w[k][j] = sd[k][j];  // the stage's pad keeps every window inside it
+        w[k][kFastDw] = 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kFastDw; ++j) {
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k)
+            if (on[k] && j < (L[k] >> 2)) h[k] = mix(h[k], funnel(w[k][j + 1], w[k][j], bs[k]));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t nw = L[k] >> 2, diff = L[k] & 3u;  // hash.rs:38-48: the tail word re-read
+        if (on[k] && diff) {
+            const uint32_t ndw = (bs[k] + L[k] + 3) >> 2;
+            const uint32_t tw = funnel(nw + 1 < ndw ? sd[k][nw + 1] : 0u, sd[k][nw], bs[k]);
+            uint32_t x = h[k];
+            if (diff >= 3) x += ((tw >> 16) & 0xffu) << 16;
+            if (diff >= 2) x += ((tw >> 8) & 0xffu) << 8;
+            x += tw & 0xffu;
+            x *= kM;
+            h[k] = x ^ (x >> 24);
+        }
+    }
+}
+
+template <typename Meta>
+__global__ void __launch_bounds__(256) hash_kernel2(const uint8_t *__restrict__ base, Meta meta,
+                                                    uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
+    __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpan2 / 4 + kSpanPad];
+    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
+    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
+    if (set * 128u >= n) return;  // wave-uniform
+    uint32_t *stage = span[wv];
+    MetaRaw ca = meta.load(set * 128u + lane, n, lane), cb = meta.load(set * 128u + 64u + lane, n, lane);
+    uint32_t *pa = out, *pb = out, va = 0, vb = 0;  // the previous set's results, stored one set late
+    bool sa = false, sb = false;
+    for (;;) {
+        const uint64_t nxt = set + W;
+        const bool more = nxt * 128u < n;  // wave-uniform
+        const MetaRaw na = meta.load(nxt * 128u + lane, n, lane), nb = meta.load(nxt * 128u + 64u + lane, n, lane);
+        const uint64_t ia = set * 128u + lane, ib = ia + 64u;
+        const bool vA = ia < n, vB = ib < n;
+        uint64_t oA, oB;
+        uint32_t LA, LB, dA, dB;
+        meta.get(ca, ia, n, lane, oA, LA, dA);
+        meta.get(cb, ib, n, lane, oB, LB, dB);
+        // candidate span: A's first key to the last valid key's end; staged
+        // only if every key lies inside it (keys packed in order)
+        const uint64_t actB = __ballot(vB), actA = __ballot(vA);
+        const uint64_t lo = __shfl(oA, 0);
+        const uint64_t hi = actB ? __shfl(oB + LB, 63 - __builtin_clzll(actB))
+                                 : __shfl(oA + LA, 63 - __builtin_clzll(actA));
+        const uint64_t lo16 = lo & ~15ull;
+        const bool inside = (!LA || (oA >= lo && oA + LA <= hi)) && (!LB || (oB >= lo && oB + LB <= hi));
+        const bool staged = hi > lo && hi - lo16 <= kSpan2 && __all(inside);  // wave-uniform
+        if (staged) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(base + lo16);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(stage);
+            u32x4 t[kCh2];
+#pragma unroll
+            for (uint32_t k = 0; k < kCh2; ++k) {
+                const uint32_t c = lane + 64u * k;
+                if (c < nch) t[k] = __builtin_nontemporal_load(src + c);
+            }
+            // the previous set's results leave after this set's loads (vmcnt
+            // is in order: waiting for the loads does not wait for them)
+            if (sa) *pa = va;
+            if (sb) *pb = vb;
+#pragma unroll
+            for (uint32_t k = 0; k < kCh2; ++k) {
+                const uint32_t c = lane + 64u * k;
+                if (c < nch) dst[c] = t[k];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            if (sa) *pa = va;
+            if (sb) *pb = vb;
+        }
+        uint32_t h[2] = {dA ^ (kM * LA), dB ^ (kM * LB)};  // hash.rs:25 (an invalid lane: L = 0)
+        const uint32_t bA = static_cast<uint32_t>(oA & 3u), bB = static_cast<uint32_t>(oB & 3u);
+        const bool fA = staged && LA && ((bA + LA + 3) >> 2) <= kFastDw;
+        const bool fB = staged && LB && ((bB + LB + 3) >> 2) <= kFastDw;
+        if (staged) {
+            const uint32_t *const sd[2] = {stage + (fA ? ((oA - bA - lo16) >> 2) : 0u),
+                                           stage + (fB ? ((oB - bB - lo16) >> 2) : 0u)};
+            const uint32_t bs[2] = {bA, bB}, Ls[2] = {LA, LB};
+            const bool on[2] = {fA, fB};
+            chains_staged<2>(sd, bs, Ls, on, h);
+        }
+        // long keys, and every key of a set whose span the stage cannot take
+        if (LA && !fA) h[0] = key_from_mem(base, oA, LA, h[0]);
+        if (LB && !fB) h[1] = key_from_mem(base, oB, LB, h[1]);
+        pa = out + (vA ? ia : 0u);
+        pb = out + (vB ? ib : 0u);
+        va = (flags & LV_HASH_SHARD) ? (h[0] >> 28) : h[0];
+        vb = (flags & LV_HASH_SHARD) ? (h[1] >> 28) : h[1];
+        sa = vA;
+        sb = vB;
+        if (!more) {
+            if (sa) *pa = va;
+            if (sb) *pb = vb;
+            break;
+        }
+        __builtin_amdgcn_wave_barrier();  // this set's LDS reads precede the next stage
+        set = nxt;
+        ca = na;
+        cb = nb;
+    }
+}
+
 // persistent grid: 8 workgroups (32 waves) per CU at most
 uint32_t hash_grid(size_t n) {
+    constexpr uint64_t kKeysPerWg = 256u * LVK_HASH_KPL;
     static std::atomic<int> cus_cache[64];
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) cus = cus_cache[dev].load(std::memory_order_relaxed);
@@ -407,7 +561,7 @@ uint32_t hash_grid(size_t n) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
         if (dev >= 0 && dev < 64) cus_cache[dev].store(cus, std::memory_order_relaxed);
     }
-    const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * kWgsPerCu;
+    const uint64_t want = (n + kKeysPerWg - 1) / kKeysPerWg, cap = static_cast<uint64_t>(cus) * kWgsPerCu;
     return static_cast<uint32_t>(want < cap ? want : cap);
 }
 
@@ -445,7 +599,7 @@ int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const ui
     if (!d_arena || !d_off || !d_len || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
     if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
-    hipLaunchKernelGGL(lvh::hash_kernel<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
+    hipLaunchKernelGGL(LVH_HASH_KERNEL<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed}, d_out,
                        static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
@@ -463,11 +617,11 @@ int lv_hash_batch_packed(const uint8_t *d_arena, const void *d_bounds, uint32_t 
         return lvgpu_internal::set_error(LV_ERR_INVALID, "bounds must be aligned to bound_bytes");
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (bound_bytes == 4)
-        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint32_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+        hipLaunchKernelGGL(LVH_HASH_KERNEL<lvh::PackedMeta<uint32_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
                            lvh::PackedMeta<uint32_t>{static_cast<const uint32_t *>(d_bounds), d_seed}, d_out,
                            static_cast<uint32_t>(n), flags);
     else
-        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint64_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+        hipLaunchKernelGGL(LVH_HASH_KERNEL<lvh::PackedMeta<uint64_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
                            lvh::PackedMeta<uint64_t>{static_cast<const uint64_t *>(d_bounds), d_seed}, d_out,
                            static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();

@@ -1,6 +1,7 @@
 // Internal declarations shared by the product sources: the WAL scan object
 // (GPU scan + host reader) and the lv_last_error plumbing.
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <memory>
@@ -23,12 +24,14 @@ struct ScanPipe {
     std::mutex m;
     std::condition_variable cv;
     size_t ready = 0;  // chunks [0, ready) are complete (all of them once rc != 0)
+    std::atomic<size_t> ready_seen{0};  // `ready`, read without the lock (set after it)
     int rc = 0;
     std::string err;
     std::thread worker;
     bool flat = false;  // the scan's flat arrays were filled
     // 0 once chunk k is complete, or the worker's error
     int wait(size_t k) {
+        if (ready_seen.load(std::memory_order_acquire) > k) return 0;  // the Reader's per-record path
         std::unique_lock<std::mutex> lk(m);
         cv.wait(lk, [&] { return ready > k || rc != 0; });
         return ready > k ? 0 : rc;

@@ -59,6 +59,10 @@ struct StreamWs {
     std::mutex em;
     uint32_t *err = nullptr;
     uint32_t *herr = nullptr;
+    // the one-launch WAL scan's count granules (wal_pipe.hip): 1,024 {tag,
+    // count} words and a retire counter, zeroed once when made; every launch
+    // leaves them zeroed again (its last workgroup to retire clears them)
+    uint64_t *gran = nullptr;
 };
 
 struct DevCtx {
@@ -85,6 +89,10 @@ struct DevCtx {
     size_t h_stage_cap[2] = {0, 0};
     hipEvent_t ev[2] = {nullptr, nullptr};
     hipStream_t stream = nullptr;
+    // the pipelined WAL scan's second slot: a stream and a device chunk copy
+    hipStream_t stream2 = nullptr;
+    uint8_t *d_arena2 = nullptr;
+    size_t d_arena2_cap = 0;
     uint8_t *d_scr[2] = {nullptr, nullptr};  // scratch for other host paths (WAL scan)
     size_t d_scr_cap[2] = {0, 0};
     int dev = 0;
@@ -151,6 +159,8 @@ inline void set_hint(lvk::Params &P, const HintCheck *hc, uint32_t dflt_len) {
 }
 // The violation word of (device, stream), allocated and zeroed on first use.
 int stream_err(DevCtx &c, hipStream_t s, uint32_t **out);
+// The stream's WAL-scan count granules (made and zeroed on the stream once).
+int stream_gran(DevCtx &c, hipStream_t s, uint64_t **out);
 // Reads and clears the current device's violation word of stream s.
 int check_hints(hipStream_t s, uint32_t *violations);
 
@@ -175,11 +185,11 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
 // (lv_crc32c_batch_device_hint; classes.hip).
 bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus);
 // The one-launch device WAL scan (wal_pipe.hip): workspace bytes, whether a
-// log of `bytes` takes it on this device, and the launch (a memset of its
-// count granules, then wal_pipe_kernel).
+// log of `bytes` takes it on this device, and the launch (wal_pipe_kernel
+// alone: its count granules are the stream's, left zeroed by each launch).
 size_t wal_pipe_ws_bytes(uint64_t bytes, uint64_t cap);
 bool wal_pipe_applies(const DevCtx &c, uint64_t bytes);
-int launch_wal_pipe(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
+int launch_wal_pipe(DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
                     uint32_t *d_info, uint64_t cap, uint64_t *d_count, uint8_t *ws, hipStream_t s);
 // The persistent class kernel over a sorted list (classes.hip).
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s);

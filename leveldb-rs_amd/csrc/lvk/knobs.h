@@ -44,6 +44,8 @@
     defined(LVK_EXP_HASH_MUL24) || \
     defined(LVK_HASH_TAIL_READ) || \
     defined(LVK_HASH_LDS_ALL) || \
+    defined(LVK_HASH_KPL) || \
+    defined(LVK_HASH_SPAN2) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
     defined(LVK_WAL_LOCAL) || \
@@ -145,6 +147,12 @@
 #endif
 #ifndef LVK_HASH_PREFETCH_EXACT  // hash: the next set's metadata loaded by every lane (clamped), no exec mask
 #define LVK_HASH_PREFETCH_EXACT 1
+#endif
+#ifndef LVK_HASH_KPL  // hash: keys per lane (1: sets of 64 keys, 2: sets of 128, two chains interleaved)
+#define LVK_HASH_KPL 1
+#endif
+#ifndef LVK_HASH_SPAN2  // hash, two keys per lane: bytes of a wave's LDS stage
+#define LVK_HASH_SPAN2 4864
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8

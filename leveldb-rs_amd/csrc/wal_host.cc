@@ -85,17 +85,18 @@ struct lv_wal_reader {
     uint64_t end_of_buffer_offset = 0;
     uint64_t initial_offset;
     bool resyncing;
-    size_t cursor = 0;  // scan index hint (reads advance monotonically)
-    size_t pchunk = 0;  // a pipelined scan: the chunk `cursor` indexes
+    // The scan entries find() searches: the whole scan, or for a pipelined
+    // scan the chunk holding the last header asked for (log offsets [ch_lo,
+    // ch_hi)); cursor is the last entry found (reads advance monotonically,
+    // so the next header is almost always the next entry).
+    const uint64_t *ch_off = nullptr;
+    const uint32_t *ch_crc = nullptr, *ch_info = nullptr;
+    size_t ch_n = 0;
+    uint64_t ch_lo = 1, ch_hi = 0;  // (empty: the first find() selects)
+    size_t cursor = ~size_t{0};
     // info / crc of a find() result
-    uint32_t info_at(long i) const {
-        if (scan->pipe) return scan->pipe->chunks[i >> 40].info[i & ((1l << 40) - 1)];
-        return scan->info[i];
-    }
-    uint32_t crc_at(long i) const {
-        if (scan->pipe) return scan->pipe->chunks[i >> 40].crc[i & ((1l << 40) - 1)];
-        return scan->crc[i];
-    }
+    uint32_t info_at(long i) const { return ch_info[i]; }
+    uint32_t crc_at(long i) const { return ch_crc[i]; }
     bool failed = false;
     std::vector<uint8_t> scratch;
 
@@ -104,30 +105,49 @@ struct lv_wal_reader {
         if (reporter && end_of_buffer_offset >= blen + bytes + initial_offset) reporter(ctx, bytes, reason);
     }
 
-    // Scan entry for the header at log offset `hdr`, or -1.  A pipelined
-    // scan: the entry within its chunk (waiting for the chunk), as (chunk <<
-    // 40) | index, read back by entry().
-    long find(uint64_t hdr) {
-        if (scan->pipe) {  // (the chunk arrays stay valid after a flatten)
-            lvgpu_internal::ScanPipe &p = *scan->pipe;
-            const size_t k = static_cast<size_t>(hdr / p.chunk_bytes);
-            if (k >= p.chunks.size() || p.wait(k)) {
-                if (k < p.chunks.size() && p.rc) lvgpu_internal::set_error(p.rc, ("WAL scan: " + p.err).c_str());
-                return -1;
-            }
-            const auto &off = p.chunks[k].off;
-            if (k == pchunk && cursor < off.size() && off[cursor] == hdr) return static_cast<long>((k << 40) | cursor);
-            auto it = std::lower_bound(off.begin(), off.end(), hdr);
-            if (it == off.end() || *it != hdr) return -1;
-            pchunk = k;
-            cursor = static_cast<size_t>(it - off.begin());
-            return static_cast<long>((k << 40) | cursor);
+    // Makes the entries covering log offset hdr current (waiting for a
+    // pipelined scan's chunk); false if there are none.
+    bool select(uint64_t hdr) {
+        cursor = ~size_t{0};
+        if (!scan->pipe) {
+            ch_off = scan->off.data();
+            ch_crc = scan->crc.data();
+            ch_info = scan->info.data();
+            ch_n = scan->off.size();
+            ch_lo = 0;
+            ch_hi = ~uint64_t{0};
+            return true;
         }
-        const auto &off = scan->off;
-        if (cursor < off.size() && off[cursor] == hdr) return static_cast<long>(cursor);
-        auto it = std::lower_bound(off.begin(), off.end(), hdr);
-        if (it == off.end() || *it != hdr) return -1;
-        cursor = static_cast<size_t>(it - off.begin());
+        lvgpu_internal::ScanPipe &p = *scan->pipe;  // (the chunk arrays stay valid after a flatten)
+        const size_t k = static_cast<size_t>(hdr / p.chunk_bytes);
+        if (k >= p.chunks.size()) return false;
+        if (p.wait(k)) {
+            lvgpu_internal::set_error(p.rc, ("WAL scan: " + p.err).c_str());
+            return false;
+        }
+        const lvgpu_internal::ScanChunk &c = p.chunks[k];
+        ch_off = c.off.data();
+        ch_crc = c.crc.data();
+        ch_info = c.info.data();
+        ch_n = c.off.size();
+        ch_lo = k * p.chunk_bytes;
+        ch_hi = ch_lo + p.chunk_bytes;
+        return true;
+    }
+
+    // Scan entry for the header at log offset `hdr` (an index into the
+    // current entries), or -1.
+    long find(uint64_t hdr) {
+        if ((hdr < ch_lo || hdr >= ch_hi) && !select(hdr)) return -1;
+        const size_t nx = cursor + 1;  // (0 after a select)
+        if (nx < ch_n && ch_off[nx] == hdr) {
+            cursor = nx;
+            return static_cast<long>(nx);
+        }
+        if (cursor < ch_n && ch_off[cursor] == hdr) return static_cast<long>(cursor);
+        const uint64_t *it = std::lower_bound(ch_off, ch_off + ch_n, hdr);
+        if (it == ch_off + ch_n || *it != hdr) return -1;
+        cursor = static_cast<size_t>(it - ch_off);
         return static_cast<long>(cursor);
     }
 

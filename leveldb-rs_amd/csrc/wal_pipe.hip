@@ -29,8 +29,10 @@
 //   5. the waves walk that local list (classes 2, 1, 0 with G = 16, 4, 1),
 //      CRCs staged in LDS by record index, and the workgroup writes its CRCs
 //      in log order at the end.
-// No cross-workgroup data moves but the 8-B counts (one grid-wide granule
-// array, zeroed by a memset before the launch).  A per-workgroup sort of
+// No cross-workgroup data moves but the 8-B counts: one granule array per
+// stream (library-owned, zeroed once when made), which every launch leaves
+// zeroed again -- the last workgroup to finish its look-back clears it -- so
+// a call is one kernel launch and no memset.  A per-workgroup sort of
 // ~700 records keeps rounds as uniform as the global sort did (simulated:
 // 0.99 of the batch-count efficiency of the global sort).
 // LDS: the image without region B (the aligned walk's merge reads the plain
@@ -86,7 +88,7 @@ static_assert(kPStage + kPStageN == kPB + 16384, "carve-out fits region B");
 struct WalPipe {
     const uint8_t *log;
     uint64_t size, nblocks;
-    uint64_t *gran;  // one {tag 1 | count} granule per workgroup, zeroed before the launch
+    uint64_t *gran;  // one {tag 1 | count} granule per workgroup, then the retire counter (zero at launch)
     uint64_t *hc;    // header cache: kPipeCache per block (pos | len << 16 | type << 32)
     uint4 *ent;      // a dense workgroup's phase-B entries (8 B each) from its base on
     uint64_t *lst;   // phase-B entries of the other workgroups: kPipeCache per block of each
@@ -468,12 +470,27 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                     }
                     return st;
                 };
-                for (uint32_t q0 = 0; q0 < count_w; q0 += 64u) {  // wave-uniform
-                    const uint32_t q = q0 + lane;
-                    uint32_t bl = 0;
+                // record q's block (binary search of the prefix) and its
+                // cached header, requested one round of 64 records ahead so
+                // the header cache's round trip overlaps the previous round
+                struct Loc {
+                    uint32_t q, bl, k;
+                    uint64_t h;
+                };
+                auto locate = [&](uint32_t q0) {
+                    Loc x;
+                    x.q = q0 + lane;
+                    x.bl = 0;
                     for (uint32_t step = kPipeMaxBlocks / 2; step >= 1; step >>= 1)
-                        if (bl + step < nblk && g_lds[kPPre + bl + step] <= q) bl += step;
-                    const uint32_t k = q - g_lds[kPPre + bl];
+                        if (x.bl + step < nblk && g_lds[kPPre + x.bl + step] <= x.q) x.bl += step;
+                    x.k = x.q - g_lds[kPPre + x.bl];
+                    x.h = x.q < count_w && x.k - 1u < kPipeCache - 1u ? a.hc[(lo + x.bl) * kPipeCache + x.k] : 0ull;
+                    return x;
+                };
+                Loc cur = locate(0);
+                for (uint32_t q0 = 0; q0 < count_w; q0 += 64u) {  // wave-uniform
+                    const Loc nx = q0 + 64u < count_w ? locate(q0 + 64u) : cur;  // wave-uniform choice
+                    const uint32_t q = cur.q, bl = cur.bl, k = cur.k;
                     const bool rec = q < count_w && k < kPipeCache;
                     const uint64_t start = lb + static_cast<uint64_t>(bl) * kPipeBlockSize;
                     const uint32_t blen =
@@ -485,15 +502,15 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                             len = r & 0xffffu;
                             type = (r >> 16) & 0xffu;
                         } else {
-                            const uint64_t h = a.hc[(lo + bl) * kPipeCache + k];
-                            pos = static_cast<uint32_t>(h) & 0xffffu;
-                            len = static_cast<uint32_t>(h >> 16) & 0xffffu;
-                            type = static_cast<uint32_t>(h >> 32) & 0xffu;
+                            pos = static_cast<uint32_t>(cur.h) & 0xffffu;
+                            len = static_cast<uint32_t>(cur.h >> 16) & 0xffffu;
+                            type = static_cast<uint32_t>(cur.h >> 32) & 0xffu;
                         }
                     }
                     const bool firstA = k == 0 && pipe_status(len, type, blen, 0) == LV_WAL_REC_OK &&
                                         len + 1u >= kPipeAMin;  // phase A walked it
                     one(q, bl, pos, len, type, blen, rec, !firstA);
+                    cur = nx;
                 }
                 for (uint32_t b0 = 0; b0 < nblk; b0 += 64u) {  // wave-uniform
                     const uint32_t bl = b0 + lane;
@@ -559,6 +576,17 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                     total += __shfl_xor(total, k);
                 }
                 PTRACE(5);
+                // retire: every granule has been read; the last workgroup to
+                // get here clears them (and the counter) for the stream's next
+                // launch -- each workgroup published before it retired
+                uint64_t d = 0;
+                if (lane == 0)
+                    d = __hip_atomic_fetch_add(gran + 1024, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                if (__shfl(d, 0) + 1u == grid) {  // wave-uniform
+                    for (uint32_t j = lane; j < grid; j += 64u)
+                        __hip_atomic_store(gran + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) __hip_atomic_store(gran + 1024, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 const bool abort = timeout || total > a.cap;
                 if (w == 0 && lane == 0) *a.count = timeout ? ~0ull : total;
                 if (timeout && lane == 0) atomicOr(a.err, 1u);
@@ -643,18 +671,17 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
 
 namespace lvh {
 
-// The one-launch scan's workspace: the count granules (zeroed before every
-// launch), the header cache, the phase-B entries.
+// The one-launch scan's workspace: an error word, the header cache, the
+// phase-B entries (the count granules are the stream's, stream_gran).
 struct PipeWs {
-    size_t gran, hc, lst, ent, err, total;
+    size_t hc, lst, ent, err, total;
 };
 
 static PipeWs pipe_ws_layout(uint64_t nblocks, uint64_t cap) {
     PipeWs w;
-    w.gran = 0;
-    w.err = al16(1024 * sizeof(uint64_t));
-    // (LVK_WAL_PIPE_TRACE: the stamps right after the error word, at byte
-    // 8,208 of the workspace: tools/wal_pipe_trace.py reads them there)
+    w.err = 0;
+    // (LVK_WAL_PIPE_TRACE: the stamps right after the error word, at byte 16
+    // of the workspace: tools/wal_pipe_trace.py reads them there)
     w.hc = w.err + 16 + (LVK_WAL_PIPE_TRACE ? 1024 * lvk::kPipeTrace * sizeof(uint64_t) : 0);
     w.lst = w.hc + al16(nblocks * lvk::kPipeCache * sizeof(uint64_t));
     w.ent = w.lst + al16(nblocks * lvk::kPipeCache * sizeof(uint64_t));
@@ -673,7 +700,7 @@ bool wal_pipe_applies(const DevCtx &c, uint64_t bytes) {
     return LVK_WAL_LOCAL && nblocks > 0 && grid <= 1024 && (nblocks + grid - 1) / grid <= lvk::kPipeMaxBlocks;
 }
 
-int launch_wal_pipe(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
+int launch_wal_pipe(DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
                     uint32_t *d_info, uint64_t cap, uint64_t *d_count, uint8_t *ws, hipStream_t s) {
     const uint64_t nblocks = (bytes + lvk::kPipeBlockSize - 1) / lvk::kPipeBlockSize;
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(c.cus), nblocks));
@@ -682,7 +709,7 @@ int launch_wal_pipe(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint6
     a.log = d_log;
     a.size = bytes;
     a.nblocks = nblocks;
-    a.gran = reinterpret_cast<uint64_t *>(ws + lay.gran);
+    if (int rc = stream_gran(c, s, &a.gran)) return rc;
     a.hc = reinterpret_cast<uint64_t *>(ws + lay.hc);
     a.ent = reinterpret_cast<uint4 *>(ws + lay.ent);
     a.lst = reinterpret_cast<uint64_t *>(ws + lay.lst);
@@ -693,9 +720,6 @@ int launch_wal_pipe(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint6
     a.cap = cap;
     a.err = reinterpret_cast<uint32_t *>(ws + lay.err);
     a.trace = LVK_WAL_PIPE_TRACE ? reinterpret_cast<uint64_t *>(ws + lay.err + 16) : nullptr;
-    // the granules every workgroup polls start at zero in every call (a
-    // memset node under graph capture)
-    LV_HIP(hipMemsetAsync(ws + lay.gran, 0, al16(static_cast<size_t>(grid) * sizeof(uint64_t)), s));
     hipLaunchKernelGGL(lvk::wal_pipe_kernel, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);
     return 0;
 }

@@ -572,13 +572,155 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
 }
 
 // Pipelined recovery pass (VERDICT r04 missing 3): the log is scanned in
-// block-aligned chunks of kPipeChunk bytes by a worker thread -- upload, the
-// one-launch device scan, the arrays back -- while a Reader over the returned
-// scan replays chunk k on the caller's thread (records never straddle a block,
-// log_writer.rs:67-80, so a chunk's scan is exact on its own).  The Reader
-// waits only for the chunk holding the header it reaches next.
+// block-aligned chunks of kPipeChunk bytes by a worker thread while a Reader
+// over the returned scan replays chunk k on the caller's thread (records never
+// straddle a block, log_writer.rs:67-80, so a chunk's scan is exact on its
+// own).  The Reader waits only for the chunk holding the header it reaches
+// next.  The worker keeps two chunks in flight on two streams: while the GPU
+// uploads and scans chunk k, the worker copies chunk k + 1 into the other
+// pinned staging slot (a pageable log) and then collects chunk k's arrays.
 constexpr uint64_t kPipeChunk = 32ull << 20;  // 1,024 blocks
 static_assert(kPipeChunk % LV_WAL_BLOCK_SIZE == 0, "chunks are whole blocks");
+static_assert(kPipeChunk <= kStageBytes, "a chunk fits one staging slot");
+
+namespace {
+
+// One of the worker's two slots: stream, device copy of a chunk, scratch,
+// pinned staging and count word, and the chunk it holds.
+struct PipeSlot {
+    hipStream_t s = nullptr;
+    uint8_t **d_log = nullptr;
+    size_t *d_log_cap = nullptr;
+    uint8_t **scr = nullptr;
+    size_t *scr_cap = nullptr;
+    uint8_t *stage = nullptr;
+    uint64_t *hcnt = nullptr;
+    uint64_t lo = 0, len = 0, cap = 0;
+    uint64_t *d_hdr = nullptr, *d_count = nullptr;
+    uint32_t *d_crc = nullptr, *d_info = nullptr;
+};
+
+// The slot's chunk (already on the device) scanned at capacity sl.cap, the
+// count copied back to the pinned word.
+int pipe_scan(PipeSlot &sl) {
+    const size_t wsb = align16(lv_wal_scan_workspace_bytes(sl.len, sl.cap));
+    const size_t need = wsb + align16(sl.cap * 8) + 2 * align16(sl.cap * 4) + 16;
+    if (int rc = grow_dev(sl.scr, sl.scr_cap, need)) return rc;
+    uint8_t *scr = *sl.scr;
+    sl.d_hdr = reinterpret_cast<uint64_t *>(scr + wsb);
+    sl.d_crc = reinterpret_cast<uint32_t *>(scr + wsb + align16(sl.cap * 8));
+    sl.d_info = reinterpret_cast<uint32_t *>(scr + wsb + align16(sl.cap * 8) + align16(sl.cap * 4));
+    sl.d_count = reinterpret_cast<uint64_t *>(scr + need - 16);
+    if (int rc = lv_wal_scan_device(*sl.d_log, sl.len, sl.d_hdr, sl.d_crc, sl.d_info, sl.cap, sl.d_count, scr, wsb,
+                                    sl.s))
+        return rc;
+    return hip_err(hipMemcpyAsync(sl.hcnt, sl.d_count, 8, hipMemcpyDeviceToHost, sl.s), "D2H");
+}
+
+// Chunk [sl.lo, sl.lo + sl.len) onto the slot's stream: the copy (for a
+// pageable log, through the slot's pinned staging -- the CPU copy overlaps
+// the other slot's upload and scan), then the scan.
+int pipe_enqueue(PipeSlot &sl, const uint8_t *log, bool pinned) {
+    if (int rc = grow_dev(sl.d_log, sl.d_log_cap, sl.len + 16)) return rc;
+    const uint8_t *src = log + sl.lo;
+    if (!pinned) {
+        par_memcpy(sl.stage, src, sl.len);
+        src = sl.stage;
+    }
+    if (int rc = hip_err(hipMemcpyAsync(*sl.d_log, src, sl.len, hipMemcpyHostToDevice, sl.s), "H2D")) return rc;
+    if (int rc = hip_err(hipMemsetAsync(*sl.d_log + sl.len, 0, 16, sl.s), "memset")) return rc;
+    lvgpu_internal::count_h2d(sl.len);
+    return pipe_scan(sl);
+}
+
+// Waits for the slot's scan (once more at the exact count if the guess was
+// short, or if its workgroups were not co-resident), then its arrays back.
+int pipe_finish(PipeSlot &sl, lvgpu_internal::ScanChunk *out) {
+    for (int attempt = 0;; ++attempt) {
+        if (int rc = hip_err(hipStreamSynchronize(sl.s), "sync")) return rc;
+        lvgpu_internal::count_d2h(8);
+        const uint64_t count = *sl.hcnt;
+        if ((count == ~0ull || count > sl.cap) && attempt < 2) {
+            if (count != ~0ull) sl.cap = count;
+            if (int rc = pipe_scan(sl)) return rc;
+            continue;
+        }
+        if (count == ~0ull) return lvgpu_internal::set_error(LV_ERR_NO_DEVICE, "WAL scan: workgroups not co-resident");
+        if (count > sl.cap) return lvgpu_internal::set_error(LV_ERR_INVALID, "WAL scan failed");
+        out->off.resize(count);
+        out->crc.resize(count);
+        out->info.resize(count);
+        if (count) {
+            int rc;
+            if ((rc = hip_err(hipMemcpyAsync(out->off.data(), sl.d_hdr, count * 8, hipMemcpyDeviceToHost, sl.s), "D2H")) ||
+                (rc = hip_err(hipMemcpyAsync(out->crc.data(), sl.d_crc, count * 4, hipMemcpyDeviceToHost, sl.s), "D2H")) ||
+                (rc = hip_err(hipMemcpyAsync(out->info.data(), sl.d_info, count * 4, hipMemcpyDeviceToHost, sl.s),
+                              "D2H")) ||
+                (rc = hip_err(hipStreamSynchronize(sl.s), "sync")))
+                return rc;
+            lvgpu_internal::count_d2h(count * 16);
+        }
+        for (auto &o : out->off) o += sl.lo;
+        return LV_OK;
+    }
+}
+
+// The worker: every chunk of the log, two in flight, each published (in
+// order) as soon as its arrays are back.
+int pipe_run(lvgpu_internal::ScanPipe *p, const uint8_t *log, size_t bytes, int device) {
+    lvgpu_internal::DeviceGuard dg;
+    if (int rc = dg.set(device)) return rc;
+    DevCtx *c = nullptr;
+    if (int rc = current_ctx(&c)) return rc;
+    std::lock_guard<std::mutex> lk(c->host_m);  // the device's host-path buffers and streams
+    if (!c->stream) LV_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (!c->stream2) LV_HIP(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    // earlier host-path copies out of the staging slots are done
+    for (auto &ev : c->ev)
+        if (ev) LV_HIP(hipEventSynchronize(ev));
+    const bool pinned = is_pinned(log);
+    if (!pinned)
+        for (int k = 0; k < 2; ++k)
+            if (int rc = grow_pinned(&c->h_stage[k], &c->h_stage_cap[k], kStageBytes)) return rc;
+    if (int rc = grow_pinned(&c->h_meta, &c->h_meta_cap, 16)) return rc;
+    PipeSlot slot[2];
+    slot[0].s = c->stream;
+    slot[0].d_log = &c->d_arena;
+    slot[0].d_log_cap = &c->d_arena_cap;
+    slot[1].s = c->stream2;
+    slot[1].d_log = &c->d_arena2;
+    slot[1].d_log_cap = &c->d_arena2_cap;
+    for (int k = 0; k < 2; ++k) {
+        slot[k].scr = &c->d_scr[k];
+        slot[k].scr_cap = &c->d_scr_cap[k];
+        slot[k].stage = c->h_stage[k];
+        slot[k].hcnt = reinterpret_cast<uint64_t *>(c->h_meta) + k;
+    }
+    auto publish = [&](size_t k) {
+        std::lock_guard<std::mutex> g(p->m);
+        p->ready = k + 1;
+        p->ready_seen.store(k + 1, std::memory_order_release);
+        p->cv.notify_all();
+    };
+    const size_t nch = p->chunks.size();
+    int rc = LV_OK;
+    for (size_t k = 0; k < nch && !rc; ++k) {
+        PipeSlot &sl = slot[k & 1];
+        sl.lo = k * kPipeChunk;
+        sl.len = std::min<uint64_t>(kPipeChunk, bytes - sl.lo);
+        const uint64_t nblocks = (sl.len + LV_WAL_BLOCK_SIZE - 1) / LV_WAL_BLOCK_SIZE;
+        sl.cap = std::max<uint64_t>(sl.len / 256, nblocks * 8);
+        rc = pipe_enqueue(sl, log, pinned);
+        if (!rc && k > 0 && !(rc = pipe_finish(slot[(k - 1) & 1], &p->chunks[k - 1]))) publish(k - 1);
+    }
+    if (!rc && !(rc = pipe_finish(slot[(nch - 1) & 1], &p->chunks[nch - 1]))) publish(nch - 1);
+    // nothing of this scan is still reading the staging slots or scratch
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream2);
+    return rc;
+}
+
+}  // namespace
 
 extern "C" lv_wal_scan *lv_wal_scan_host_pipelined(const uint8_t *log, size_t bytes, int device) {
     if (!log && bytes) {
@@ -595,19 +737,13 @@ extern "C" lv_wal_scan *lv_wal_scan_host_pipelined(const uint8_t *log, size_t by
         p->flat = true;
         return scan;
     }
-    p->worker = std::thread([p, log, bytes, device, nch] {
-        for (size_t k = 0; k < nch; ++k) {
-            const uint64_t lo = k * kPipeChunk, len = std::min<uint64_t>(kPipeChunk, bytes - lo);
-            const int rc = lvgpu_internal::scan_host_range(log + lo, len, lo, device, &p->chunks[k]);
+    p->worker = std::thread([p, log, bytes, device] {
+        const int rc = pipe_run(p, log, bytes, device);
+        if (rc) {
             std::lock_guard<std::mutex> lk(p->m);
-            if (rc) {
-                p->rc = rc;
-                p->err = lv_last_error();
-            } else {
-                p->ready = k + 1;
-            }
+            p->rc = rc;
+            p->err = lv_last_error();
             p->cv.notify_all();
-            if (rc) return;
         }
     });
     return scan;

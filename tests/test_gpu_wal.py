@@ -102,7 +102,7 @@ def test_pipelined_scan_reader_over_chunks(gpu):
     same way by both scans' readers."""
     import lvgpu.wal as LW
     rng = np.random.default_rng(41)
-    recs = _random_records(rng, 20000, maxlog=14)
+    recs = _random_records(rng, 24000, maxlog=16)
     log = LW.encode(recs)
     assert len(log) > 2 * (32 << 20)
     rep = W.ReportCollector()

@@ -50,6 +50,23 @@ double lv_replay_recover(const uint8_t *log, size_t bytes, int device, int reps,
     return best;
 }
 
+/* The pipelined scan alone: lv_wal_scan_host_pipelined, lv_wal_scan_wait,
+ * lv_wal_scan_free; best of `reps` (-1.0 on an error). */
+double lv_replay_scan_pipelined(const uint8_t *log, size_t bytes, int device, int reps) {
+    double best = -1.0;
+    for (int r = 0; r < reps; ++r) {
+        const double t0 = now_s();
+        lv_wal_scan *scan = lv_wal_scan_host_pipelined(log, bytes, device);
+        if (!scan) return -1.0;
+        const int rc = lv_wal_scan_wait(scan);
+        lv_wal_scan_free(scan);
+        const double el = now_s() - t0;
+        if (rc) return -1.0;
+        if (best < 0 || el < best) best = el;
+    }
+    return best;
+}
+
 /* Replays the whole log `reps` times; returns the best pass in seconds and
  * the records / payload bytes of one pass (-1.0 on a reader error). */
 double lv_replay_reader(const uint8_t *log, size_t bytes, const lv_wal_scan *scan, int reps, uint64_t *records,

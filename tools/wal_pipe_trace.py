@@ -46,13 +46,13 @@ _, _, _, count = LW.scan_device(d_log, 0)
 torch.cuda.synchronize()
 cap = int(count.item())
 ws = torch.zeros(LW.scan_workspace_bytes(log.size, cap), dtype=torch.uint8, device="cuda:0")
-assert ws.numel() >= 8208 + 1024 * KT * 8
+assert ws.numel() >= 16 + 1024 * KT * 8
 runs = []
 for rep in range(int(sys.argv[1]) if len(sys.argv) > 1 else 5):
     hdr, crc, info, cnt = LW.scan_device(d_log, cap, workspace=ws)
     torch.cuda.synchronize()
     assert int(cnt.item()) == cap
-    tr = ws[8208:8208 + 1024 * KT * 8].cpu().numpy().view(np.uint64).reshape(1024, KT).astype(np.int64)
+    tr = ws[16:16 + 1024 * KT * 8].cpu().numpy().view(np.uint64).reshape(1024, KT).astype(np.int64)
     grid = int((tr[:, 0] != 0).sum())
     tr = tr[:grid]
     t0 = tr[:, 0].min()
@@ -67,5 +67,9 @@ for rep in range(int(sys.argv[1]) if len(sys.argv) > 1 else 5):
                  "phaseA_done_first_wave": pct(us[:, 8:24].min(1)), "phaseA_done_last_wave": pct(us[:, 8:24].max(1)),
                  "ready_seen_last_wave": pct(us[:, 24:40].max(1)),
                  "walk_done_first_wave": pct(us[:, 40:56].min(1)), "walk_done_last_wave": pct(us[:, 40:56].max(1)),
-                 "end": pct(us[:, 56])})
+                 "end": pct(us[:, 56]),
+                 # wave time lost per workgroup, as a fraction of its waves x its end:
+                 # waiting for the phase-B list after phase A, and idle after the walk
+                 "idle_wait_list": pct(np.clip(us[:, 24:40] - us[:, 8:24], 0, None).sum(1) / (16 * us[:, 56])),
+                 "idle_after_walk": pct((us[:, 56:57] - us[:, 40:56]).sum(1) / (16 * us[:, 56]))})
 print(json.dumps(runs[-1], indent=1))
