@@ -860,6 +860,77 @@ def table_cpu_baseline(f, offs, sizes, unit_bytes, seconds):
     return {"verify": v, "seal": s}
 
 
+# VALU issue of the hash kernels: a wave64 VALU
+# instruction occupies its SIMD's issue slot for 4 cycles; MI355X has 256 CUs
+# x 4 SIMDs at up to 2.4 GHz (MI355X_MICROARCH.md).  SQ_INSTS_VALU counts
+# wave-level VALU instructions; SQ_VALU_SCALE converts the counter to them on
+# this part (tools/pmc_calib.hip: a kernel of known VALU count,
+# profiles/r05/valu/).
+VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4
+SQ_VALU_SCALE = 1.0
+
+
+def measure_hash_valu(args):
+    """Child process: rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES over a short hash
+    run (kernel counters only).  Returns {kernel api: VALU instructions per
+    launch} or (None, reason)."""
+    import collections
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return None, "skipped (running under rocprofv3)"
+    out = tempfile.mkdtemp(prefix="lvgpu_valu_", dir="/tmp")
+    cmd = [exe, "--pmc", "SQ_INSTS_VALU", "SQ_WAVES", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+           sys.executable, os.path.abspath(__file__), "--hash", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0",
+           "--traffic", "off"]
+    if args.blocks:
+        cmd += ["--blocks", str(args.blocks)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       timeout=300, check=True)
+    except Exception as e:  # noqa: BLE001 - report, never fail the bench on the profiler
+        return None, f"rocprofv3 pass failed: {e}"
+    per = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "")
+                if "hash_kernel" in name and row.get("Counter_Name") == "SQ_INSTS_VALU":
+                    api = "packed_u32" if "unsigned int" in name else "packed_u64" if "unsigned long" in name \
+                        else "offsets"
+                    per[api].append(float(row["Counter_Value"]))
+    shutil.rmtree(out, ignore_errors=True)
+    if not per:
+        return None, "no hash_kernel counters in the pass"
+    return {k: SQ_VALU_SCALE * sum(v) / len(v) for k, v in per.items()}, \
+        "rocprofv3 --pmc SQ_INSTS_VALU (its own pass), mean per launch"
+
+
+def hash_rooflines(key_bytes, ms, valu_instr):
+    """The hash line's two bounds: key bytes over HBM and VALU
+    issue (instructions x 4 cycles over 1,024 SIMDs at 2.4 GHz); `roofline`
+    is the one closer to its peak."""
+    g = key_bytes / (ms * 1e-3) / 1e9
+    hbm = {"bound": "hbm", "achieved": round(g, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(g / HBM_PEAK_GBS, 4), "bytes_per_launch": key_bytes,
+           "algorithmic_bytes": "key bytes only (SURVEY 8d: metadata reported alongside, not counted)"}
+    if valu_instr is None:
+        return hbm, hbm, None
+    peak_ips = VALU_SIMDS * VALU_CLOCK_HZ / VALU_CYCLES  # wave-level VALU instructions per second
+    ips = valu_instr / (ms * 1e-3)
+    valu = {"bound": "valu", "achieved": round(ips / 1e12, 4), "peak": round(peak_ips / 1e12, 4),
+            "unit": "T wave-VALU instr/s", "frac": round(ips / peak_ips, 4),
+            "instr_per_launch": round(valu_instr), "cycles_per_instr": VALU_CYCLES}
+    return (valu if valu["frac"] > hbm["frac"] else hbm), hbm, valu
+
+
 def hash_cpu_baseline(arena, offs, lens, seconds):
     """hash.rs:20-51 per key on one host core (oracle_hash_batch) over the
     same byte-packed keys copied to host memory, in G keys/s."""
@@ -932,14 +1003,10 @@ def hash_bench(args):
         torch.cuda.synchronize()
         if not variant and not np.array_equal(out[:k].cpu().numpy().view(np.uint32), want):
             raise SystemExit(f"hash bench parity check failed (packed, {width}-byte bounds)")
-        g = total / (pavg * 1e-3) / 1e9
         mv = total + (width + 4) * n
         packed[f"packed_u{8 * width}"] = {
             "api": f"lv_hash_batch_packed, {width}-byte bounds", "value": round(n / (pavg * 1e-3) / 1e9, 3),
-            "unit": "Gkeys/s", "ms_avg": round(pavg, 4), "ms_p50": round(pp50, 4),
-            "roofline": {"bound": "hbm", "achieved": round(g, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(g / HBM_PEAK_GBS, 4), "bytes_per_launch": total,
-                         "algorithmic_bytes": "key bytes only"},
+            "unit": "Gkeys/s", "ms_avg": round(pavg, 4), "ms_p50": round(pp50, 4), "_ms": pavg,
             "with_metadata": {"bytes_per_launch": mv, "frac_of_8TBps": round(mv / (pavg * 1e-3) / 8e12, 4),
                               "note": f"key bytes + {width} B bound read + 4 B output written per key"}}
         del b
@@ -953,14 +1020,20 @@ def hash_bench(args):
         raise SystemExit("hash bench parity check failed (all keys)")
     del host_all
     cpu = hash_cpu_baseline(arena, offs, lens, args.cpu_seconds) if args.cpu_seconds > 0 else None
+    del arena, o, ln, out
+    torch.cuda.empty_cache()
+    # the VALU side (its own rocprofv3 pass, after this process's timed runs)
+    valu, valu_note = measure_hash_valu(args) if args.traffic != "off" else (None, "skipped (--traffic off)")
+    vget = (lambda k: valu.get(k)) if isinstance(valu, dict) else (lambda k: None)
+    for k, rec in packed.items():
+        rec["roofline"], rec["roofline_hbm"], rec["roofline_valu"] = hash_rooflines(total, rec.pop("_ms"), vget(k))
     moved = total + 16 * n  # key bytes + off/len + out
-    key_gbs = total / (avg * 1e-3) / 1e9
+    roof, roof_hbm, roof_valu = hash_rooflines(total, avg, vget("offsets"))
     res = {"metric": "batched leveldb hash() + cache shard, device-resident", "unit": "Gkeys/s",
            "keys": n, "key_bytes": total, "value": round(n / (avg * 1e-3) / 1e9, 3), "ms_avg": round(avg, 4),
            "ms_p50": round(p50, 4),
-           "roofline": {"bound": "hbm", "achieved": round(key_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(key_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": total,
-                        "algorithmic_bytes": "key bytes only (SURVEY 8d: metadata reported alongside, not counted)"},
+           "roofline": roof, "roofline_hbm": roof_hbm, "roofline_valu": roof_valu,
+           "valu_source": valu_note if isinstance(valu, dict) else f"none: {valu_note}",
            "with_metadata": {"bytes_per_launch": moved, "GB_per_s": round(moved / (avg * 1e-3) / 1e9, 1),
                              "frac_of_8TBps": round(moved / (avg * 1e-3) / 8e12, 4),
                              "note": "key bytes + 8 B offset + 4 B length read + 4 B output written per key"},
@@ -1040,6 +1113,10 @@ def wal_bench(args):
     assert nrec == sizes.size, (nrec, sizes.size)
     # the same Reader loop as a native caller runs it: lv_wal_reader_read_record
     # in one C loop (tools/host_replay.c), no per-record FFI hop
+    if lvgpu.experiment_variant() and os.environ.get("LVGPU_LIB"):
+        # a timing variant: its lv_* symbols first in the global scope, so the
+        # replay helper (linked against the product library) binds to them
+        ctypes.CDLL(os.environ["LVGPU_LIB"], mode=os.RTLD_GLOBAL | os.RTLD_NOW)
     R = ctypes.CDLL(os.path.join(ROOT, "leveldb-rs_amd", "lib", "libhostreplay.so"))
     R.lv_replay_reader.restype = ctypes.c_double
     R.lv_replay_reader.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int,

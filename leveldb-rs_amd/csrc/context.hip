@@ -133,7 +133,7 @@ bool is_pinned(const void *p) {
 // memcpy split over up to 8 host threads (pageable -> pinned staging).
 void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes) {
     unsigned nt = std::thread::hardware_concurrency();
-    nt = nt == 0 ? 1 : (nt > 8 ? 8 : nt);
+    nt = nt == 0 ? 1 : (nt > LVK_MEMCPY_THREADS ? LVK_MEMCPY_THREADS : nt);
     if (bytes < (4u << 20) || nt == 1) {
         std::memcpy(dst, src, bytes);
         return;
@@ -249,7 +249,7 @@ int stream_gran(DevCtx &c, hipStream_t s, uint64_t **out) {
     StreamWs *w = find_ws(c, s, true);
     std::lock_guard<std::mutex> lk(w->em);
     if (!w->gran) {
-        constexpr size_t kBytes = (1024 + 2) * sizeof(uint64_t);
+        constexpr size_t kBytes = kWalSyncWords * sizeof(uint64_t);
         LV_HIP(hipMalloc(&w->gran, kBytes));
         counters().allocs++;
         LV_HIP(hipMemsetAsync(w->gran, 0, kBytes, s));

@@ -54,8 +54,8 @@
 #include "lv_internal.h"
 #include "lvk/knobs.h"
 
-#if LVK_HASH_KPL == 2
-#define LVH_HASH_KERNEL lvh::hash_kernel2
+#if LVK_HASH_GLDS2
+#define LVH_HASH_KERNEL lvh::hash_kernel_g2
 #else
 #define LVH_HASH_KERNEL lvh::hash_kernel
 #endif
@@ -416,144 +416,142 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     }
 }
 
-// ---- two keys per lane (LVK_HASH_KPL == 2) ----
-// A wave hashes sets of 128 keys: lane l owns keys 128 s + l and 128 s + 64 +
-// l, both halves' metadata requested one set ahead (every lane, clamped), the
-// set's span staged through LDS once, and the two keys' chains run in one
-// loop so their exec-mask steps and the per-set wave work (span, ballots,
-// staging, stores) are paid once per 128 keys instead of per 64.  A stage of
-// kSpan2 bytes per wave (LDS: 4 x (kSpan2 + 80) B per workgroup).
-constexpr uint32_t kSpan2 = LVK_HASH_SPAN2;
-constexpr uint32_t kCh2 = (kSpan2 / 16 + 63) / 64;
-static_assert(kSpan2 % 16 == 0, "stage of whole granules");
+// ---- LDS-DMA prefetch in issue order (LVK_HASH_GLDS2) ----
+// Round 4's LDS-DMA kernel (the next set's span requested by
+// global_load_lds_dwordx4 into a second stage while this set hashes) was
+// slower, 145 -> 172 us: its ISA shows a vmcnt(0) right after the next
+// span's DMA (before the metadata load that followed it), so every set still
+// waited for a full round trip.  Here a set's memory operations are all
+// issued before its chains run: (0) one vmcnt(0) -- this set's DMA, the next
+// set's metadata and the previous set's store, all issued a set ago (the
+// compiler does not order LDS-DMA before ds_read itself), (1) its key window
+// and tail dwords read from its stage, the previous set's results stored,
+// (2) the next set's geometry, its successor's metadata requested, the next
+// span's DMA into the other stage, (3) the chains from registers.  Stages of kGStage bytes
+// (64 keys of <= ~39 B on average); a set whose span does not fit, or whose
+// keys are out of order, reads its keys from memory.  LDS: 4 waves x 2 x
+// (2,560 + 80) B per workgroup, 7 workgroups per CU.
+constexpr uint32_t kGStage = 2560;
+constexpr uint32_t kGStageWords = kGStage / 4 + kSpanPad;
 
-// hash.rs:25-48 for K keys whose windows (<= kFastDw dwords from the key's
-// aligned-down start) lie in LDS at sd[k]; on[k] false leaves h[k] alone.
-template <uint32_t K>
-__device__ __forceinline__ void chains_staged(const uint32_t *const (&sd)[K], const uint32_t (&bs)[K],
-                                              const uint32_t (&L)[K], const bool (&on)[K], uint32_t (&h)[K]) {
-    uint32_t w[K][kFastDw + 1];
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+struct GSpan {
+    uint64_t lo16;
+    uint32_t nch;
+    bool staged;
+};
+
+__device__ __forceinline__ GSpan gspan_of(bool valid, uint64_t o, uint32_t L) {
+    const uint64_t act = __ballot(valid);
+    const int last = act ? 63 - __builtin_clzll(act) : 0;
+    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
+    GSpan g;
+    g.lo16 = lo & ~15ull;
+    const bool inside = !L || (o >= lo && o + L <= hi);
+    g.staged = act && hi > lo && hi - g.lo16 <= kGStage && __all(inside);  // wave-uniform
+    g.nch = g.staged ? static_cast<uint32_t>((hi - g.lo16 + 15) >> 4) : 0u;
+    return g;
+}
+
+// The span's granules into `stage` (granule c at byte 16 c): up to three
+// 1-KiB LDS-DMA instructions, lanes past the span masked off.
+__device__ __forceinline__ void gspan_issue(const uint8_t *__restrict__ base, const GSpan &g, uint32_t *stage,
+                                            uint32_t lane) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(base + g.lo16);
 #pragma unroll
-    for (uint32_t k = 0; k < K; ++k) {
-#pragma unroll
-        for (uint32_t j = 0; j < kFastDw; ++j) w[k][j] = sd[k][j];  // the stage's pad keeps every window inside it
-        w[k][kFastDw] = 0u;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kFastDw; ++j) {
-#pragma unroll
-        for (uint32_t k = 0; k < K; ++k)
-            if (on[k] && j < (L[k] >> 2)) h[k] = mix(h[k], funnel(w[k][j + 1], w[k][j], bs[k]));
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < K; ++k) {
-        const uint32_t nw = L[k] >> 2, diff = L[k] & 3u;  // hash.rs:38-48: the tail word re-read
-        if (on[k] && diff) {
-            const uint32_t ndw = (bs[k] + L[k] + 3) >> 2;
-            const uint32_t tw = funnel(nw + 1 < ndw ? sd[k][nw + 1] : 0u, sd[k][nw], bs[k]);
-            uint32_t x = h[k];
-            if (diff >= 3) x += ((tw >> 16) & 0xffu) << 16;
-            if (diff >= 2) x += ((tw >> 8) & 0xffu) << 8;
-            x += tw & 0xffu;
-            x *= kM;
-            h[k] = x ^ (x >> 24);
+    for (uint32_t k = 0; k < (kGStage + 1023) / 1024; ++k) {
+        if (64u * k < g.nch) {  // wave-uniform
+            const uint32_t c = lane + 64u * k;
+            if (c < g.nch)
+                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + c), (lds_void_t *)(stage + 256u * k), 16, 0, 0);
         }
     }
 }
 
 template <typename Meta>
-__global__ void __launch_bounds__(256) hash_kernel2(const uint8_t *__restrict__ base, Meta meta,
-                                                    uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
-    __shared__ __attribute__((aligned(16))) uint32_t span[4][kSpan2 / 4 + kSpanPad];
+__global__ void __launch_bounds__(256, 7) hash_kernel_g2(const uint8_t *__restrict__ base, Meta meta,
+                                                     uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[4][2][kGStageWords];
     const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
     uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
-    if (set * 128u >= n) return;  // wave-uniform
-    uint32_t *stage = span[wv];
-    MetaRaw ca = meta.load(set * 128u + lane, n, lane), cb = meta.load(set * 128u + 64u + lane, n, lane);
-    uint32_t *pa = out, *pb = out, va = 0, vb = 0;  // the previous set's results, stored one set late
-    bool sa = false, sb = false;
-    for (;;) {
-        const uint64_t nxt = set + W;
-        const bool more = nxt * 128u < n;  // wave-uniform
-        const MetaRaw na = meta.load(nxt * 128u + lane, n, lane), nb = meta.load(nxt * 128u + 64u + lane, n, lane);
-        const uint64_t ia = set * 128u + lane, ib = ia + 64u;
-        const bool vA = ia < n, vB = ib < n;
-        uint64_t oA, oB;
-        uint32_t LA, LB, dA, dB;
-        meta.get(ca, ia, n, lane, oA, LA, dA);
-        meta.get(cb, ib, n, lane, oB, LB, dB);
-        // candidate span: A's first key to the last valid key's end; staged
-        // only if every key lies inside it (keys packed in order)
-        const uint64_t actB = __ballot(vB), actA = __ballot(vA);
-        const uint64_t lo = __shfl(oA, 0);
-        const uint64_t hi = actB ? __shfl(oB + LB, 63 - __builtin_clzll(actB))
-                                 : __shfl(oA + LA, 63 - __builtin_clzll(actA));
-        const uint64_t lo16 = lo & ~15ull;
-        const bool inside = (!LA || (oA >= lo && oA + LA <= hi)) && (!LB || (oB >= lo && oB + LB <= hi));
-        const bool staged = hi > lo && hi - lo16 <= kSpan2 && __all(inside);  // wave-uniform
-        if (staged) {
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
-            const u32x4 *src = reinterpret_cast<const u32x4 *>(base + lo16);
-            u32x4 *dst = reinterpret_cast<u32x4 *>(stage);
-            u32x4 t[kCh2];
+    if (set * 64u >= n) return;  // wave-uniform
+    // prologue: the first set's metadata and span, the second's metadata
+    uint64_t o;
+    uint32_t L, sd;
+    meta.get(meta.load(set * 64u + lane, n, lane), set * 64u + lane, n, lane, o, L, sd);
+    GSpan g = gspan_of(set * 64u + lane < n, o, L);
+    if (g.staged) gspan_issue(base, g, stage[wv][0], lane);
+    MetaRaw nx = meta.load((set + W) * 64u + lane, n, lane);  // (clamped)
+    uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late
+    bool pst = false;
+    for (uint32_t k = 0;; ++k) {
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): expcnt / lgkmcnt untouched
+        const uint64_t i = set * 64u + lane;
+        const bool valid = i < n;
+        const uint32_t bs = static_cast<uint32_t>(o & 3u), nw = L >> 2, diff = L & 3u;
+        const bool fast = g.staged && valid && L && ((bs + L + 3) >> 2) <= kFastDw;
+        // 1. this set's window and tail dwords from its stage
+        uint32_t w[kFastDw + 1];
+        uint32_t t0 = 0, t1 = 0;
+        if (g.staged) {  // wave-uniform
+            const uint32_t *sp = stage[wv][k & 1u] + (fast ? ((o - bs - g.lo16) >> 2) : 0u);
 #pragma unroll
-            for (uint32_t k = 0; k < kCh2; ++k) {
-                const uint32_t c = lane + 64u * k;
-                if (c < nch) t[k] = __builtin_nontemporal_load(src + c);
-            }
-            // the previous set's results leave after this set's loads (vmcnt
-            // is in order: waiting for the loads does not wait for them)
-            if (sa) *pa = va;
-            if (sb) *pb = vb;
+            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = sp[j];  // (the stage's pad keeps the window inside)
+            t0 = sp[nw];
+            t1 = sp[nw + 1u];
+        }
+        w[kFastDw] = 0u;
+        if (pst) *pout = pval;
+        // 2. the next set: geometry, its successor's metadata, its span's DMA
+        const uint64_t nset = set + W;
+        const bool more = nset * 64u < n;  // wave-uniform
+        uint64_t on = 0;
+        uint32_t Ln = 0, sdn = 0;
+        GSpan gn{};
+        if (more) {
+            meta.get(nx, nset * 64u + lane, n, lane, on, Ln, sdn);
+            gn = gspan_of(nset * 64u + lane < n, on, Ln);
+        }
+        nx = meta.load((nset + W) * 64u + lane, n, lane);  // (clamped)
+        if (more && gn.staged) gspan_issue(base, gn, stage[wv][(k + 1u) & 1u], lane);
+        // 3. this set's hashes from registers (hash.rs:25-48)
+        uint32_t h = sd ^ (kM * L);
+        if (fast) {
 #pragma unroll
-            for (uint32_t k = 0; k < kCh2; ++k) {
-                const uint32_t c = lane + 64u * k;
-                if (c < nch) dst[c] = t[k];
+            for (uint32_t j = 0; j < kFastDw; ++j)
+                if (j < nw) h = mix(h, funnel(w[j + 1], w[j], bs));
+            if (diff) {
+                const uint32_t ndw = (bs + L + 3) >> 2;
+                const uint32_t tw = funnel(nw + 1 < ndw ? t1 : 0u, t0, bs);
+                if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
+                if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;
+                h += tw & 0xffu;
+                h *= kM;
+                h ^= h >> 24;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else {
-            if (sa) *pa = va;
-            if (sb) *pb = vb;
+        } else if (valid && L) {
+            h = key_from_mem(base, o, L, h);
         }
-        uint32_t h[2] = {dA ^ (kM * LA), dB ^ (kM * LB)};  // hash.rs:25 (an invalid lane: L = 0)
-        const uint32_t bA = static_cast<uint32_t>(oA & 3u), bB = static_cast<uint32_t>(oB & 3u);
-        const bool fA = staged && LA && ((bA + LA + 3) >> 2) <= kFastDw;
-        const bool fB = staged && LB && ((bB + LB + 3) >> 2) <= kFastDw;
-        if (staged) {
-            const uint32_t *const sd[2] = {stage + (fA ? ((oA - bA - lo16) >> 2) : 0u),
-                                           stage + (fB ? ((oB - bB - lo16) >> 2) : 0u)};
-            const uint32_t bs[2] = {bA, bB}, Ls[2] = {LA, LB};
-            const bool on[2] = {fA, fB};
-            chains_staged<2>(sd, bs, Ls, on, h);
-        }
-        // long keys, and every key of a set whose span the stage cannot take
-        if (LA && !fA) h[0] = key_from_mem(base, oA, LA, h[0]);
-        if (LB && !fB) h[1] = key_from_mem(base, oB, LB, h[1]);
-        pa = out + (vA ? ia : 0u);
-        pb = out + (vB ? ib : 0u);
-        va = (flags & LV_HASH_SHARD) ? (h[0] >> 28) : h[0];
-        vb = (flags & LV_HASH_SHARD) ? (h[1] >> 28) : h[1];
-        sa = vA;
-        sb = vB;
+        pout = out + (valid ? i : 0u);
+        pval = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
+        pst = valid;
         if (!more) {
-            if (sa) *pa = va;
-            if (sb) *pb = vb;
+            if (pst) *pout = pval;
             break;
         }
-        __builtin_amdgcn_wave_barrier();  // this set's LDS reads precede the next stage
-        set = nxt;
-        ca = na;
-        cb = nb;
+        set = nset;
+        o = on;
+        L = Ln;
+        sd = sdn;
+        g = gn;
     }
 }
 
 // persistent grid: 8 workgroups (32 waves) per CU at most
 uint32_t hash_grid(size_t n) {
-    constexpr uint64_t kKeysPerWg = 256u * LVK_HASH_KPL;
     static std::atomic<int> cus_cache[64];
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) cus = cus_cache[dev].load(std::memory_order_relaxed);
@@ -561,7 +559,7 @@ uint32_t hash_grid(size_t n) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
         if (dev >= 0 && dev < 64) cus_cache[dev].store(cus, std::memory_order_relaxed);
     }
-    const uint64_t want = (n + kKeysPerWg - 1) / kKeysPerWg, cap = static_cast<uint64_t>(cus) * kWgsPerCu;
+    const uint64_t want = (n + 255) / 256, cap = static_cast<uint64_t>(cus) * kWgsPerCu;
     return static_cast<uint32_t>(want < cap ? want : cap);
 }
 

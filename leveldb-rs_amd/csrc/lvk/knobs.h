@@ -44,8 +44,9 @@
     defined(LVK_EXP_HASH_MUL24) || \
     defined(LVK_HASH_TAIL_READ) || \
     defined(LVK_HASH_LDS_ALL) || \
-    defined(LVK_HASH_KPL) || \
-    defined(LVK_HASH_SPAN2) || \
+    defined(LVK_HASH_GLDS2) || \
+    defined(LVK_PIPE_CHUNK_MB) || \
+    defined(LVK_MEMCPY_THREADS) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
     defined(LVK_WAL_LOCAL) || \
@@ -148,11 +149,14 @@
 #ifndef LVK_HASH_PREFETCH_EXACT  // hash: the next set's metadata loaded by every lane (clamped), no exec mask
 #define LVK_HASH_PREFETCH_EXACT 1
 #endif
-#ifndef LVK_HASH_KPL  // hash: keys per lane (1: sets of 64 keys, 2: sets of 128, two chains interleaved)
-#define LVK_HASH_KPL 1
+#ifndef LVK_PIPE_CHUNK_MB  // host: chunk of the pipelined WAL scan (MiB, block multiple)
+#define LVK_PIPE_CHUNK_MB 32
 #endif
-#ifndef LVK_HASH_SPAN2  // hash, two keys per lane: bytes of a wave's LDS stage
-#define LVK_HASH_SPAN2 4864
+#ifndef LVK_MEMCPY_THREADS  // host: threads of the pageable -> pinned staging copy
+#define LVK_MEMCPY_THREADS 8
+#endif
+#ifndef LVK_HASH_GLDS2  // hash: the next set's span prefetched by LDS-DMA, in issue order (7 workgroups per CU)
+#define LVK_HASH_GLDS2 0
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8

@@ -579,7 +579,7 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
 // next.  The worker keeps two chunks in flight on two streams: while the GPU
 // uploads and scans chunk k, the worker copies chunk k + 1 into the other
 // pinned staging slot (a pageable log) and then collects chunk k's arrays.
-constexpr uint64_t kPipeChunk = 32ull << 20;  // 1,024 blocks
+constexpr uint64_t kPipeChunk = static_cast<uint64_t>(LVK_PIPE_CHUNK_MB) << 20;  // 32 MiB: 1,024 blocks
 static_assert(kPipeChunk % LV_WAL_BLOCK_SIZE == 0, "chunks are whole blocks");
 static_assert(kPipeChunk <= kStageBytes, "a chunk fits one staging slot");
 
