@@ -860,13 +860,14 @@ def table_cpu_baseline(f, offs, sizes, unit_bytes, seconds):
     return {"verify": v, "seal": s}
 
 
-# VALU issue of the hash kernels: a wave64 VALU
-# instruction occupies its SIMD's issue slot for 4 cycles; MI355X has 256 CUs
-# x 4 SIMDs at up to 2.4 GHz (MI355X_MICROARCH.md).  SQ_INSTS_VALU counts
-# wave-level VALU instructions; SQ_VALU_SCALE converts the counter to them on
-# this part (tools/pmc_calib.hip: a kernel of known VALU count,
-# profiles/r05/valu/).
-VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 4
+# VALU issue of the hash kernels.  MI355X: 256 CUs x 4
+# SIMDs at up to 2.4 GHz (MI355X_MICROARCH.md).  Measured on this part
+# (tools/pmc_calib.hip, profiles/r05/valu/): SQ_INSTS_VALU is the exact
+# whole-GPU count of wave-level VALU instructions, and a dependent stream of
+# simple 32-bit wave64 ops issues one per 2.44 SIMD cycles at the 2.4 GHz
+# clock (v_mul_lo_u32: 4.56) -- so the VALU peak is 1,024 x 2.4e9 / 2.44
+# wave instructions per second, every instruction priced as a simple op.
+VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2.44
 SQ_VALU_SCALE = 1.0
 
 
@@ -913,14 +914,17 @@ def measure_hash_valu(args):
         "rocprofv3 --pmc SQ_INSTS_VALU (its own pass), mean per launch"
 
 
-def hash_rooflines(key_bytes, ms, valu_instr):
-    """The hash line's two bounds: key bytes over HBM and VALU
-    issue (instructions x 4 cycles over 1,024 SIMDs at 2.4 GHz); `roofline`
-    is the one closer to its peak."""
+def hash_rooflines(key_bytes, ms, valu_instr, moved_bytes):
+    """The hash line's two bounds: HBM -- `frac` by key bytes,
+    `frac_all_bytes` by every byte the API moves (keys, metadata, output) --
+    and VALU issue (instructions x 2.44 cycles over 1,024 SIMDs at 2.4 GHz).
+    `roofline` is the one closer to its peak, HBM by all bytes against VALU."""
     g = key_bytes / (ms * 1e-3) / 1e9
+    ga = moved_bytes / (ms * 1e-3) / 1e9
     hbm = {"bound": "hbm", "achieved": round(g, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(g / HBM_PEAK_GBS, 4), "bytes_per_launch": key_bytes,
-           "algorithmic_bytes": "key bytes only (SURVEY 8d: metadata reported alongside, not counted)"}
+           "algorithmic_bytes": "key bytes only (SURVEY 8d)",
+           "frac_all_bytes": round(ga / HBM_PEAK_GBS, 4), "all_bytes_per_launch": moved_bytes}
     if valu_instr is None:
         return hbm, hbm, None
     peak_ips = VALU_SIMDS * VALU_CLOCK_HZ / VALU_CYCLES  # wave-level VALU instructions per second
@@ -928,7 +932,7 @@ def hash_rooflines(key_bytes, ms, valu_instr):
     valu = {"bound": "valu", "achieved": round(ips / 1e12, 4), "peak": round(peak_ips / 1e12, 4),
             "unit": "T wave-VALU instr/s", "frac": round(ips / peak_ips, 4),
             "instr_per_launch": round(valu_instr), "cycles_per_instr": VALU_CYCLES}
-    return (valu if valu["frac"] > hbm["frac"] else hbm), hbm, valu
+    return (valu if valu["frac"] > hbm["frac_all_bytes"] else hbm), hbm, valu
 
 
 def hash_cpu_baseline(arena, offs, lens, seconds):
@@ -1026,9 +1030,10 @@ def hash_bench(args):
     valu, valu_note = measure_hash_valu(args) if args.traffic != "off" else (None, "skipped (--traffic off)")
     vget = (lambda k: valu.get(k)) if isinstance(valu, dict) else (lambda k: None)
     for k, rec in packed.items():
-        rec["roofline"], rec["roofline_hbm"], rec["roofline_valu"] = hash_rooflines(total, rec.pop("_ms"), vget(k))
+        rec["roofline"], rec["roofline_hbm"], rec["roofline_valu"] = hash_rooflines(
+            total, rec.pop("_ms"), vget(k), rec["with_metadata"]["bytes_per_launch"])
     moved = total + 16 * n  # key bytes + off/len + out
-    roof, roof_hbm, roof_valu = hash_rooflines(total, avg, vget("offsets"))
+    roof, roof_hbm, roof_valu = hash_rooflines(total, avg, vget("offsets"), moved)
     res = {"metric": "batched leveldb hash() + cache shard, device-resident", "unit": "Gkeys/s",
            "keys": n, "key_bytes": total, "value": round(n / (avg * 1e-3) / 1e9, 3), "ms_avg": round(avg, 4),
            "ms_p50": round(p50, 4),

@@ -44,6 +44,16 @@
 // two-deep form -- the next set's span in flight in registers while this
 // set hashes from LDS, metadata two sets ahead, 64 VGPRs at 8 waves/SIMD --
 // measured 106 vs 117 G keys/s, three interleaved reps: not kept.)
+// Round 5 (profiles/r05/hash_kpl2/, hash_glds2/, valu/): two keys per lane,
+// chains interleaved in one loop over a 128-key set (95 VGPRs, 5 waves per
+// SIMD): 0.41-0.49 vs 0.53 by key bytes; the LDS-DMA prefetch again, with
+// every memory operation of a set issued before its chains and one vmcnt(0)
+// a set (the round-4 version waited on its own prefetch): 0.41 vs 0.53.
+// Neither kept.  Nor is the VALU the bound: SQ_INSTS_VALU = 43.4 M per
+// launch (165 per set), at the 2.44 cycles a simple wave64 op measures on
+// this part (tools/pmc_calib.hip) 0.30 of the launch's issue capacity.
+// What the launch moves -- keys + 12 B of metadata + 4 B of output per key,
+// 0.87 GB -- runs at 0.77 of 8 TB/s: HBM binds.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -54,11 +64,6 @@
 #include "lv_internal.h"
 #include "lvk/knobs.h"
 
-#if LVK_HASH_GLDS2
-#define LVH_HASH_KERNEL lvh::hash_kernel_g2
-#else
-#define LVH_HASH_KERNEL lvh::hash_kernel
-#endif
 
 namespace lvh {
 
@@ -416,140 +421,6 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     }
 }
 
-// ---- LDS-DMA prefetch in issue order (LVK_HASH_GLDS2) ----
-// Round 4's LDS-DMA kernel (the next set's span requested by
-// global_load_lds_dwordx4 into a second stage while this set hashes) was
-// slower, 145 -> 172 us: its ISA shows a vmcnt(0) right after the next
-// span's DMA (before the metadata load that followed it), so every set still
-// waited for a full round trip.  Here a set's memory operations are all
-// issued before its chains run: (0) one vmcnt(0) -- this set's DMA, the next
-// set's metadata and the previous set's store, all issued a set ago (the
-// compiler does not order LDS-DMA before ds_read itself), (1) its key window
-// and tail dwords read from its stage, the previous set's results stored,
-// (2) the next set's geometry, its successor's metadata requested, the next
-// span's DMA into the other stage, (3) the chains from registers.  Stages of kGStage bytes
-// (64 keys of <= ~39 B on average); a set whose span does not fit, or whose
-// keys are out of order, reads its keys from memory.  LDS: 4 waves x 2 x
-// (2,560 + 80) B per workgroup, 7 workgroups per CU.
-constexpr uint32_t kGStage = 2560;
-constexpr uint32_t kGStageWords = kGStage / 4 + kSpanPad;
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-
-struct GSpan {
-    uint64_t lo16;
-    uint32_t nch;
-    bool staged;
-};
-
-__device__ __forceinline__ GSpan gspan_of(bool valid, uint64_t o, uint32_t L) {
-    const uint64_t act = __ballot(valid);
-    const int last = act ? 63 - __builtin_clzll(act) : 0;
-    const uint64_t lo = __shfl(o, 0), hi = __shfl(o + L, last);
-    GSpan g;
-    g.lo16 = lo & ~15ull;
-    const bool inside = !L || (o >= lo && o + L <= hi);
-    g.staged = act && hi > lo && hi - g.lo16 <= kGStage && __all(inside);  // wave-uniform
-    g.nch = g.staged ? static_cast<uint32_t>((hi - g.lo16 + 15) >> 4) : 0u;
-    return g;
-}
-
-// The span's granules into `stage` (granule c at byte 16 c): up to three
-// 1-KiB LDS-DMA instructions, lanes past the span masked off.
-__device__ __forceinline__ void gspan_issue(const uint8_t *__restrict__ base, const GSpan &g, uint32_t *stage,
-                                            uint32_t lane) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(base + g.lo16);
-#pragma unroll
-    for (uint32_t k = 0; k < (kGStage + 1023) / 1024; ++k) {
-        if (64u * k < g.nch) {  // wave-uniform
-            const uint32_t c = lane + 64u * k;
-            if (c < g.nch)
-                __builtin_amdgcn_global_load_lds((gbl_void_t *)(src + c), (lds_void_t *)(stage + 256u * k), 16, 0, 0);
-        }
-    }
-}
-
-template <typename Meta>
-__global__ void __launch_bounds__(256, 7) hash_kernel_g2(const uint8_t *__restrict__ base, Meta meta,
-                                                     uint32_t *__restrict__ out, uint32_t n, uint32_t flags) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage[4][2][kGStageWords];
-    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u;
-    uint64_t set = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
-    if (set * 64u >= n) return;  // wave-uniform
-    // prologue: the first set's metadata and span, the second's metadata
-    uint64_t o;
-    uint32_t L, sd;
-    meta.get(meta.load(set * 64u + lane, n, lane), set * 64u + lane, n, lane, o, L, sd);
-    GSpan g = gspan_of(set * 64u + lane < n, o, L);
-    if (g.staged) gspan_issue(base, g, stage[wv][0], lane);
-    MetaRaw nx = meta.load((set + W) * 64u + lane, n, lane);  // (clamped)
-    uint32_t *pout = out, pval = 0;  // the previous set's result, stored one set late
-    bool pst = false;
-    for (uint32_t k = 0;; ++k) {
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): expcnt / lgkmcnt untouched
-        const uint64_t i = set * 64u + lane;
-        const bool valid = i < n;
-        const uint32_t bs = static_cast<uint32_t>(o & 3u), nw = L >> 2, diff = L & 3u;
-        const bool fast = g.staged && valid && L && ((bs + L + 3) >> 2) <= kFastDw;
-        // 1. this set's window and tail dwords from its stage
-        uint32_t w[kFastDw + 1];
-        uint32_t t0 = 0, t1 = 0;
-        if (g.staged) {  // wave-uniform
-            const uint32_t *sp = stage[wv][k & 1u] + (fast ? ((o - bs - g.lo16) >> 2) : 0u);
-#pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = sp[j];  // (the stage's pad keeps the window inside)
-            t0 = sp[nw];
-            t1 = sp[nw + 1u];
-        }
-        w[kFastDw] = 0u;
-        if (pst) *pout = pval;
-        // 2. the next set: geometry, its successor's metadata, its span's DMA
-        const uint64_t nset = set + W;
-        const bool more = nset * 64u < n;  // wave-uniform
-        uint64_t on = 0;
-        uint32_t Ln = 0, sdn = 0;
-        GSpan gn{};
-        if (more) {
-            meta.get(nx, nset * 64u + lane, n, lane, on, Ln, sdn);
-            gn = gspan_of(nset * 64u + lane < n, on, Ln);
-        }
-        nx = meta.load((nset + W) * 64u + lane, n, lane);  // (clamped)
-        if (more && gn.staged) gspan_issue(base, gn, stage[wv][(k + 1u) & 1u], lane);
-        // 3. this set's hashes from registers (hash.rs:25-48)
-        uint32_t h = sd ^ (kM * L);
-        if (fast) {
-#pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j)
-                if (j < nw) h = mix(h, funnel(w[j + 1], w[j], bs));
-            if (diff) {
-                const uint32_t ndw = (bs + L + 3) >> 2;
-                const uint32_t tw = funnel(nw + 1 < ndw ? t1 : 0u, t0, bs);
-                if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
-                if (diff >= 2) h += ((tw >> 8) & 0xffu) << 8;
-                h += tw & 0xffu;
-                h *= kM;
-                h ^= h >> 24;
-            }
-        } else if (valid && L) {
-            h = key_from_mem(base, o, L, h);
-        }
-        pout = out + (valid ? i : 0u);
-        pval = (flags & LV_HASH_SHARD) ? (h >> 28) : h;
-        pst = valid;
-        if (!more) {
-            if (pst) *pout = pval;
-            break;
-        }
-        set = nset;
-        o = on;
-        L = Ln;
-        sd = sdn;
-        g = gn;
-    }
-}
-
 // persistent grid: 8 workgroups (32 waves) per CU at most
 uint32_t hash_grid(size_t n) {
     static std::atomic<int> cus_cache[64];
@@ -597,7 +468,7 @@ int lv_hash_batch_device(const uint8_t *d_arena, const uint64_t *d_off, const ui
     if (!d_arena || !d_off || !d_len || !d_out) return lvgpu_internal::set_error(LV_ERR_INVALID, "null device pointer");
     if (n > 0xffffffffull) return lvgpu_internal::set_error(LV_ERR_INVALID, "more than 2^32-1 buffers per call");
     if (flags & ~LV_HASH_SHARD) return lvgpu_internal::set_error(LV_ERR_INVALID, "unknown flags");
-    hipLaunchKernelGGL(LVH_HASH_KERNEL<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
+    hipLaunchKernelGGL(lvh::hash_kernel<lvh::OffsetsMeta>, dim3(lvh::hash_grid(n)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), d_arena, lvh::OffsetsMeta{d_off, d_len, d_seed}, d_out,
                        static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();
@@ -615,11 +486,11 @@ int lv_hash_batch_packed(const uint8_t *d_arena, const void *d_bounds, uint32_t 
         return lvgpu_internal::set_error(LV_ERR_INVALID, "bounds must be aligned to bound_bytes");
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (bound_bytes == 4)
-        hipLaunchKernelGGL(LVH_HASH_KERNEL<lvh::PackedMeta<uint32_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint32_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
                            lvh::PackedMeta<uint32_t>{static_cast<const uint32_t *>(d_bounds), d_seed}, d_out,
                            static_cast<uint32_t>(n), flags);
     else
-        hipLaunchKernelGGL(LVH_HASH_KERNEL<lvh::PackedMeta<uint64_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
+        hipLaunchKernelGGL(lvh::hash_kernel<lvh::PackedMeta<uint64_t>>, dim3(lvh::hash_grid(n)), dim3(256), 0, s, d_arena,
                            lvh::PackedMeta<uint64_t>{static_cast<const uint64_t *>(d_bounds), d_seed}, d_out,
                            static_cast<uint32_t>(n), flags);
     return lvgpu_internal::launch_status();

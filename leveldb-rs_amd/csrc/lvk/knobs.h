@@ -44,7 +44,6 @@
     defined(LVK_EXP_HASH_MUL24) || \
     defined(LVK_HASH_TAIL_READ) || \
     defined(LVK_HASH_LDS_ALL) || \
-    defined(LVK_HASH_GLDS2) || \
     defined(LVK_PIPE_CHUNK_MB) || \
     defined(LVK_MEMCPY_THREADS) || \
     defined(LVK_WALK_EXACT) || \
@@ -154,9 +153,6 @@
 #endif
 #ifndef LVK_MEMCPY_THREADS  // host: threads of the pageable -> pinned staging copy
 #define LVK_MEMCPY_THREADS 8
-#endif
-#ifndef LVK_HASH_GLDS2  // hash: the next set's span prefetched by LDS-DMA, in issue order (7 workgroups per CU)
-#define LVK_HASH_GLDS2 0
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8

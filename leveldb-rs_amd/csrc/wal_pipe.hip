@@ -285,11 +285,18 @@ __device__ __forceinline__ void pipe_walk_class(const PipeRest &rc, uint32_t n, 
     constexpr uint32_t K = 64 / G;
     const uint64_t nr = (n + K - 1) / K;
     if (!nr) return;  // (wave-uniform)
-    const uint64_t first = claim();
+    // claim() returns lane 0's atomic result unread (a vector register):
+    // reading it (readfirstlane) is what waits for the atomic, so the pending
+    // claim is read only when its round is needed
+    auto rd = [](uint64_t k) {
+        return (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k >> 32))) << 32) |
+               __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k));
+    };
+    const uint64_t first = rd(claim());
     if (first >= nr) return;
     uint64_t pend = claim();
     auto next = [&]() {
-        const uint64_t rr = pend;
+        const uint64_t rr = rd(pend);
         pend = claim();
         return rr;
     };
@@ -703,10 +710,10 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
         }
         for (uint32_t lists = 0; lists < 4u * grid; ++lists) {
             gu64 *const pools = sy + kSyPool + 4u * v;
-            auto claim = [&](uint32_t c) {  // (lane 0's result, in scalar registers)
+            auto claim = [&](uint32_t c) {  // (lane 0's result; pipe_walk_class reads it)
                 uint64_t k = 0;
                 if (lane == 0) k = __hip_atomic_fetch_add(pools + c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return (static_cast<uint64_t>(uni(static_cast<uint32_t>(k >> 32))) << 32) | uni(static_cast<uint32_t>(k));
+                return k;
             };
             PipeRest rc = r;
             pipe_walk_class<16>(rc, nn[0], L, lane, [&]() { return claim(0); });

@@ -9,6 +9,7 @@ root=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
+timeout -k 10 60 "$root/tools/pmc_calib" > "$out/calib_timed.json" 2>&1 && cat "$out/calib_timed.json" &&
 timeout -s KILL 60 rocprofv3 --pmc $C --output-format csv -d "$out/calib" -o pmc -- "$root/tools/pmc_calib" \
   > "$out/calib.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$out/hash" -o pmc -- python3 "$root/bench.py" --hash \
@@ -27,3 +28,5 @@ with open(os.path.join(out, "summary.txt"), "w") as fo:
         v = sorted(agg[k]); line = f"{k[0]:52s} {k[1]:22s} median {v[len(v)//2]:.6g}  n={len(v)}"
         print(line); fo.write(line + "\n")
 PY
+# the counter CSVs are large (one row per launch and counter): keep the summary only
+rm -rf "$out/calib" "$out/hash"
