@@ -59,9 +59,9 @@ struct StreamWs {
     std::mutex em;
     uint32_t *err = nullptr;
     uint32_t *herr = nullptr;
-    // the one-launch WAL scan's sync buffer (wal_pipe.hip: count granules,
-    // per-workgroup phase-B records and round counters), zeroed once when
-    // made; every launch leaves it zeroed again (its last workgroup out)
+    // the one-launch WAL scan's count granules and retire counter
+    // (wal_pipe.hip), zeroed once when made; every launch leaves them zeroed
+    // again (its last workgroup to retire clears them)
     uint64_t *gran = nullptr;
 };
 
@@ -99,7 +99,7 @@ struct DevCtx {
 };
 
 constexpr size_t kStageBytes = 64ull << 20;  // pinned staging slot for pageable input
-constexpr size_t kWalSyncWords = 1032 + 8 * 1024;  // the WAL scan's per-stream sync buffer (u64 words)
+constexpr size_t kWalSyncWords = 1024 + 2;  // the WAL scan's per-stream count granules + retire counter (u64 words)
 
 // lv_device_counters: per-device host-path traffic and allocations
 struct DevCounters {
@@ -160,7 +160,7 @@ inline void set_hint(lvk::Params &P, const HintCheck *hc, uint32_t dflt_len) {
 }
 // The violation word of (device, stream), allocated and zeroed on first use.
 int stream_err(DevCtx &c, hipStream_t s, uint32_t **out);
-// The stream's WAL-scan sync buffer (kWalSyncWords, made and zeroed on the stream once).
+// The stream's WAL-scan count granules (kWalSyncWords, made and zeroed on the stream once).
 int stream_gran(DevCtx &c, hipStream_t s, uint64_t **out);
 // Reads and clears the current device's violation word of stream s.
 int check_hints(hipStream_t s, uint32_t *violations);

@@ -29,6 +29,14 @@
 //   5. the waves walk that local list (classes 2, 1, 0 with G = 16, 4, 1),
 //      CRCs staged in LDS by record index, and the workgroup writes its CRCs
 //      in log order at the end.
+// (Round 5: phase-B rounds shared across workgroups -- per-workgroup round
+// counters in global memory, claimed with device-scope atomics one round
+// ahead, idle waves taking rounds of the workgroup with the most left -- ran
+// the call in 0.42-0.44 ms instead of 0.21; with the same code on LDS
+// counters and no sharing 0.256 ms (profiles/r05/wal_steal/).  A device
+// atomic under the scan's read stream costs far more than a round of the
+// small classes, and the direct scattered CRC stores of that version cost
+// ~40 us more than staging them in LDS.  Not kept.)
 // No cross-workgroup data moves but the 8-B counts: one granule array per
 // stream (library-owned, zeroed once when made), which every launch leaves
 // zeroed again -- the last workgroup to finish its look-back clears it -- so
@@ -64,10 +72,8 @@ constexpr uint32_t kPSortA = kPCrcA + kPipeMaxBlocks;    // phase-A list: block 
 constexpr uint32_t kPHist = kPSortA + kPipeMaxBlocks;    // phase-B key counts, then cursors
 constexpr uint32_t kPHistA = kPHist + kKeys;             // phase-A bucket counts, then cursors
 constexpr uint32_t kPCtl = kPHistA + 64;                 // control words (below)
-constexpr uint32_t kPBits = kPCtl + 64;                  // staged-CRC bitmap (by local record index)
-constexpr uint32_t kPStage = kPBits + 352;               // CRCs by local record index
-constexpr uint32_t kPStageN = kPB + 16384 - kPStage;     // records whose CRC can be staged (10,528)
-static_assert(kPStageN <= 32u * 352u, "the bitmap covers the staging");
+constexpr uint32_t kPStage = kPCtl + 64;                 // CRCs by local record index
+constexpr uint32_t kPStageN = kPB + 16384 - kPStage;     // records whose CRC is staged (10,880)
 enum : uint32_t {
     kCPoolA,    // round counters of the four lists
     kCPool16,
@@ -84,24 +90,13 @@ enum : uint32_t {
     kCBaseHi,
     kCCount,    // this workgroup's records
     kCDense,    // the phase-B list is in ent[base, ...) (more records than the local slice holds)
-    kCKnown,    // the base is known: phase-B CRCs go straight to crc[base + index]
-    kCTotLo,    // every workgroup's records (the look-back's total)
-    kCTotHi,
 };
 static_assert(kPStage + kPStageN == kPB + 16384, "carve-out fits region B");
-
-// The stream's sync buffer (lvh::kWalSyncWords u64 words, zero at launch; the
-// last workgroup to finish zeroes what the launch used): count granules, the
-// exit and abort words, then per workgroup a phase-B record {ready tag | dense
-// | base, n16 | n4 << 32, n1} and its phase-B round counters (16, 4, 1) --
-// global, so that workgroups done with their own lists take rounds of others.
-constexpr uint32_t kSyExit = 1024, kSyAbort = 1025, kSyRec = 1032, kSyPool = kSyRec + 4 * 1024;
-static_assert(kSyPool + 4 * 1024 == lvh::kWalSyncWords, "sync buffer layout");
 
 struct WalPipe {
     const uint8_t *log;
     uint64_t size, nblocks;
-    uint64_t *gran;  // the stream's sync buffer (above)
+    uint64_t *gran;  // one {tag 1 | count} granule per workgroup, then the retire counter (zero at launch)
     uint64_t *hc;    // header cache: kPipeCache per block (pos | len << 16 | type << 32)
     uint4 *ent;      // a dense workgroup's phase-B entries (8 B each) from its base on
     uint64_t *lst;   // phase-B entries of the other workgroups: kPipeCache per block of each
@@ -114,7 +109,7 @@ struct WalPipe {
 };
 
 // Timing variant (LVK_WAL_PIPE_TRACE): stamps of the phases per workgroup.
-constexpr uint32_t kPipeTrace = 80;
+constexpr uint32_t kPipeTrace = 64;
 #if LVK_WAL_PIPE_TRACE
 #define PTRACE(slot)                                                                                   \
     do {                                                                                               \
@@ -127,9 +122,6 @@ constexpr uint32_t kPipeTrace = 80;
 #endif
 
 __device__ __forceinline__ uint32_t &pctl(uint32_t k) { return g_lds[kPCtl + k]; }
-
-// (global address space: agent-scope sc1 stores / loads / atomics, never flat)
-typedef __attribute__((address_space(1))) uint64_t gu64;
 
 // Phase A: the sorted first records, geometry from LDS (no memory load).
 struct PipeFirst {
@@ -174,9 +166,8 @@ struct PipeRest {
     static constexpr uint32_t kExact = LVK_WALK_EXACT;
     static constexpr bool kPlainMerge = true;
     const uint64_t *lst;
-    uint64_t blk0;  // address of the list owner's first block
-    uint32_t *crc;  // own list: d_crc (+ the base once known, read at flush); another's: d_crc + its base
-    bool own;
+    uint64_t blk0;  // address of the workgroup's first block
+    uint32_t *crc;  // a dense workgroup: d_crc + its base
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
         const uint64_t ec = valid ? e : P.n - 1;
@@ -198,15 +189,10 @@ struct PipeRest {
     __device__ __forceinline__ void flush(const Params &, uint32_t wave, uint32_t lane, uint32_t nslots) const {
         const uint32_t li = g_oidx[wave][lane], c = g_ocrc[wave][lane];
         if (lane >= nslots || li == 0xffffffffu) return;
-        if (!own) {
-            crc[li] = c;
-        } else if (__hip_atomic_load(&g_lds[kPCtl + kCKnown], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            const uint64_t base = (static_cast<uint64_t>(g_lds[kPCtl + kCBaseHi]) << 32) | g_lds[kPCtl + kCBaseLo];
-            crc[base + li] = c;
-        } else {  // before the look-back (a local list, li < kPStageN): staged, copied out at the end
+        if (li < kPStageN)
             g_lds[kPStage + li] = c;
-            atomicOr(&g_lds[kPBits + (li >> 5)], 1u << (li & 31u));
-        }
+        else
+            crc[li] = c;
     }
 };
 
@@ -276,35 +262,6 @@ __device__ __forceinline__ uint32_t pipe_order_key(uint32_t o) {
     return o < 64u ? 128u + o : o < 128u ? o : o < 192u ? o - 128u : o;
 }
 
-// One class of a phase-B list: rounds claimed from the owner's global
-// counter, each claim requested one round ahead (its latency under the round
-// before it).
-template <int G, class Claim>
-__device__ __forceinline__ void pipe_walk_class(const PipeRest &rc, uint32_t n, const Lut &L, uint32_t lane,
-                                                Claim claim) {
-    constexpr uint32_t K = 64 / G;
-    const uint64_t nr = (n + K - 1) / K;
-    if (!nr) return;  // (wave-uniform)
-    // claim() returns lane 0's atomic result unread (a vector register):
-    // reading it (readfirstlane) is what waits for the atomic, so the pending
-    // claim is read only when its round is needed
-    auto rd = [](uint64_t k) {
-        return (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k >> 32))) << 32) |
-               __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k));
-    };
-    const uint64_t first = rd(claim());
-    if (first >= nr) return;
-    uint64_t pend = claim();
-    auto next = [&]() {
-        const uint64_t rr = rd(pend);
-        pend = claim();
-        return rr;
-    };
-    Params P{};
-    P.n = n;
-    sorted_stream<G>(P, rc, lane, L, first, next);
-}
-
 __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uint4 *__restrict__ image) {
     const uint32_t t = threadIdx.x, lane = t & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -325,7 +282,7 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
         // 7-byte last block)
         if (blen1 >= kPipeHeader) w1 = *reinterpret_cast<const uint32_t *>(log + start + 4);
     }
-    for (uint32_t k = t; k < kKeys + 64 + 64 + 352; k += kThreads) g_lds[kPHist + k] = 0;  // hist, histA, ctl, bits
+    for (uint32_t k = t; k < kKeys + 64 + 64; k += kThreads) g_lds[kPHist + k] = 0;  // hist, histA, ctl
     stage_tables_ab(image);
     __syncthreads();
     if (t < nblk) {
@@ -465,6 +422,8 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
             }
             const uint32_t count_w = run;
             PTRACE(4);
+            // (global address space: an agent-scope sc1 store / load, never flat)
+            typedef __attribute__((address_space(1))) uint64_t gu64;
             gu64 *const gran = reinterpret_cast<gu64 *>(reinterpret_cast<uint64_t>(a.gran));
             if (lane == 0) __hip_atomic_store(gran + w, (1ull << 32) | count_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // phase-B key starts in walk order (class 2, 1, 0); lanes 0-15
@@ -625,198 +584,95 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
                     total += __shfl_xor(total, k);
                 }
                 PTRACE(5);
+                // retire: every granule has been read; the last workgroup to
+                // get here clears them (and the counter) for the stream's next
+                // launch -- each workgroup published before it retired
+                uint64_t d = 0;
+                if (lane == 0)
+                    d = __hip_atomic_fetch_add(gran + 1024, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                if (__shfl(d, 0) + 1u == grid) {  // wave-uniform
+                    for (uint32_t j = lane; j < grid; j += 64u)
+                        __hip_atomic_store(gran + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) __hip_atomic_store(gran + 1024, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 const bool abort = timeout || total > a.cap;
-                if (timeout && lane == 0)
-                    __hip_atomic_store(gran + kSyAbort, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (w == 0 && lane == 0) *a.count = timeout ? ~0ull : total;
+                if (timeout && lane == 0) atomicOr(a.err, 1u);
                 if (lane == 0) {
                     pctl(kCBaseLo) = static_cast<uint32_t>(base);
                     pctl(kCBaseHi) = static_cast<uint32_t>(base >> 32);
-                    pctl(kCTotLo) = static_cast<uint32_t>(total);
-                    pctl(kCTotHi) = static_cast<uint32_t>(total >> 32);
                     pctl(kCAbort) = abort ? 1u : 0u;
                 }
                 return abort;
-            };
-            // This workgroup's phase-B record for the others (after its list
-            // is in memory): a workgroup done with its own lists takes rounds
-            // of this one's, its CRCs straight to crc[base + index].  An
-            // aborted workgroup offers none.
-            auto publish = [&](bool dense, bool abort) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) {
-                    gu64 *const rec = gran + kSyRec + 4u * w;
-                    const uint64_t n16 = abort ? 0u : pctl(kCN16), n4 = abort ? 0u : pctl(kCN4),
-                                   n1 = abort ? 0u : pctl(kCN1);
-                    __hip_atomic_store(rec + 1, n16 | (n4 << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(rec + 2, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(rec + 0, (1ull << 63) | (dense ? 1ull << 62 : 0ull) | base, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
             };
             const bool local = count_w <= kPStageN && count_w <= kPipeCache * nblk;
             if (local) {
                 // the list in this workgroup's slice of the workspace: ready
                 // as soon as the framing is done, before any other workgroup's
-                // count is known (CRCs staged in LDS until the base is)
+                // count is known
                 emit(a.lst + lo * kPipeCache, nullptr, nullptr);
                 ready();
-                const bool abort = lookback();
-                // (an aborted call writes no CRC: its own walks keep staging in LDS, never copied out)
-                if (lane == 0 && !abort)
-                    __hip_atomic_store(&pctl(kCKnown), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                publish(false, abort);
-                if (!abort) emit(nullptr, a.hdr_off + base, a.info + base);
+                if (!lookback()) emit(nullptr, a.hdr_off + base, a.info + base);
             } else {
                 // a dense workgroup: the list goes to ent[base, ...) (at most
                 // cap entries in all), so it waits for the base
-                const bool abort = lookback();
-                if (!abort)
+                if (!lookback())
                     emit(reinterpret_cast<uint64_t *>(a.ent) + base, a.hdr_off + base, a.info + base);
                 else if (lane == 0)
                     pctl(kCN16) = pctl(kCN4) = pctl(kCN1) = 0u;
-                if (lane == 0) {
-                    pctl(kCDense) = 1u;
-                    pctl(kCKnown) = 1u;
-                }
-                publish(true, abort);
+                if (lane == 0) pctl(kCDense) = 1u;
                 ready();
             }
         }
     }
 
-    // ---- 4. every wave: phase A, then (after the flag) the phase-B lists:
-    // its own workgroup's, then any other's with rounds left ----
+    // ---- 4. every wave: phase A, then (after the flag) the phase-B lists ----
     walk_first();
     PTRACE(8 + wave);
     while (__hip_atomic_load(&pctl(kCReady), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(16);
     PTRACE(24 + wave);
     {
-        gu64 *const sy = reinterpret_cast<gu64 *>(reinterpret_cast<uint64_t>(a.gran));
-        // One list's three classes (the own workgroup's first, then
-        // another's): rounds claimed from the owner's global counters, each
-        // claim requested one round ahead (its latency under the round before).
-        uint32_t v = w;
-        PipeRest r;
-        uint32_t nn[3];
-        {
-            const bool dense = uni(pctl(kCDense)) != 0u;
-            const uint64_t base = dense ? (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo)) : 0u;
-            r = PipeRest{dense ? reinterpret_cast<const uint64_t *>(a.ent) + base : a.lst + lo * kPipeCache, blk0, a.crc,
-                         true};
-            nn[0] = uni(pctl(kCN16));
-            nn[1] = uni(pctl(kCN4));
-            nn[2] = uni(pctl(kCN1));
-        }
-        for (uint32_t lists = 0; lists < 4u * grid; ++lists) {
-            gu64 *const pools = sy + kSyPool + 4u * v;
-            auto claim = [&](uint32_t c) {  // (lane 0's result; pipe_walk_class reads it)
-                uint64_t k = 0;
-                if (lane == 0) k = __hip_atomic_fetch_add(pools + c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return k;
-            };
-            PipeRest rc = r;
-            pipe_walk_class<16>(rc, nn[0], L, lane, [&]() { return claim(0); });
-            rc.lst = r.lst + nn[0];
-            pipe_walk_class<4>(rc, nn[1], L, lane, [&]() { return claim(1); });
-            rc.lst = r.lst + nn[0] + nn[1];
-            pipe_walk_class<1>(rc, nn[2], L, lane, [&]() { return claim(2); });
-            if (lists == 0) PTRACE(40 + wave);
-            // the next list: a sweep of every workgroup's record and counters
-            // (64 per load) picks the one with the most rounds left; none left
-            // anywhere ends the walk
-            uint64_t best = 0;
-            uint32_t bv = 0;
-            for (uint32_t j0 = 0; j0 < grid; j0 += 64u) {  // wave-uniform
-                const uint32_t j = j0 + lane;
-                uint64_t left = 0;
-                if (j < grid) {
-                    const gu64 *const rec = sy + kSyRec + 4u * j, *const pl = sy + kSyPool + 4u * j;
-                    const uint64_t r0 = __hip_atomic_load(rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t r1 = __hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t r2 = __hip_atomic_load(rec + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t c16 = __hip_atomic_load(pl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t c4 = __hip_atomic_load(pl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t c1 = __hip_atomic_load(pl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (r0 >> 63) {  // bytes left, roughly: a class-16 round weighs 4 class-4 and 16 class-1 ones
-                        const uint64_t m16 = ((r1 & 0xffffffffu) + 3) / 4, m4 = ((r1 >> 32) + 15) / 16,
-                                       m1 = (r2 + 63) / 64;
-                        left = 16u * (m16 > c16 ? m16 - c16 : 0u) + 4u * (m4 > c4 ? m4 - c4 : 0u) +
-                               (m1 > c1 ? m1 - c1 : 0u);
-                    }
-                }
-                uint64_t key = (left << 10) | j;  // the most left (ties: the highest index)
-#pragma unroll
-                for (int k = 32; k >= 1; k >>= 1) {
-                    const uint64_t o = __shfl_xor(key, k);
-                    key = o > key ? o : key;
-                }
-                if ((key >> 10) > best) {
-                    best = key >> 10;
-                    bv = static_cast<uint32_t>(key & 1023u);
-                }
-            }
-            if (!best) break;  // (wave-uniform)
-            v = __builtin_amdgcn_readfirstlane(bv);
-            const gu64 *const rec = sy + kSyRec + 4u * v;
-            auto uni64 = [&](uint64_t x) {
-                return (static_cast<uint64_t>(uni(static_cast<uint32_t>(x >> 32))) << 32) | uni(static_cast<uint32_t>(x));
-            };
-            const uint64_t r0 = uni64(__hip_atomic_load(rec, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
-            const uint64_t r1 = uni64(__hip_atomic_load(rec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            const uint64_t r2 = uni64(__hip_atomic_load(rec + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            const uint64_t vbase = r0 & ((1ull << 62) - 1);
-            const uint64_t vlo = a.nblocks * v / grid;
-            r = PipeRest{(r0 >> 62) & 1u ? reinterpret_cast<const uint64_t *>(a.ent) + vbase : a.lst + vlo * kPipeCache,
-                         reinterpret_cast<uint64_t>(a.log) + vlo * kPipeBlockSize, a.crc + vbase, v == w};
-            if (v == w) r.crc = a.crc;  // (own rounds left by the other waves: the base from LDS, as above)
-            nn[0] = static_cast<uint32_t>(r1);
-            nn[1] = static_cast<uint32_t>(r1 >> 32);
-            nn[2] = static_cast<uint32_t>(r2);
-        }
+        const bool dense = uni(pctl(kCDense)) != 0u;
+        const uint32_t n16 = uni(pctl(kCN16)), n4 = uni(pctl(kCN4)), n1 = uni(pctl(kCN1));
+        const uint64_t base = dense ? (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo)) : 0u;
+        const uint64_t *const lst = dense ? reinterpret_cast<const uint64_t *>(a.ent) + base : a.lst + lo * kPipeCache;
+        uint32_t *const crcd = a.crc + base;  // dense: records past the LDS staging go straight out
+        const PipeRest r16{lst, blk0, crcd};
+        const PipeRest r4{lst + n16, blk0, crcd};
+        const PipeRest r1{lst + n16 + n4, blk0, crcd};
+        Params P{};
+        auto next16 = [&]() { return pool(kCPool16); };
+        auto next4 = [&]() { return pool(kCPool4); };
+        auto next1 = [&]() { return pool(kCPool1); };
+        P.n = n16;
+        sorted_stream<16>(P, r16, lane, L, next16(), next16);
+        P.n = n4;
+        sorted_stream<4>(P, r4, lane, L, next4(), next4);
+        P.n = n1;
+        sorted_stream<1>(P, r1, lane, L, next1(), next1);
     }
-    PTRACE(56 + wave);
+    PTRACE(40 + wave);
     __syncthreads();
-    gu64 *const sy = reinterpret_cast<gu64 *>(reinterpret_cast<uint64_t>(a.gran));
-    const bool abort = uni(pctl(kCAbort)) != 0u;
-    // ---- 5. the workgroup's own CRCs still in LDS, in log order ----
-    if (!abort) {
-        const uint64_t base = (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo));
-        const uint32_t count_w = uni(pctl(kCCount));
-        uint32_t *const crc = a.crc + base;
-        for (uint32_t bl = t; bl < nblk; bl += kThreads) {  // phase A's CRCs at their record index
-            const uint32_t r = g_lds[kPRecA + bl];
-            if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK && (r & 0xffffu) + 1u >= kPipeAMin)
-                crc[g_lds[kPPre + bl]] = g_lds[kPCrcA + bl];
+    if (uni(pctl(kCAbort))) return;
+    // ---- 5. the workgroup's CRCs in log order ----
+    const uint64_t base = (static_cast<uint64_t>(uni(pctl(kCBaseHi))) << 32) | uni(pctl(kCBaseLo));
+    const uint32_t count_w = uni(pctl(kCCount));
+    uint32_t *const crc = a.crc + base;
+    for (uint32_t bl = t; bl < nblk; bl += kThreads) {  // phase A's CRCs to their record index
+        const uint32_t r = g_lds[kPRecA + bl];
+        if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK && (r & 0xffffu) + 1u >= kPipeAMin) {
+            const uint32_t li = g_lds[kPPre + bl];
+            if (li < kPStageN)
+                g_lds[kPStage + li] = g_lds[kPCrcA + bl];
+            else
+                crc[li] = g_lds[kPCrcA + bl];
         }
-        const uint32_t ns = count_w < kPStageN ? count_w : kPStageN;
-        for (uint32_t i = t; i < ns; i += kThreads)  // phase-B CRCs staged before the base was known
-            if ((g_lds[kPBits + (i >> 5)] >> (i & 31u)) & 1u) crc[i] = g_lds[kPStage + i];
     }
-    // ---- 6. the last workgroup out: the count, and the sync buffer zeroed ----
-    if (wave == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint64_t e = 0;
-        if (lane == 0) e = __hip_atomic_fetch_add(sy + kSyExit, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (__shfl(e, 0) + 1u == grid) {  // wave-uniform: every other workgroup is done with the buffer
-            const uint64_t ab = __hip_atomic_load(sy + kSyAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t total = (static_cast<uint64_t>(uni(pctl(kCTotHi))) << 32) | uni(pctl(kCTotLo));
-            if (lane == 0) *a.count = ab ? ~0ull : total;
-            for (uint32_t j = lane; j < grid; j += 64u) {
-                __hip_atomic_store(sy + j, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
-                    __hip_atomic_store(sy + kSyRec + 4u * j + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(sy + kSyPool + 4u * j + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (lane == 0) {
-                __hip_atomic_store(sy + kSyAbort, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(sy + kSyExit, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        PTRACE(72);
-    }
+    __syncthreads();
+    const uint32_t ns = count_w < kPStageN ? count_w : kPStageN;
+    for (uint32_t i = t; i < ns; i += kThreads) crc[i] = g_lds[kPStage + i];
+    if (wave == 0) PTRACE(56);
 }
 
 }  // namespace lvk

@@ -23,7 +23,7 @@ import lvgpu  # noqa: E402
 import lvgpu.wal as LW  # noqa: E402
 import wal_oracle as W  # noqa: E402
 
-KT = 80
+KT = 64
 r = W.Random(301)
 sizes, tot = [], 0
 while tot < 262144 * 4096:
@@ -66,22 +66,20 @@ for rep in range(int(sys.argv[1]) if len(sys.argv) > 1 else 5):
                  "published": pct(us[:, 4]), "lookback_done": pct(us[:, 5]), "ready": pct(us[:, 6]),
                  "phaseA_done_first_wave": pct(us[:, 8:24].min(1)), "phaseA_done_last_wave": pct(us[:, 8:24].max(1)),
                  "ready_seen_last_wave": pct(us[:, 24:40].max(1)),
-                 "own_done_first_wave": pct(us[:, 40:56].min(1)), "own_done_last_wave": pct(us[:, 40:56].max(1)),
-                 "walk_done_first_wave": pct(us[:, 56:72].min(1)), "walk_done_last_wave": pct(us[:, 56:72].max(1)),
-                 "end": pct(us[:, 72]),
+                 "walk_done_first_wave": pct(us[:, 40:56].min(1)), "walk_done_last_wave": pct(us[:, 40:56].max(1)),
+                 "end": pct(us[:, 56]),
                  # wave time lost per workgroup, as a fraction of its waves x its end:
                  # waiting for the phase-B list after phase A, and idle after the walk
-                 "idle_wait_list": pct(100 * np.clip(us[:, 24:40] - us[:, 8:24], 0, None).sum(1) / (16 * us[:, 72])),
-                 "idle_after_walk": pct(100 * (us[:, 72:73] - us[:, 56:72]).sum(1) / (16 * us[:, 72])),
+                 "idle_wait_list": pct(100 * np.clip(us[:, 24:40] - us[:, 8:24], 0, None).sum(1) / (16 * us[:, 56])),
+                 "idle_after_walk": pct(100 * (us[:, 56:57] - us[:, 40:56]).sum(1) / (16 * us[:, 56])),
                  "idle_units": "percent of the workgroup's 16 waves x its end"})
     # per-wave stamps of the first-, median- and last-ending workgroups
-    order = np.argsort(us[:, 72])
+    order = np.argsort(us[:, 56])
     runs[-1]["waves"] = {name: {"wg": int(order[k]), "framed": round(float(fr[order[k]]), 1),
                                 "ready": round(float(us[order[k], 6]), 1),
                                 "phaseA_done": [round(float(x), 1) for x in us[order[k], 8:24]],
                                 "ready_seen": [round(float(x), 1) for x in us[order[k], 24:40]],
-                                "own_done": [round(float(x), 1) for x in us[order[k], 40:56]],
-                                "walk_done": [round(float(x), 1) for x in us[order[k], 56:72]],
-                                "end": round(float(us[order[k], 72]), 1)}
+                                "walk_done": [round(float(x), 1) for x in us[order[k], 40:56]],
+                                "end": round(float(us[order[k], 56]), 1)}
                          for name, k in (("first", 0), ("median", grid // 2), ("last", grid - 1))}
 print(json.dumps(runs[-1], indent=1))
