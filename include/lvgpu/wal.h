@@ -51,10 +51,12 @@ lv_wal_scan *lv_wal_scan_host_pipelined(const uint8_t *log, size_t bytes, int de
  * Immediate for any other scan. */
 int lv_wal_scan_wait(lv_wal_scan *scan);
 /* Device-resident scan of a log already in HBM (8-byte aligned), with no
- * host synchronisation: every 32 KiB block's header chain is walked inside
- * its workgroup's pass and every [type || payload] unit is checksummed: a
- * memset and one kernel launch on `stream` (five launches for logs of more
- * than 1,024 blocks per compute unit).  Records go to d_hdr_off / d_crc /
+ * host synchronisation: every 32 KiB block's header chain is walked as
+ * read_physical_record frames it and every [type || payload] unit is
+ * checksummed, in five launches on `stream` (framing, one global length sort,
+ * the CRC kernel, the log-order write-back) -- or, with
+ * lv_wal_scan_set_path(1), in one launch (every workgroup frames, sorts and
+ * checksums its own blocks).  Records go to d_hdr_off / d_crc /
  * d_info in log order (the lv_wal_scan arrays below), at most `cap` of them;
  * *d_count (device memory) receives the number of records.  If that number
  * exceeds cap, nothing else is written: call again with a larger capacity.
@@ -62,11 +64,9 @@ int lv_wal_scan_wait(lv_wal_scan *scan);
  * another kernel held compute units for ~0.2 s; nothing was written.)
  * d_workspace: >= lv_wal_scan_workspace_bytes(bytes, cap) bytes, 16-B aligned. */
 size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap);
-/* Debug / test hook (calling thread): 0 (default) lets lv_wal_scan_device
- * pick its path, 1 forces the one-launch scan (every workgroup frames, sorts
- * and checksums its own blocks; LV_ERR_INVALID from the scan where it does
- * not apply: more than 1,024 blocks per compute unit), 2 the five-launch scan
- * (framing kernels, one global length sort, the class kernel, the unsort).
+/* Debug / test hook (calling thread): 0 (default) and 2 run the five-launch
+ * scan, 1 the one-launch scan (LV_ERR_INVALID from the scan where it does
+ * not apply: more than 1,024 blocks per compute unit).
  * Returns the previous setting, or LV_ERR_INVALID for another value. */
 int lv_wal_scan_set_path(int path);
 int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,

@@ -441,9 +441,13 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     uint8_t *wb = static_cast<uint8_t *>(d_workspace);
     const bool pipe = wal_pipe_applies(*c, bytes);
     if (g_wal_path == 1 && !pipe) return set_err(LV_ERR_INVALID, "the one-launch scan does not apply to this log");
-    if (pipe && g_wal_path != 2) {
-        // one launch: every workgroup frames, sorts and checksums its own
-        // blocks (wal_pipe.hip)
+    // The five-launch scan is the default: the one-launch scan (wal_pipe.hip;
+    // every workgroup frames, sorts and checksums its own blocks) measured
+    // 0.622 of 8 TB/s against its 0.632 on the same box (216 vs 212.5 us per
+    // 1.075 GB call, profiles/r05/wal_paths/): its per-workgroup rounds end
+    // ragged (9 % of wave time idle at the end) and the slowest workgroup sets
+    // the launch.  lv_wal_scan_set_path(1) selects it (tests run both).
+    if (pipe && g_wal_path == 1) {
         if (int rc = launch_wal_pipe(*c, d_log, bytes, d_hdr_off, d_crc, d_info, cap, d_count, wb, s)) return rc;
         g_kernel = "wal_pipe_kernel";
         return check_launch();

@@ -1115,7 +1115,9 @@ HINT_LIE_CASES = {
                               "crc32c_blocks_kernel<16,pieces,gather>+combine_pieces_kernel"),
     "identity_understated": (5000, 4000, False, "longer", lvgpu.HINT_ERR_NOT_UNIFORM,
                              "hint_len_kernel+crc32c_classes_kernel"),
-    "fused_uniform_shorter": (600, 1000, False, "shorter", lvgpu.HINT_ERR_NOT_UNIFORM, "crc32c_fused_small_kernel"),
+    # (the fused kernel sums every length too: a shorter one also misses the total)
+    "fused_uniform_shorter": (600, 1000, False, "shorter", lvgpu.HINT_ERR_NOT_UNIFORM | lvgpu.HINT_ERR_TOTAL,
+                              "crc32c_fused_small_kernel"),
     "fused_understated_max": (600, 1000, False, "nonuniform_longer",
                               lvgpu.HINT_ERR_LONGER | lvgpu.HINT_ERR_TOTAL, "crc32c_fused_small_kernel"),
 }
