@@ -131,9 +131,9 @@ bool is_pinned(const void *p) {
 }
 
 // memcpy split over up to 8 host threads (pageable -> pinned staging).
-void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes) {
+void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, unsigned threads) {
     unsigned nt = std::thread::hardware_concurrency();
-    nt = nt == 0 ? 1 : (nt > LVK_MEMCPY_THREADS ? LVK_MEMCPY_THREADS : nt);
+    nt = nt == 0 ? 1 : (nt > threads ? threads : nt);
     if (bytes < (4u << 20) || nt == 1) {
         std::memcpy(dst, src, bytes);
         return;

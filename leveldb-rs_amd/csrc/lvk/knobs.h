@@ -46,6 +46,7 @@
     defined(LVK_HASH_LDS_ALL) || \
     defined(LVK_PIPE_CHUNK_MB) || \
     defined(LVK_MEMCPY_THREADS) || \
+    defined(LVK_PIPE_COPY_THREADS) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
     defined(LVK_WAL_LOCAL) || \
@@ -153,6 +154,9 @@
 #endif
 #ifndef LVK_MEMCPY_THREADS  // host: threads of the pageable -> pinned staging copy
 #define LVK_MEMCPY_THREADS 8
+#endif
+#ifndef LVK_PIPE_COPY_THREADS  // host: the same in the pipelined WAL scan's worker (a Reader runs beside it)
+#define LVK_PIPE_COPY_THREADS 4
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8

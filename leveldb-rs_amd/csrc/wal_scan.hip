@@ -628,7 +628,11 @@ int pipe_enqueue(PipeSlot &sl, const uint8_t *log, bool pinned) {
     if (int rc = grow_dev(sl.d_log, sl.d_log_cap, sl.len + 16)) return rc;
     const uint8_t *src = log + sl.lo;
     if (!pinned) {
-        par_memcpy(sl.stage, src, sl.len);
+        // (4 copy threads, not the host path's 8: the Reader on the caller's
+        // thread replays beside this copy, and with 8 it ran ~35 % slower --
+        // recovery 21.4-22.1 GiB/s with 8, 26.7-26.9 with 4, the scan alone
+        // 20.2-20.5 ms either way; profiles/r05/wal_host/)
+        par_memcpy(sl.stage, src, sl.len, LVK_PIPE_COPY_THREADS);
         src = sl.stage;
     }
     if (int rc = hip_err(hipMemcpyAsync(*sl.d_log, src, sl.len, hipMemcpyHostToDevice, sl.s), "H2D")) return rc;

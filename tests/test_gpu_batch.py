@@ -1105,10 +1105,9 @@ def _hint_case(torch, dev, rng, n, L, aligned, seeded=False, slack=1 << 16):
 
 # name: (n, L, aligned hint, how the device arrays contradict the hint, bits, kernel)
 HINT_LIE_CASES = {
-    "gather_misaligned_offset": (3000, 4096, True, "misalign", lvgpu.HINT_ERR_MISALIGNED,
-                                 "crc32c_blocks_kernel<16,gather>"),
-    "gather_understated_max_len": (3000, 4096, True, "longer", lvgpu.HINT_ERR_NOT_UNIFORM,
-                                   "crc32c_blocks_kernel<16,gather>"),
+    # (the blocks kernel's group size is the strided plan's, G = 16 or 64 by CU count)
+    "gather_misaligned_offset": (3000, 4096, True, "misalign", lvgpu.HINT_ERR_MISALIGNED, "crc32c_blocks_kernel<"),
+    "gather_understated_max_len": (3000, 4096, True, "longer", lvgpu.HINT_ERR_NOT_UNIFORM, "crc32c_blocks_kernel<"),
     "gather_pieces_misaligned": (1024, 65536, True, "misalign", lvgpu.HINT_ERR_MISALIGNED,
                                  "crc32c_blocks_kernel<16,pieces,fused,gather>"),
     "gather_pieces_shorter": (16, 1 << 20, True, "shorter", lvgpu.HINT_ERR_NOT_UNIFORM,
@@ -1142,6 +1141,7 @@ def test_wrong_hint_is_reported(torch_dev, case):
     ln = torch.from_numpy(lens.view(np.int32)).to(dev)
     out = lvgpu.batch_hint(a, o, ln, hint, masked=True)
     assert lvgpu.last_kernel().startswith(kern), lvgpu.last_kernel()
+    assert ("gather" in lvgpu.last_kernel()) == aligned, lvgpu.last_kernel()
     lvgpu.batch_check()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle_batch(arena, offs, lens, None, True))
     # now the device arrays contradict the (unchanged) hint
