@@ -1385,7 +1385,15 @@ def main():
     kern_ms = head["kern_ms"]
     kern_avg_ms = sum(kern_ms) / len(kern_ms)
     own = rank_record(torch, dev, rank, local, nbytes, args.steps, head["timing"], kern_avg_ms)
+    if n > 0:  # every rank checks a sample of its own batch against the oracle
+        if args.scaling == "weak":
+            own["parity_sample"] = rank_sample_check(off, ln, out, n, PAYLOAD_SEED ^ (shard_rank * 0x9E3779B9))
+        elif args.workload in ("c3", "c5"):  # a uniform global batch: its global offsets
+            own["parity_sample"] = rank_sample_check(off, ln, out, n, None, sh)
     per_rank = shard.gather_ranks(own, dist, world)
+    if n > 0 and not all(r.get("parity_sample", True) for r in per_rank):
+        raise SystemExit("parity sample failed on rank(s) "
+                         + str([r["rank"] for r in per_rank if not r.get("parity_sample", True)]))
     agg = shard.aggregate(per_rank, args.steps, head["timing"].own_max)
     agg_b = shard.aggregate(per_rank, args.steps, head["timing"].barrier_max)
     value = agg["GiB_per_s"]
@@ -1558,6 +1566,35 @@ def c5_strong_record(torch, lvgpu, args, dist, backend, dev, rank, local, world,
             "per_gpu": per, "load_imbalance": round(agg["imbalance"], 4),
             "parity": "every rank's first and last 8 blocks vs the oracle over host bytes generated at the "
                       "same global offsets"}
+
+
+def rank_sample_check(off, ln, out, n, seed, sh=None, k=8):
+    """This rank's first and last k buffers vs the oracle over host bytes
+    from the oracle's own splitmix generator: at the buffers' offsets in the
+    rank's arena (weak scaling: each rank's arena generated from offset 0 with
+    its own seed), or -- one global batch (strong) -- at their global offsets."""
+    import numpy as np
+    if sh is not None:
+        return c5_sample_check(None, out, sh, k)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    L = W.lib()
+    got = out[:n].cpu().numpy().view(np.uint32)
+    offs = off.cpu().numpy().astype(np.uint64)
+    lens = ln.cpu().numpy().view(np.uint32)
+    for lo in sorted({0, max(0, n - k)}):
+        m = min(k, n - lo)
+        o, l = offs[lo:lo + m], lens[lo:lo + m]
+        b0 = int(o.min())
+        buf = np.empty(max(1, int((o + l).max()) - b0), dtype=np.uint8)
+        L.oracle_fill_splitmix(buf.ctypes.data, b0, buf.size, seed)
+        ho = (o - np.uint64(b0)).astype(np.uint64)
+        hl = np.ascontiguousarray(l, dtype=np.uint32)
+        want = np.zeros(m, dtype=np.uint32)
+        L.oracle_batch(buf.ctypes.data, ho.ctypes.data, hl.ctypes.data, None, want.ctypes.data, m, 0)
+        if not np.array_equal(got[lo:lo + m], want):
+            return False
+    return True
 
 
 def c5_sample_check(arena, out, sh, k=8):

@@ -51,6 +51,7 @@
     defined(LVK_WAL_UNSORT) || \
     defined(LVK_WAL_LOCAL) || \
     defined(LVK_WAL_PIPE_TRACE) || \
+    defined(LVK_PIPE_AMIN) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -163,6 +164,9 @@
 #endif
 #ifndef LVK_WAL_LOCAL  // WAL scan: one persistent launch, each workgroup frames, sorts and walks its own blocks
 #define LVK_WAL_LOCAL 1
+#endif
+#ifndef LVK_PIPE_AMIN  // WAL one-launch scan: smallest first-record unit walked in phase A (> 2048: class 2)
+#define LVK_PIPE_AMIN 2049
 #endif
 #ifndef LVK_WAL_PIPE_TRACE  // timing only: wal_pipe_kernel writes s_memrealtime stamps per workgroup to its workspace
 #define LVK_WAL_PIPE_TRACE 0

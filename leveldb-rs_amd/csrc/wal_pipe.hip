@@ -60,7 +60,7 @@ constexpr uint32_t kPipeBlockSize = 32768;  // log_format.rs:63
 constexpr uint32_t kPipeHeader = 7;         // log_format.rs:66
 constexpr uint32_t kPipeMaxBlocks = 1024;   // blocks per workgroup (the LDS block tables)
 constexpr uint32_t kPipeCache = 64;         // headers per block in the global header cache
-constexpr uint32_t kPipeAMin = 2049;        // phase A: first records of class-2 units (> 2 KiB)
+constexpr uint32_t kPipeAMin = LVK_PIPE_AMIN;  // phase A: first records of units >= this (class 2: > 2 KiB)
 
 // Region B carve-out (word offsets into g_lds).
 constexpr uint32_t kPB = kRegionB / 4;
