@@ -645,12 +645,21 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
         auto next16 = [&]() { return pool(kCPool16); };
         auto next4 = [&]() { return pool(kCPool4); };
         auto next1 = [&]() { return pool(kCPool1); };
-        P.n = n16;
-        sorted_stream<16>(P, r16, lane, L, next16(), next16);
-        P.n = n4;
-        sorted_stream<4>(P, r4, lane, L, next4(), next4);
-        P.n = n1;
-        sorted_stream<1>(P, r1, lane, L, next1(), next1);
+        if constexpr (LVK_PIPE_B_SMALL_FIRST) {  // classes 1, 0, then 2 (longest first: the round ends short)
+            P.n = n4;
+            sorted_stream<4>(P, r4, lane, L, next4(), next4);
+            P.n = n1;
+            sorted_stream<1>(P, r1, lane, L, next1(), next1);
+            P.n = n16;
+            sorted_stream<16>(P, r16, lane, L, next16(), next16);
+        } else {
+            P.n = n16;
+            sorted_stream<16>(P, r16, lane, L, next16(), next16);
+            P.n = n4;
+            sorted_stream<4>(P, r4, lane, L, next4(), next4);
+            P.n = n1;
+            sorted_stream<1>(P, r1, lane, L, next1(), next1);
+        }
     }
     PTRACE(40 + wave);
     __syncthreads();
