@@ -147,6 +147,17 @@ def test_encode_then_scan_then_read(gpu):
 
 SORTED = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel"
 PIPE = "wal_pipe_kernel"
+OVL = "wal_pipe_kernel<first>|wal_hist+sort_scan+wal_scatter -> crc32c_classes_kernel<dyn>+wal_unsort"
+FRAME_CUS = 16  # LVK_WAL_FRAME_CUS
+
+
+def _overlapped_applies(nbytes):
+    """Path 3 (the overlapped scan) runs when every phase-A workgroup (all CUs
+    but the framing stream's) owns at least one block; otherwise the
+    five-launch scan does."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    return -(-nbytes // B) >= cus - FRAME_CUS
 
 
 def _check_scan_device(log, cap=None, shift=0):
@@ -165,7 +176,9 @@ def _check_scan_device(log, cap=None, shift=0):
     # reads nothing of the workspace it did not write first
     dirty = torch.full((LW.scan_workspace_bytes(len(log), cap),), 0xff, dtype=torch.uint8, device="cuda:0")
     try:
-        for path, kern in ((1, PIPE), (2, SORTED + ("+wal_unsort" if cap else ""))):
+        sorted_kern = SORTED + ("+wal_unsort" if cap else "")
+        ovl = OVL if cap else OVL.replace("+wal_unsort", "")
+        for path, kern in ((1, PIPE), (2, sorted_kern), (3, ovl if _overlapped_applies(len(log)) else sorted_kern)):
             LW.set_scan_path(path)
             for ws in (None, dirty):
                 hdr, crc, info, count = LW.scan_device(t, cap, workspace=ws)
@@ -241,6 +254,40 @@ def test_scan_device_capacity(gpu):
     n = len(W.scan_log(tiny)[0])
     for cap in (n - 1, n, n + 1, 2 * n):
         _check_scan_device(tiny, cap=cap)
+
+
+def test_scan_device_overlapped(gpu):
+    """Path 3 (phase A on a CU-masked stream beside the framing kernels, then
+    the class kernel over the rest, merged by wal_unsort) on logs of >= 240
+    blocks: bench-like mixed records, corruption, truncation, a zero tail,
+    blocks of > 64 tiny records, every record a block's first (full
+    fragments), too small a capacity, an 8-B-aligned log."""
+    rng = np.random.default_rng(41)
+    mixed = _random_records(rng, 2600, maxlog=16)
+    log = bytearray(_oracle_encode(mixed, int(rng.integers(0, B))))
+    assert _overlapped_applies(len(log)), len(log)
+    _check_scan_device(bytes(log))
+    _check_scan_device(bytes(log), shift=8)
+    n = len(W.scan_log(bytes(log))[0])
+    _check_scan_device(bytes(log), cap=n - 1)
+    for pos in rng.integers(0, len(log), size=200):
+        log[int(pos)] ^= int(rng.integers(1, 256))
+    for blk in rng.integers(0, len(log) // B, size=10):  # first headers hit directly
+        log[int(blk) * B + 4 + int(rng.integers(0, 3))] ^= 0x5a
+    _check_scan_device(bytes(log[:len(log) - 777]))
+    # 40 KiB records: each block's first record a FIRST / MIDDLE / LAST fragment
+    frag = _oracle_encode([rng.integers(0, 256, size=40000, dtype=np.uint8).tobytes() for _ in range(260)])
+    _check_scan_device(frag + bytes(2 * B + 5))
+    # phase-A units around the threshold (a first record of 2,047 / 2,048 B of
+    # payload: unit 2,048 / 2,049) and many tiny records per block
+    edge = []
+    for k in range(300):  # each group fills its block exactly: the next one's record is a first record
+        grp = [bytes([k % 256]) * (2047 + k % 3)] + [bytes([k % 5]) * (k % 4)] * (3 + k % 90)
+        grp.append(bytes(B - sum(H + len(r) for r in grp) - H))
+        edge.extend(grp)
+    elog = _oracle_encode(edge)
+    assert len(elog) == 300 * B
+    _check_scan_device(elog)
 
 
 def test_scan_device_rejects_non_byte_views(gpu):
