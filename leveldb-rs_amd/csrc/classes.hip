@@ -626,7 +626,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, 
 namespace lvh {
 
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s) {
-    if (P.gpool)
+    if (P.gpool && seeded)
+        hipLaunchKernelGGL((lvk::crc32c_classes_kernel<true, true>), dim3(static_cast<uint32_t>(c.cus)),
+                           dim3(lvk::kThreads), 0, s, P, c.image[2], ws);
+    else if (P.gpool)
         hipLaunchKernelGGL((lvk::crc32c_classes_kernel<false, true>), dim3(static_cast<uint32_t>(c.cus)),
                            dim3(lvk::kThreads), 0, s, P, c.image[2], ws);
     else if (seeded)

@@ -54,6 +54,7 @@
     defined(LVK_PIPE_AMIN) || \
     defined(LVK_PIPE_B_SMALL_FIRST) || \
     defined(LVK_WAL_FRAME_CUS) || \
+    defined(LVK_CLASS_DYN) || \
     defined(LVK_WAL_HIST_CACHE) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
@@ -173,6 +174,9 @@
 #endif
 #ifndef LVK_PIPE_AMIN  // WAL one-launch scan: smallest first-record unit walked in phase A (> 2048: class 2)
 #define LVK_PIPE_AMIN 2049
+#endif
+#ifndef LVK_CLASS_DYN  // class kernel after the sort: rounds of classes 2+3 in chunks from a device counter
+#define LVK_CLASS_DYN 0
 #endif
 #ifndef LVK_WAL_FRAME_CUS  // WAL overlapped scan: CUs of the framing stream (phase A gets the rest)
 #define LVK_WAL_FRAME_CUS 16

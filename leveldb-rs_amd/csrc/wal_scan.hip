@@ -537,8 +537,9 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
         g_kernel = "wal_pipe_kernel<first>|wal_hist+sort_scan+wal_scatter -> crc32c_classes_kernel<dyn>+wal_unsort";
         return check_launch();
     }
+    P.gpool = LVK_CLASS_DYN ? ws + lvk::kWsPool : nullptr;
     hipLaunchKernelGGL(lvk::wal_hist<>, g, dim3(lvk::kWalHistThreads), 0, s, d_log, static_cast<uint64_t>(bytes), nblocks,
-                       chunk, M, wgrec, blk, hc, nullptr);
+                       chunk, M, wgrec, blk, hc, P.gpool);
     // (Round 3: claiming each workgroup's key runs with device atomics in
     // wal_hist instead of this column scan -- a memset of the totals first --
     // measured 0.6 % slower: the memset launch and wal_hist's returning
