@@ -31,19 +31,7 @@ constexpr uint32_t kSmallRounds = LVK_SMALL_ROUNDS;  // small-class rounds per w
 // every workgroup walking every class in turn, with the image restaged per
 // G -- the small classes ran alone, latency- and VALU-bound, for ~100 us of
 // C2's 1.2 ms.)
-//
-// DYN (the overlapped WAL scan, wal_scan.hip): the kernel starts while another
-// kernel still holds most CUs, so its workgroups start over ~50 us; the large
-// rounds come from one device counter (P.gpool) in chunks of kDynRounds
-// instead of b + k * grid.  The workgroup's waves still take rounds from its
-// LDS counter; chunk c's base sits in an LDS slot tagged c + 1, and the wave
-// that takes the middle round of chunk c claims chunk c + 1 (one device
-// atomic per kDynRounds rounds, waited for by that wave alone, half a chunk
-// ahead of its use).  (A per-wave claim one round ahead kept the claim in a
-// VGPR across the round: one spill, whose reload waits for every prefetch.)
-constexpr uint32_t kDynRounds = 16;
-constexpr uint32_t kDynSlots = 256;  // u64 slots in combine table 5's words after kPoolWord (unused here)
-template <bool SEEDED, bool DYN = false>
+template <bool SEEDED>
 __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, const uint4 *__restrict__ image,
                                                                   const uint32_t *ws) {
     // The class ranges [start k, count 4 + k): the sort's workspace header,
@@ -59,14 +47,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         return k < 4u ? (k <= c ? 0u : nn) : (k - 4u == c ? nn : 0u);
     };
     const bool ident = hostid || ws[kWsIdent] != 0u;  // sort_scatter skipped a one-key batch
-    uint64_t *const dslot = reinterpret_cast<uint64_t *>(&g_lds[kPoolWord + 2]);
-    uint32_t chunk0 = 0;
-    if (DYN && threadIdx.x == 0) chunk0 = atomicAdd(P.gpool, kDynRounds);
     stage_tables(image);
-    if (threadIdx.x == 0) {
-        g_lds[kPoolWord] = 0;
-        if (DYN) dslot[0] = (1ull << 32) | chunk0;
-    }
+    if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const Lut L = make_lut(lane);
@@ -132,27 +114,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         const uint64_t rrot = (LVK_CLASS3_FIRST && cls(6) && cls(7)) ? n23 / 4u : 0u;  // K = 4 entries per round
         const uint64_t s3 = cls(6) / 4u;
         auto pool = [&]() -> uint64_t {
-            uint64_t rho;
-            if constexpr (DYN) {
-                uint32_t k = 0;
-                if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
-                k = __builtin_amdgcn_readfirstlane(__shfl(k, 0));
-                const uint32_t c = k / kDynRounds, i = k % kDynRounds;
-                if (i == kDynRounds / 2 && lane == 0) {
-                    const uint32_t v = atomicAdd(P.gpool, kDynRounds);
-                    __hip_atomic_store(&dslot[(c + 1) % kDynSlots], (static_cast<uint64_t>(c + 2) << 32) | v,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                uint64_t sv;
-                while (((sv = __hip_atomic_load(&dslot[c % kDynSlots], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >>
-                        32) != c + 1u)
-                    __builtin_amdgcn_s_sleep(1);
-                rho = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(sv)) + i;
-            } else {
-                uint32_t k = 0;
-                if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
-                rho = blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
-            }
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
+            uint64_t rho = blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
             if (rho < rrot) {
                 rho += s3;
                 if (rho >= rrot) rho -= rrot;
@@ -626,13 +590,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, 
 namespace lvh {
 
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s) {
-    if (P.gpool && seeded)
-        hipLaunchKernelGGL((lvk::crc32c_classes_kernel<true, true>), dim3(static_cast<uint32_t>(c.cus)),
-                           dim3(lvk::kThreads), 0, s, P, c.image[2], ws);
-    else if (P.gpool)
-        hipLaunchKernelGGL((lvk::crc32c_classes_kernel<false, true>), dim3(static_cast<uint32_t>(c.cus)),
-                           dim3(lvk::kThreads), 0, s, P, c.image[2], ws);
-    else if (seeded)
+    if (seeded)
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<true>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0,
                            s, P, c.image[2], ws);
     else

@@ -258,34 +258,6 @@ int stream_gran(DevCtx &c, hipStream_t s, uint64_t **out) {
     return 0;
 }
 
-// The overlapped WAL scan's side streams: CU bits [0, kWalFrameCus) for the
-// framing, the rest for phase A (bit i is a logical CU; the driver spreads
-// consecutive bits over the XCDs and shader engines).
-int stream_side(DevCtx &c, hipStream_t s, WalSide **out) {
-    StreamWs *w = find_ws(c, s, true);
-    std::lock_guard<std::mutex> lk(w->em);
-    if (!w->side) {
-        std::unique_ptr<WalSide> sd(new WalSide);
-        const uint32_t cus = static_cast<uint32_t>(c.cus), words = (cus + 31) / 32;
-        std::vector<uint32_t> ma(words, 0), mf(words, 0);
-        for (uint32_t i = 0; i < cus; ++i) (i < kWalFrameCus ? mf : ma)[i / 32] |= 1u << (i % 32);
-        sd->masked = cus > 2 * kWalFrameCus && hipExtStreamCreateWithCUMask(&sd->st[0], words, ma.data()) == hipSuccess &&
-                     hipExtStreamCreateWithCUMask(&sd->st[1], words, mf.data()) == hipSuccess;
-        if (!sd->masked) {
-            (void)hipGetLastError();
-            if (sd->st[0]) (void)hipStreamDestroy(sd->st[0]);
-            sd->st[0] = nullptr;
-            LV_HIP(hipStreamCreateWithFlags(&sd->st[0], hipStreamNonBlocking));
-            LV_HIP(hipStreamCreateWithFlags(&sd->st[1], hipStreamNonBlocking));
-        }
-        for (auto &e : sd->ev) LV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        sd->cus_a = cus > 2 * kWalFrameCus ? cus - kWalFrameCus : cus;  // unmasked: the same grid, CUs left free
-        w->side = std::move(sd);
-    }
-    *out = w->side.get();
-    return 0;
-}
-
 // lv_crc32c_batch_check: read and clear the stream's violation word.
 int check_hints(hipStream_t s, uint32_t *violations) {
     if (violations) *violations = 0;

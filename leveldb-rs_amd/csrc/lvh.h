@@ -50,7 +50,6 @@ const std::vector<uint32_t> &host_image(int gi);
 // lookup through the last launch of a call, so one call's sort passes are
 // enqueued back to back and a growing hipFree never frees a buffer another
 // thread has been handed but not yet launched on.
-struct WalSide;
 struct StreamWs {
     std::mutex m;
     uint8_t *p = nullptr;
@@ -64,8 +63,6 @@ struct StreamWs {
     // (wal_pipe.hip), zeroed once when made; every launch leaves them zeroed
     // again (its last workgroup to retire clears them)
     uint64_t *gran = nullptr;
-    // the overlapped WAL scan's side streams (stream_side)
-    std::unique_ptr<WalSide> side;
 };
 
 struct DevCtx {
@@ -195,23 +192,6 @@ size_t wal_pipe_ws_bytes(uint64_t bytes, uint64_t cap);
 bool wal_pipe_applies(const DevCtx &c, uint64_t bytes);
 int launch_wal_pipe(DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
                     uint32_t *d_info, uint64_t cap, uint64_t *d_count, uint8_t *ws, hipStream_t s);
-// Phase A of the overlapped WAL scan (wal_pipe.hip, wal_pipe_kernel<true>):
-// whether `grid` workgroups can own a log of `bytes`, and the launch.
-bool wal_first_applies(uint64_t bytes, uint32_t grid);
-void launch_wal_first(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint32_t *crc_a, uint32_t grid,
-                      hipStream_t s);
-// The overlapped WAL scan's side streams of (device, stream s): [0] phase A
-// on all CUs but kWalFrameCus, [1] the framing kernels on those (CU masks;
-// plain streams if the runtime refuses a mask), three events, and the CUs
-// stream [0] has.  Made once per (device, stream).
-constexpr uint32_t kWalFrameCus = LVK_WAL_FRAME_CUS;
-struct WalSide {
-    hipStream_t st[2] = {nullptr, nullptr};
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    uint32_t cus_a = 0;
-    bool masked = false;
-};
-int stream_side(DevCtx &c, hipStream_t s, WalSide **out);
 // The persistent class kernel over a sorted list (classes.hip).
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s);
 // One group-size kernel over a batch, offsets or strided (blocks.hip).

@@ -332,9 +332,6 @@ struct Params {
     uint64_t htotal;  // the hint's total_bytes
     uint32_t hlen;    // the hint's max_len
     uint32_t huni;    // the hint's uniform word
-    // class kernel <DYN>: the rounds of classes 2+3 come from this device
-    // counter (zero at launch), so workgroups that start late take fewer
-    uint32_t *gpool;
 };
 
 // Geometry of one buffer [a, a+len) on the 16-B granule grid.  Batches of

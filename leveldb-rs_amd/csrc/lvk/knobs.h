@@ -53,9 +53,6 @@
     defined(LVK_WAL_PIPE_TRACE) || \
     defined(LVK_PIPE_AMIN) || \
     defined(LVK_PIPE_B_SMALL_FIRST) || \
-    defined(LVK_WAL_FRAME_CUS) || \
-    defined(LVK_CLASS_DYN) || \
-    defined(LVK_WAL_HIST_CACHE) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -174,15 +171,6 @@
 #endif
 #ifndef LVK_PIPE_AMIN  // WAL one-launch scan: smallest first-record unit walked in phase A (> 2048: class 2)
 #define LVK_PIPE_AMIN 2049
-#endif
-#ifndef LVK_CLASS_DYN  // class kernel after the sort: rounds of classes 2+3 in chunks from a device counter
-#define LVK_CLASS_DYN 0
-#endif
-#ifndef LVK_WAL_FRAME_CUS  // WAL overlapped scan: CUs of the framing stream (phase A gets the rest)
-#define LVK_WAL_FRAME_CUS 16
-#endif
-#ifndef LVK_WAL_HIST_CACHE  // WAL overlapped scan: headers per block wal_hist caches in LDS (the rest: stored in the hop)
-#define LVK_WAL_HIST_CACHE 16
 #endif
 #ifndef LVK_WAL_PIPE_TRACE  // timing only: wal_pipe_kernel writes s_memrealtime stamps per workgroup to its workspace
 #define LVK_WAL_PIPE_TRACE 0

@@ -32,7 +32,7 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
 
 // Sort workspace, 16-B aligned.  Header (u32 words): [0, 4) the long-buffer
 // split's piece and long-buffer counters and the batch's payload bytes (u64);
-// [4] the identity flag; [8] the class kernel's round counter (DYN); else unused to 256; [256, 264) class start x4, count x4; [264, 520) per-key
+// [4, 256) unused; [256, 264) class start x4, count x4; [264, 520) per-key
 // totals; [520, 528) unused.  Then the per-workgroup histogram matrix
 // M[wgs][256], the per-workgroup payload sums (u64), n + kPieceBudget sorted
 // 16-B entries (the pieces of split long buffers follow the n sorted ones),
@@ -42,7 +42,6 @@ constexpr uint32_t kWsPieces = 0;
 constexpr uint32_t kWsLongs = 1;
 constexpr uint32_t kWsBytes = 2;
 constexpr uint32_t kWsIdent = 4;  // 1: the sorted list is the identity (one key, no split): see sort_scatter
-constexpr uint32_t kWsPool = 8;   // the class kernel's device round counter (LVK_CLASS_DYN), zeroed by the histogram pass
 constexpr uint32_t kPieceBudget = 65536;  // piece entries per call (each split buffer takes <= kMaxPieces)
 constexpr uint32_t kMaxPieces = LVK_MAX_PIECES;
 constexpr uint32_t kPieceFlag = 0x80000000u;  // output slot flag of a piece entry (slot < kPieceBudget)

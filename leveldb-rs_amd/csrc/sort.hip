@@ -27,7 +27,6 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t *__rest
     if (blockIdx.x == 0 && t == 0) {  // counters of the long-buffer split (read by later launches)
         ws[kWsPieces] = 0;
         ws[kWsLongs] = 0;
-        ws[kWsPool] = 0;
     }
     uint64_t mybytes = 0;
     __syncthreads();
@@ -347,7 +346,6 @@ uint4 *launch_sort(uint8_t *ws_bytes, const uint64_t *off, const uint32_t *len, 
     P->tmp = reinterpret_cast<uint32_t *>(ws_bytes + lay.tmp);
     P->sseed = seed ? sseed : nullptr;
     P->part = longs ? part : nullptr;
-    P->gpool = LVK_CLASS_DYN ? ws + lvk::kWsPool : nullptr;
     return longs;
 }
 

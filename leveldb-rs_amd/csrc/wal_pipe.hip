@@ -262,10 +262,6 @@ __device__ __forceinline__ uint32_t pipe_order_key(uint32_t o) {
     return o < 64u ? 128u + o : o < 128u ? o : o < 192u ? o - 128u : o;
 }
 
-// FIRST (the overlapped scan, wal_scan.hip): phase A only -- no framers, no
-// look-back -- and each first record's CRC to a.crc[block] (the unsort kernel
-// merges them).
-template <bool FIRST>
 __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uint4 *__restrict__ image) {
     const uint32_t t = threadIdx.x, lane = t & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -343,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
     };
 
     // ---- 2. framer waves: the rest of every chain; the others: phase A ----
-    const uint32_t nframers = FIRST ? 0u : nblk > 64u ? 2u : 1u;
+    const uint32_t nframers = nblk > 64u ? 2u : 1u;
     if (wave < nframers) {
         const uint32_t fl = wave * 64u + lane;
         uint32_t touched = 0;
@@ -633,15 +629,6 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
     // ---- 4. every wave: phase A, then (after the flag) the phase-B lists ----
     walk_first();
     PTRACE(8 + wave);
-    if constexpr (FIRST) {
-        __syncthreads();
-        for (uint32_t bl = t; bl < nblk; bl += kThreads) {
-            const uint32_t r = g_lds[kPRecA + bl];
-            if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK && (r & 0xffffu) + 1u >= kPipeAMin)
-                a.crc[lo + bl] = g_lds[kPCrcA + bl];
-        }
-        return;
-    }
     while (__hip_atomic_load(&pctl(kCReady), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(16);
     PTRACE(24 + wave);
@@ -750,25 +737,8 @@ int launch_wal_pipe(DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d
     a.cap = cap;
     a.err = reinterpret_cast<uint32_t *>(ws + lay.err);
     a.trace = LVK_WAL_PIPE_TRACE ? reinterpret_cast<uint64_t *>(ws + lay.err + 16) : nullptr;
-    hipLaunchKernelGGL(lvk::wal_pipe_kernel<false>, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);
+    hipLaunchKernelGGL(lvk::wal_pipe_kernel, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);
     return 0;
-}
-
-bool wal_first_applies(uint64_t bytes, uint32_t grid) {
-    const uint64_t nblocks = (bytes + lvk::kPipeBlockSize - 1) / lvk::kPipeBlockSize;
-    return grid > 0 && nblocks >= grid && (nblocks + grid - 1) / grid <= lvk::kPipeMaxBlocks;
-}
-
-// Phase A of the overlapped scan: crc_a[b] = the CRC of block b's first record
-// when it is a unit of >= kPipeAMin bytes (other words untouched).
-void launch_wal_first(const DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint32_t *crc_a, uint32_t grid,
-                      hipStream_t s) {
-    lvk::WalPipe a{};
-    a.log = d_log;
-    a.size = bytes;
-    a.nblocks = (bytes + lvk::kPipeBlockSize - 1) / lvk::kPipeBlockSize;
-    a.crc = crc_a;
-    hipLaunchKernelGGL(lvk::wal_pipe_kernel<true>, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);
 }
 
 }  // namespace lvh

@@ -126,28 +126,17 @@ __device__ __forceinline__ uint32_t wal_touch(const uint8_t *log, uint64_t b0, u
 // 33 KiB of header cache) the 32,768 blocks of a 1 GiB log spread over 512
 // workgroups on all CUs; 256 threads (130 KiB each, one workgroup per CU)
 // left half the CUs idle and put two chains per SIMD.
-//
-// The overlapped scan (SKIPA): a block's first record of a unit >= kWalAMin
-// bytes is phase A's (wal_pipe_kernel<true>), so it is not counted into the
-// sort; and the kernel runs on kWalFrameCus CUs beside phase A, so it keeps
-// HC < kHdrCache headers per block in LDS (more workgroups per CU) and stores
-// the rest of the cache in the hop.  gpool: the class kernel's round counter,
-// zeroed here.
 constexpr uint32_t kWalHistThreads = 64;
-constexpr uint32_t kWalAMin = LVK_PIPE_AMIN;
-template <bool SKIPA = false, uint32_t HC = kHdrCache>
 __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__restrict__ log, uint64_t size,
                                                             uint64_t nblocks, uint64_t chunk,
                                                             uint32_t *__restrict__ M, uint64_t *__restrict__ wgrec,
                                                             uint32_t *__restrict__ blkcnt,
-                                                            uint64_t *__restrict__ hcache, uint32_t *gpool) {
+                                                            uint64_t *__restrict__ hcache) {
     constexpr uint32_t T = kWalHistThreads;
-    static_assert(HC <= kHdrCache, "LDS cache within the global one");
     __shared__ uint32_t h[kKeys + 64];  // + a dummy bin per lane (finished lanes)
     __shared__ uint64_t wsum[T / 64];
-    __shared__ uint64_t hcl[T * (HC + 1)];  // per-thread header cache
+    __shared__ uint64_t hcl[T * (kHdrCache + 1)];  // per-thread header cache
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    if (gpool && blockIdx.x == 0 && t == 0) *gpool = 0u;
     for (uint32_t k = t; k < kKeys; k += T) h[k] = 0;
     __syncthreads();
     const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < nblocks ? lo + chunk : nblocks;
@@ -163,7 +152,7 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         // global store in the hop (vmcnt counts stores too, in order) made
         // every hop's wait for its header load also wait for the previous
         // hop's store.
-        uint64_t *const hl = hcl + t * (HC + 1);  // stride HC + 1 words: lanes spread over the banks
+        uint64_t *const hl = hcl + t * (kHdrCache + 1);  // stride 65 words: lanes spread over the banks
         // Branch-free hop (round 3): every lane runs every instruction of the
         // loop body (no exec-mask branches) but the loads; the next header's
         // loads are issued right after the decode, and this record's
@@ -207,12 +196,9 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
             const uint32_t npos = pos + kWalHeader + len;
             const bool nact = active && ok && blen - npos >= kWalHeader;
             issue(npos, nact);
-            const uint32_t slot = active && cnt < HC ? cnt : HC;
+            const uint32_t slot = active && cnt < kHdrCache ? cnt : kHdrCache;
             hl[slot] = hdr_pack(pos, len, type);
-            if (HC < kHdrCache && active && cnt - HC < kHdrCache - HC)
-                hcache[b * kHdrCache + cnt] = hdr_pack(pos, len, type);
-            const bool skip = SKIPA && cnt == 0 && ok && len + 1u >= kWalAMin;  // phase A's
-            const uint32_t key = active && !skip ? sort_key(ok ? len + 1u : 0u) : kKeys + lane;
+            const uint32_t key = active ? sort_key(ok ? len + 1u : 0u) : kKeys + lane;
             __hip_atomic_fetch_add(&h[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             cnt += active ? 1u : 0u;
             pos = npos;
@@ -221,7 +207,7 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
         // (Writing the cache block by block with consecutive lanes -- one
         // contiguous run per block instead of 64 scattered 8-B stores per
         // step -- measured slower: 0.633 -> 0.622, profiles/r04/wal_hc/.)
-        for (uint32_t c = 0; c < cnt && c < HC; ++c) hcache[b * kHdrCache + c] = hl[c];
+        for (uint32_t c = 0; c < cnt && c < kHdrCache; ++c) hcache[b * kHdrCache + c] = hl[c];
         if (b < hi) blkcnt[b] = cnt;
         mine += cnt;
     }
@@ -247,10 +233,6 @@ struct WalOut {
     uint32_t *spos;  // each record's sorted position (wal_unsort), or null
 };
 
-// SKIPA: phase A's records (a block's first, unit >= kWalAMin) get no sorted
-// slot; their spos word is 1 << 31 | block (wal_unsort takes the CRC from
-// phase A's per-block array).
-template <bool SKIPA = false>
 __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__restrict__ log, uint64_t size,
                                                             uint64_t nblocks, uint64_t chunk, uint32_t *__restrict__ ws,
                                                             const uint32_t *__restrict__ M,
@@ -325,17 +307,15 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
                                                            : (r.type == 0 && r.len == 0 ? LV_WAL_REC_ZERO : LV_WAL_REC_OK);
                 r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
             }
-            const bool isa = SKIPA && rec && k == 0 && r.ulen >= kWalAMin;
-            const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec && !isa, lane);
+            const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
             if (rec) {
                 const uint64_t rid = run + q;  // log order: blocks in order, records in chain order
                 const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
-                if (!isa)
-                    ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
-                                           static_cast<uint32_t>(rid));
+                ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
+                                       static_cast<uint32_t>(rid));
                 o.hdr_off[rid] = start + pos;
                 o.info[rid] = r.type | (r.status << 8) | (r.len << 16);
-                if (o.spos) o.spos[rid] = isa ? 0x80000000u | static_cast<uint32_t>(bj) : slot;
+                if (o.spos) o.spos[rid] = slot;
             }
         }
         // blocks with more records than the cache holds walk on from there
@@ -378,18 +358,14 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
 // consecutive words); crc[rid] = tmp[spos[rid]] writes them in log order,
 // whole lines (scattered single-word stores from the class kernel cost the
 // offsets API's C2 ~35 us, profiles/r04/outstore/).
-// (crc_a: the overlapped scan's phase-A CRCs by block, for spos 1 << 31 | block.)
 __global__ __launch_bounds__(1024) void wal_unsort(const uint32_t *__restrict__ ws, const uint32_t *__restrict__ tmp,
                                                    const uint32_t *__restrict__ spos, uint32_t *__restrict__ crc,
-                                                   uint64_t cap, const uint32_t *__restrict__ crc_a) {
+                                                   uint64_t cap) {
     const uint64_t total = (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];  // records
     if (total > cap) return;  // nothing was written: the caller retries with a larger capacity
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride)
-    {
-        const uint32_t p = spos[i];
-        crc[i] = crc_a && (p >> 31) ? crc_a[p & 0x7fffffffu] : tmp[p];
-    }
+        crc[i] = tmp[spos[i]];
 }
 
 }  // namespace lvk
@@ -407,7 +383,7 @@ static uint64_t wal_wgs(uint64_t nblocks, uint64_t *chunk) {
 }
 
 struct WalWs {
-    size_t m, wgrec, blk, hc, ent, tmp, pos, crca, gpool, total;
+    size_t m, wgrec, blk, hc, ent, tmp, pos, total;
 };
 
 static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
@@ -423,17 +399,14 @@ static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
     // with LVK_WAL_UNSORT: the CRCs by sorted position and each record's sorted position
     w.tmp = w.ent + cap * sizeof(uint4);
     w.pos = w.tmp + (LVK_WAL_UNSORT ? al16(cap * sizeof(uint32_t)) : 0);
-    // the overlapped scan: phase A's CRCs by block, the class kernel's round counter
-    w.crca = w.pos + (LVK_WAL_UNSORT ? al16(cap * sizeof(uint32_t)) : 0);
-    w.gpool = w.crca + al16(nblocks * sizeof(uint32_t));
-    w.total = w.gpool + 16;
+    w.total = w.pos + (LVK_WAL_UNSORT ? al16(cap * sizeof(uint32_t)) : 0);
     return w;
 }
 
 static thread_local int g_wal_path = 0;  // lv_wal_scan_set_path
 
 int lv_wal_scan_set_path(int path) {
-    if (path < 0 || path > 3) return set_err(LV_ERR_INVALID, "path must be 0, 1, 2 or 3");
+    if (path < 0 || path > 2) return set_err(LV_ERR_INVALID, "path must be 0, 1 or 2");
     const int prev = g_wal_path;
     g_wal_path = path;
     return prev;
@@ -488,9 +461,18 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     uint64_t chunk = 0;
     const uint64_t wgs = wal_wgs(nblocks, &chunk);
     const dim3 g(static_cast<uint32_t>(wgs)), b(lvk::kSortThreads);
+    hipLaunchKernelGGL(lvk::wal_hist, g, dim3(lvk::kWalHistThreads), 0, s, d_log, static_cast<uint64_t>(bytes), nblocks,
+                       chunk, M, wgrec, blk, hc);
+    // (Round 3: claiming each workgroup's key runs with device atomics in
+    // wal_hist instead of this column scan -- a memset of the totals first --
+    // measured 0.6 % slower: the memset launch and wal_hist's returning
+    // atomics cost more than sort_scan, profiles/r03/wal2/atomic_totals/.)
+    launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgrec, s);
     uint32_t *tmp = LVK_WAL_UNSORT ? reinterpret_cast<uint32_t *>(wb + lay.tmp) : nullptr;
     uint32_t *spos = LVK_WAL_UNSORT ? reinterpret_cast<uint32_t *>(wb + lay.pos) : nullptr;
     lvk::WalOut o{d_hdr_off, d_info, d_count, cap, spos};
+    hipLaunchKernelGGL(lvk::wal_scatter, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws, M, wgrec,
+                       blk, hc, ent, o);
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(d_log);
     P.out = d_crc;
@@ -498,60 +480,11 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
     P.nplain = cap;
     P.ent = ent;
     P.tmp = tmp;
-    // The overlapped scan (path 3): phase A -- every block's first record of
-    // a unit > 2 KiB, 59 % of the bench log's bytes, known from one header
-    // read per block -- on all CUs but kWalFrameCus (wal_pipe_kernel<true>,
-    // a CU-masked side stream), while the framing kernels run on those
-    // (wal_hist<skip A> / sort_scan / wal_scatter<skip A>, the other side
-    // stream); the class kernel takes the rest of the records as soon as the
-    // framing is done, its workgroups starting as phase A's finish (rounds
-    // from a device counter), and wal_unsort merges both in log order.
-    WalSide *sd = nullptr;
-    if (g_wal_path == 3 && tmp) {
-        if (int rc = stream_side(*c, s, &sd)) return rc;
-        if (!wal_first_applies(bytes, sd->cus_a)) sd = nullptr;
-    }
-    if (sd) {
-        uint32_t *crca = reinterpret_cast<uint32_t *>(wb + lay.crca);
-        uint32_t *gpool = reinterpret_cast<uint32_t *>(wb + lay.gpool);
-        hipStream_t sa = sd->st[0], sf = sd->st[1];
-        LV_HIP(hipEventRecord(sd->ev[0], s));
-        LV_HIP(hipStreamWaitEvent(sa, sd->ev[0], 0));
-        LV_HIP(hipStreamWaitEvent(sf, sd->ev[0], 0));
-        launch_wal_first(*c, d_log, bytes, crca, sd->cus_a, sa);
-        LV_HIP(hipEventRecord(sd->ev[1], sa));
-        hipLaunchKernelGGL((lvk::wal_hist<true, LVK_WAL_HIST_CACHE>), g, dim3(lvk::kWalHistThreads), 0, sf, d_log,
-                           static_cast<uint64_t>(bytes), nblocks, chunk, M, wgrec, blk, hc, gpool);
-        launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgrec, sf);
-        hipLaunchKernelGGL(lvk::wal_scatter<true>, g, b, 0, sf, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws,
-                           M, wgrec, blk, hc, ent, o);
-        LV_HIP(hipEventRecord(sd->ev[2], sf));
-        LV_HIP(hipStreamWaitEvent(s, sd->ev[2], 0));
-        P.gpool = gpool;
-        launch_classes(*c, false, P, ws, s);
-        LV_HIP(hipStreamWaitEvent(s, sd->ev[1], 0));
-        if (cap)
-            hipLaunchKernelGGL(lvk::wal_unsort,
-                               dim3(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (cap + 1023) / 1024))), dim3(1024),
-                               0, s, ws, tmp, spos, d_crc, static_cast<uint64_t>(cap), crca);
-        g_kernel = "wal_pipe_kernel<first>|wal_hist+sort_scan+wal_scatter -> crc32c_classes_kernel<dyn>+wal_unsort";
-        return check_launch();
-    }
-    P.gpool = LVK_CLASS_DYN ? ws + lvk::kWsPool : nullptr;
-    hipLaunchKernelGGL(lvk::wal_hist<>, g, dim3(lvk::kWalHistThreads), 0, s, d_log, static_cast<uint64_t>(bytes), nblocks,
-                       chunk, M, wgrec, blk, hc, P.gpool);
-    // (Round 3: claiming each workgroup's key runs with device atomics in
-    // wal_hist instead of this column scan -- a memset of the totals first --
-    // measured 0.6 % slower: the memset launch and wal_hist's returning
-    // atomics cost more than sort_scan, profiles/r03/wal2/atomic_totals/.)
-    launch_sort_scan(M, static_cast<uint32_t>(wgs), ws, wgrec, s);
-    hipLaunchKernelGGL(lvk::wal_scatter<>, g, b, 0, s, d_log, static_cast<uint64_t>(bytes), nblocks, chunk, ws, M, wgrec,
-                       blk, hc, ent, o);
     launch_classes(*c, false, P, ws, s);
     g_kernel = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel";
     if (tmp && cap) {
         hipLaunchKernelGGL(lvk::wal_unsort, dim3(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (cap + 1023) / 1024))),
-                           dim3(1024), 0, s, ws, tmp, spos, d_crc, static_cast<uint64_t>(cap), nullptr);
+                           dim3(1024), 0, s, ws, tmp, spos, d_crc, static_cast<uint64_t>(cap));
         g_kernel = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel+wal_unsort";
     }
     return check_launch();

@@ -170,8 +170,7 @@ def scan_device(log, cap: int, workspace=None, stream=None):
 
 def set_scan_path(path: int) -> int:
     """Debug / test hook (lv_wal_scan_set_path): 0 auto, 1 the one-launch
-    scan, 2 the five-launch scan, 3 the overlapped scan (phase A beside the
-    framing); returns the previous setting."""
+    scan, 2 the five-launch scan; returns the previous setting."""
     rc = _bind().lv_wal_scan_set_path(path)
     if rc < 0:
         _err("lv_wal_scan_set_path")

@@ -147,17 +147,6 @@ def test_encode_then_scan_then_read(gpu):
 
 SORTED = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel"
 PIPE = "wal_pipe_kernel"
-OVL = "wal_pipe_kernel<first>|wal_hist+sort_scan+wal_scatter -> crc32c_classes_kernel<dyn>+wal_unsort"
-FRAME_CUS = 16  # LVK_WAL_FRAME_CUS
-
-
-def _overlapped_applies(nbytes):
-    """Path 3 (the overlapped scan) runs when every phase-A workgroup (all CUs
-    but the framing stream's) owns at least one block; otherwise the
-    five-launch scan does."""
-    import torch
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    return -(-nbytes // B) >= cus - FRAME_CUS
 
 
 def _check_scan_device(log, cap=None, shift=0):
@@ -176,9 +165,7 @@ def _check_scan_device(log, cap=None, shift=0):
     # reads nothing of the workspace it did not write first
     dirty = torch.full((LW.scan_workspace_bytes(len(log), cap),), 0xff, dtype=torch.uint8, device="cuda:0")
     try:
-        sorted_kern = SORTED + ("+wal_unsort" if cap else "")
-        ovl = OVL if cap else OVL.replace("+wal_unsort", "")
-        for path, kern in ((1, PIPE), (2, sorted_kern), (3, ovl if _overlapped_applies(len(log)) else sorted_kern)):
+        for path, kern in ((1, PIPE), (2, SORTED + ("+wal_unsort" if cap else ""))):
             LW.set_scan_path(path)
             for ws in (None, dirty):
                 hdr, crc, info, count = LW.scan_device(t, cap, workspace=ws)
@@ -256,16 +243,17 @@ def test_scan_device_capacity(gpu):
         _check_scan_device(tiny, cap=cap)
 
 
-def test_scan_device_overlapped(gpu):
-    """Path 3 (phase A on a CU-masked stream beside the framing kernels, then
-    the class kernel over the rest, merged by wal_unsort) on logs of >= 240
-    blocks: bench-like mixed records, corruption, truncation, a zero tail,
-    blocks of > 64 tiny records, every record a block's first (full
-    fragments), too small a capacity, an 8-B-aligned log."""
+def test_scan_device_large_logs(gpu):
+    """Both device paths on logs of a block per CU and more (every workgroup
+    of the one-launch scan owns blocks): bench-like mixed records,
+    corruption, truncation, a zero tail, every block's first record a
+    fragment, first records around the phase-A threshold (2,048 / 2,049-B
+    units) followed by > 64 tiny records, too small a capacity, an 8-B-aligned
+    log."""
     rng = np.random.default_rng(41)
     mixed = _random_records(rng, 2600, maxlog=16)
     log = bytearray(_oracle_encode(mixed, int(rng.integers(0, B))))
-    assert _overlapped_applies(len(log)), len(log)
+    assert len(log) >= 256 * B, len(log)
     _check_scan_device(bytes(log))
     _check_scan_device(bytes(log), shift=8)
     n = len(W.scan_log(bytes(log))[0])

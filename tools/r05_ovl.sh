@@ -18,6 +18,6 @@ for r in 1 2; do
   done
 done
 for f in "$out"/p*_*.json; do python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], d['roofline']['frac'], d['roofline']['ms_avg'], d.get('parity'))" "$f"; done
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$root/$out/prof" -o trace -- python3 "$root/bench.py" --wal-device --wal-path 3 --cpu-seconds 0 --steps 20 --warmup 5 > "$root/$out/prof.json" 2>> "$root/$out/err.txt" || exit 1
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof" -o trace -- python3 "$root/bench.py" --wal-device --wal-path 3 --cpu-seconds 0 --steps 20 --warmup 5 > "$root/$out/prof.json" 2>> "$root/$out/err.txt" || exit 1
 cd "$root" && find "$out/prof" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats_p3.csv" \; && find "$out/prof" -name "*kernel_trace.csv" -exec python3 tools/ovl_trace.py {} "$out/timeline_p3.txt" \; ; rm -rf "$out/prof"
 echo "all steps done"
