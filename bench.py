@@ -876,6 +876,16 @@ VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2.44
 SQ_VALU_SCALE = 1.0
 
 
+def hash_api_of(kernel_name):
+    """The hash API a hash_kernel<Meta> dispatch serves, by its template
+    argument (every variant's parameter list holds "unsigned int")."""
+    if "PackedMeta<unsigned int>" in kernel_name:
+        return "packed_u32"
+    if "PackedMeta<unsigned long>" in kernel_name:
+        return "packed_u64"
+    return "offsets"
+
+
 def measure_hash_valu(args):
     """Child process: rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES over a short hash
     run (kernel counters only).  Returns {kernel api: VALU instructions per
@@ -909,8 +919,7 @@ def measure_hash_valu(args):
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "")
                 if "hash_kernel" in name and row.get("Counter_Name") == "SQ_INSTS_VALU":
-                    api = "packed_u32" if "unsigned int" in name else "packed_u64" if "unsigned long" in name \
-                        else "offsets"
+                    api = hash_api_of(name)
                     per[api].append(float(row["Counter_Value"]))
     shutil.rmtree(out, ignore_errors=True)
     if not per:

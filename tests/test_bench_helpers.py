@@ -1,0 +1,41 @@
+"""bench.py's pure helpers (no GPU): the hash line's rooflines and the
+kernel-name classification its VALU pass uses."""
+import importlib.util
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("lvgpu_bench", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_hash_api_of_kernel_names():
+    """Every hash_kernel<Meta> variant's parameter list holds "unsigned int";
+    only the template argument tells the APIs apart (rocprofv3 names)."""
+    b = _bench()
+    sig = "(unsigned char const*, {m}, unsigned int*, unsigned int, unsigned int)"
+    assert b.hash_api_of("void lvh::hash_kernel<lvh::OffsetsMeta>" + sig.format(m="lvh::OffsetsMeta")) == "offsets"
+    m32 = "lvh::PackedMeta<unsigned int>"
+    assert b.hash_api_of(f"void lvh::hash_kernel<{m32}>" + sig.format(m=m32)) == "packed_u32"
+    m64 = "lvh::PackedMeta<unsigned long>"
+    assert b.hash_api_of(f"void lvh::hash_kernel<{m64}>" + sig.format(m=m64)) == "packed_u64"
+
+
+def test_hash_rooflines_pick_the_binding_bound():
+    b = _bench()
+    key, moved, ms = 600_000_000, 870_000_000, 0.14
+    roof, hbm, valu = b.hash_rooflines(key, ms, None, moved)
+    assert roof is hbm and valu is None and roof["bound"] == "hbm"
+    assert abs(hbm["frac"] - key / (ms * 1e-3) / 8e12) < 1e-3
+    assert abs(hbm["frac_all_bytes"] - moved / (ms * 1e-3) / 8e12) < 1e-3
+    # a VALU count far below the issue rate: HBM (all bytes) binds
+    roof, hbm, valu = b.hash_rooflines(key, ms, 1e6, moved)
+    assert roof is hbm and valu["frac"] < hbm["frac_all_bytes"]
+    # one at the issue peak: VALU binds
+    peak = b.VALU_SIMDS * b.VALU_CLOCK_HZ / b.VALU_CYCLES * ms * 1e-3
+    roof, hbm, valu = b.hash_rooflines(key, ms, peak, moved)
+    assert roof is valu and abs(valu["frac"] - 1.0) < 1e-3
