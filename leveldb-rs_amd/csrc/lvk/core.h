@@ -674,5 +674,7 @@ constexpr uint32_t kBaseMats = 48;
 // image, host_image(kTableImage)).
 constexpr uint32_t kSstRows = LVK_SST_ROWS;
 static_assert(kSstRows == 3 || kSstRows == 4, "table walk: 3 or 4 rows per batch");
+constexpr uint32_t kSealRows = LVK_SEAL_ROWS;  // the seal's rows per batch (4: on the G = 16 image)
+static_assert(kSealRows == kSstRows || kSealRows == 4, "seal: the table image's rows, or 4 on the G = 16 image");
 
 }  // namespace lvk

@@ -31,6 +31,7 @@
     defined(LVK_CLASS_STAGGER) || \
     defined(LVK_SEAL_FLUSH) || \
     defined(LVK_SST_ROWS) || \
+    defined(LVK_SEAL_ROWS) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_CLASS3_FIRST) || \
     defined(LVK_SMALL_ADAPT) || \
@@ -117,6 +118,9 @@
 #endif
 #ifndef LVK_SST_ROWS  // table walk rows per batch (round 4, verify with exact waits: 4 rows 0.69 vs 3 rows 0.71, profiles/r04/sst_rows/)
 #define LVK_SST_ROWS 3
+#endif
+#ifndef LVK_SEAL_ROWS  // the seal's rows per batch: LVK_SST_ROWS, or 4 on the G = 16 image
+#define LVK_SEAL_ROWS LVK_SST_ROWS
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

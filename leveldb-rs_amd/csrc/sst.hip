@@ -164,7 +164,8 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
         if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
         return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
     };
-    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), kSstRows>(P, src, lane, L, pool(), pool);
+    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), SEAL ? kSealRows : kSstRows>(P, src, lane, L, pool(),
+                                                                                          pool);
 }
 
 }  // namespace lvk
@@ -185,7 +186,9 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     if (seal) {
         lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
         g_kernel = "sst_blocks_kernel<seal>";
-        hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P, c->image[kTableImage], u);
+        // (4 rows per batch: Shift_1024 is the G = 16 image's own row shift)
+        hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P,
+                           c->image[lvk::kSealRows == 4 ? 2 : kTableImage], u);
     } else if (d_crc) {
         lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
         g_kernel = "sst_blocks_kernel<verify,crc>";
