@@ -32,7 +32,6 @@
     defined(LVK_SEAL_FLUSH) || \
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
-    defined(LVK_SMALL_INDEX_ORDER) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_CLASS3_FIRST) || \
     defined(LVK_SMALL_ADAPT) || \
@@ -122,9 +121,6 @@
 #endif
 #ifndef LVK_SEAL_ROWS  // the seal's rows per batch: LVK_SST_ROWS, or 4 on the G = 16 image
 #define LVK_SEAL_ROWS LVK_SST_ROWS
-#endif
-#ifndef LVK_SMALL_INDEX_ORDER  // length sort: classes 0 and 1 as one key each (index order, no batch buckets)
-#define LVK_SMALL_INDEX_ORDER 0
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

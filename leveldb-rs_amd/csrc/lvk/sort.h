@@ -27,7 +27,6 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     const uint32_t gu16 = 16u * (c >= 2 ? kAlRows : U) * (c == 0 ? 1u : c == 1 ? 4u : 16u);
     uint32_t nb = (len + gu16 - 1) / gu16;  // batches, ignoring start alignment
     nb = nb < kBuckets - 1 ? nb : kBuckets - 1;
-    if (LVK_SMALL_INDEX_ORDER && c <= 1u) nb = 0;  // one key per small class: its buffers in index order
     return c * kBuckets + (kBuckets - 1 - nb);
 }
 
