@@ -32,7 +32,6 @@
     defined(LVK_SEAL_FLUSH) || \
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
-    defined(LVK_WAL_KEY_AT) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_CLASS3_FIRST) || \
     defined(LVK_SMALL_ADAPT) || \
@@ -122,9 +121,6 @@
 #endif
 #ifndef LVK_SEAL_ROWS  // the seal's rows per batch: LVK_SST_ROWS, or 4 on the G = 16 image
 #define LVK_SEAL_ROWS LVK_SST_ROWS
-#endif
-#ifndef LVK_WAL_KEY_AT  // WAL framing: G = 16 classes keyed by their walk's exact batch count (unit address known)
-#define LVK_WAL_KEY_AT 0
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

@@ -30,21 +30,6 @@ __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     return c * kBuckets + (kBuckets - 1 - nb);
 }
 
-// sort_key of a unit whose address is known where the key is made (the WAL
-// framing: alo = the unit address's low 8 bits): a G = 16 class (>= 2) is
-// bucketed by the batch count its aligned-row walk will run -- rows on the
-// absolute 256-B grid (al_geo / round_nbw_al in walk.h) -- instead of
-// ceil(len / 1 KiB), so the four units of a round end in the same batch.
-__device__ __forceinline__ uint32_t sort_key_at(uint32_t len, uint32_t alo) {
-    const uint32_t c = len_class(len);
-    if (!LVK_WAL_KEY_AT || c < 2u) return sort_key(len);
-    const uint32_t ng = ((alo & 15u) + len) >> 4;        // whole granules from the 16-B base
-    const uint32_t row_e = (((alo >> 4) & 15u) + ng - 1u) >> 4;  // row of the last one
-    uint32_t nb = row_e / kAlRows + 1u;
-    nb = nb < kBuckets - 1 ? nb : kBuckets - 1;
-    return c * kBuckets + (kBuckets - 1 - nb);
-}
-
 // Sort workspace, 16-B aligned.  Header (u32 words): [0, 4) the long-buffer
 // split's piece and long-buffer counters and the batch's payload bytes (u64);
 // [4, 256) unused; [256, 264) class start x4, count x4; [264, 520) per-key

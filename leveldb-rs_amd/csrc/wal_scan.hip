@@ -198,8 +198,7 @@ __global__ __launch_bounds__(kWalHistThreads) void wal_hist(const uint8_t *__res
             issue(npos, nact);
             const uint32_t slot = active && cnt < kHdrCache ? cnt : kHdrCache;
             hl[slot] = hdr_pack(pos, len, type);
-            const uint32_t alo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(blk)) + pos + 6u;  // [type || payload]
-            const uint32_t key = active ? sort_key_at(ok ? len + 1u : 0u, alo) : kKeys + lane;
+            const uint32_t key = active ? sort_key(ok ? len + 1u : 0u) : kKeys + lane;
             __hip_atomic_fetch_add(&h[key], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             cnt += active ? 1u : 0u;
             pos = npos;
@@ -308,11 +307,10 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
                                                            : (r.type == 0 && r.len == 0 ? LV_WAL_REC_ZERO : LV_WAL_REC_OK);
                 r.ulen = r.status == LV_WAL_REC_OK ? r.len + 1 : 0u;
             }
-            const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
-            const uint32_t alo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(log) + ua);
-            const uint32_t slot = wave_claim(cur, sort_key_at(r.ulen, alo), rec, lane);
+            const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
             if (rec) {
                 const uint64_t rid = run + q;  // log order: blocks in order, records in chain order
+                const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
                 ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
                                        static_cast<uint32_t>(rid));
                 o.hdr_off[rid] = start + pos;
@@ -337,10 +335,9 @@ __global__ __launch_bounds__(kSortThreads) void wal_scatter(const uint8_t *__res
                 WalRec r{};
                 const bool rec = active;
                 if (active) r = wal_record(log, size, start, blen, pos);
-                const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
-                const uint32_t alo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(log) + ua);
-                const uint32_t slot = wave_claim(cur, sort_key_at(r.ulen, alo), rec, lane);
+                const uint32_t slot = wave_claim(cur, sort_key(r.ulen), rec, lane);
                 if (rec) {
+                    const uint64_t ua = start + pos + 6;  // [type || payload], log_reader.rs:336
                     ent[slot] = make_uint4(static_cast<uint32_t>(ua), static_cast<uint32_t>(ua >> 32), r.ulen,
                                            static_cast<uint32_t>(rid));
                     o.hdr_off[rid] = start + pos;
