@@ -152,8 +152,8 @@ PIPE = "wal_pipe_kernel"
 def _check_scan_device(log, cap=None, shift=0):
     """shift: the log's offset from a 16-B boundary (the scan needs 8-B
     alignment).  Both device paths (lv_wal_scan_set_path): the one-launch
-    scan (every workgroup frames, sorts and checksums its own blocks, the
-    default) and the five-launch one (global length sort)."""
+    scan (every workgroup frames, sorts and checksums its own blocks) and the
+    five-launch one (global length sort, the default)."""
     import lvgpu
     import lvgpu.wal as LW
     import torch
