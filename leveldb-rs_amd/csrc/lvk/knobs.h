@@ -54,7 +54,6 @@
     defined(LVK_WAL_PIPE_TRACE) || \
     defined(LVK_PIPE_AMIN) || \
     defined(LVK_PIPE_B_SMALL_FIRST) || \
-    defined(LVK_PIPE_PIECE) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -173,9 +172,6 @@
 #endif
 #ifndef LVK_PIPE_B_SMALL_FIRST  // WAL one-launch scan: phase B walks classes 1, 0 before class 2
 #define LVK_PIPE_B_SMALL_FIRST 0
-#endif
-#ifndef LVK_PIPE_PIECE  // WAL one-launch scan: phase-A first records walked as pieces of this many bytes (0: whole)
-#define LVK_PIPE_PIECE 0
 #endif
 #ifndef LVK_PIPE_AMIN  // WAL one-launch scan: smallest first-record unit walked in phase A (> 2048: class 2)
 #define LVK_PIPE_AMIN 2049

@@ -61,27 +61,15 @@ constexpr uint32_t kPipeHeader = 7;         // log_format.rs:66
 constexpr uint32_t kPipeMaxBlocks = 1024;   // blocks per workgroup (the LDS block tables)
 constexpr uint32_t kPipeCache = 64;         // headers per block in the global header cache
 constexpr uint32_t kPipeAMin = LVK_PIPE_AMIN;  // phase A: first records of units >= this (class 2: > 2 KiB)
-// Phase-A pieces (LVK_PIPE_PIECE = kPipePiece bytes, 0: whole units): a first
-// record longer than kPipePiece is walked as up to kPipePieces pieces, the
-// last ones exactly kPipePiece bytes and the first the rest, each by its own
-// group, so a round of four long units no longer holds a wave for ~80 us;
-// the pieces' raw registers are joined at the end by Shift_{j kPipePiece}
-// (the base byte tables, DevCtx::base_tabs).
-constexpr uint32_t kPipePiece = LVK_PIPE_PIECE;
-constexpr uint32_t kPipePieces = kPipePiece ? 4u : 1u;
-static_assert(kPipePiece == 0 || kPipePiece == 8192, "pieces of 8 KiB: joined by Shift_8192 / Shift_16384");
-__device__ __forceinline__ uint32_t pipe_npieces(uint32_t ulen) {
-    return kPipePiece ? (ulen + kPipePiece - 1) / kPipePiece : 1u;  // <= 4: a unit is <= 32,762 B
-}
 
 // Region B carve-out (word offsets into g_lds).
 constexpr uint32_t kPB = kRegionB / 4;
 constexpr uint32_t kPCnt = kPB;                          // records per block
 constexpr uint32_t kPPre = kPCnt + kPipeMaxBlocks;       // exclusive prefix of kPCnt
 constexpr uint32_t kPRecA = kPPre + kPipeMaxBlocks;      // first record: len | type << 16 | status << 24, ~0 none
-constexpr uint32_t kPCrcA = kPRecA + kPipeMaxBlocks;     // phase-A CRCs by block (pieces: raw registers by block * 4 + piece)
-constexpr uint32_t kPSortA = kPCrcA + kPipePieces * kPipeMaxBlocks;  // phase-A list: block | piece << 10, longest first
-constexpr uint32_t kPHist = kPSortA + kPipePieces * kPipeMaxBlocks;  // phase-B key counts, then cursors
+constexpr uint32_t kPCrcA = kPRecA + kPipeMaxBlocks;     // phase-A CRCs by block
+constexpr uint32_t kPSortA = kPCrcA + kPipeMaxBlocks;    // phase-A list: block indices, longest first
+constexpr uint32_t kPHist = kPSortA + kPipeMaxBlocks;    // phase-B key counts, then cursors
 constexpr uint32_t kPHistA = kPHist + kKeys;             // phase-A bucket counts, then cursors
 constexpr uint32_t kPCtl = kPHistA + 64;                 // control words (below)
 constexpr uint32_t kPStage = kPCtl + 64;                 // CRCs by local record index
@@ -117,7 +105,6 @@ struct WalPipe {
     uint64_t *count;
     uint64_t cap;
     uint32_t *err;  // set when a workgroup's count never arrived (bounded poll)
-    const uint32_t *tabs;  // Shift_{2^i} byte tables (DevCtx::base_tabs): the phase-A pieces' join
     uint64_t *trace;  // LVK_WAL_PIPE_TRACE: kPipeTrace s_memrealtime stamps per workgroup
 };
 
@@ -147,32 +134,20 @@ struct PipeFirst {
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
         const uint32_t i = static_cast<uint32_t>(valid ? e : P.n - 1);
-        const uint32_t v = g_lds[kPSortA + i];
-        const uint32_t bl = v & (kPipeMaxBlocks - 1u);
+        const uint32_t bl = g_lds[kPSortA + i];
         const uint32_t r = g_lds[kPRecA + bl];
-        const uint32_t ulen = (r & 0xffffu) + 1u;
         RGeo q;
         q.a = blk0 + static_cast<uint64_t>(bl) * kPipeBlockSize + 6u;  // [type || payload], log_reader.rs:336
-        q.len = ulen;
+        q.len = (r & 0xffffu) + 1u;
         q.seed = 0;
         q.bid = valid ? bl : 0xffffffffu;
-        if constexpr (kPipePiece != 0) {
-            // piece k of np: the first (ulen - (np - 1) kPipePiece bytes, with
-            // the seed) or one of the last np - 1 of kPipePiece (raw from 0)
-            const uint32_t k = v >> 10, np = pipe_npieces(ulen);
-            const uint32_t first = ulen - (np - 1u) * kPipePiece;
-            q.a += k ? first + (k - 1u) * kPipePiece : 0u;
-            q.len = k ? kPipePiece : first;
-            q.seed = k ? 0xffffffffu : 0u;  // R(~seed, .): the zero register
-            q.bid = valid ? bl * kPipePieces + k : 0xffffffffu;
-        }
         q.aux = 0;
         return q;
     }
     __device__ __forceinline__ uint2 trailer(const RGeo &, uint32_t) const { return make_uint2(0, 0); }
     __device__ __forceinline__ void stage(const Params &, uint32_t, uint32_t, const RGeo &q, uint32_t X,
                                           uint2) const {
-        if (q.bid != 0xffffffffu) g_lds[kPCrcA + q.bid] = kPipePiece ? X : ~X;  // pieces: the raw register
+        if (q.bid != 0xffffffffu) g_lds[kPCrcA + q.bid] = ~X;
     }
     __device__ __forceinline__ void flush(const Params &, uint32_t, uint32_t, uint32_t) const {}
 };
@@ -317,12 +292,7 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
             const uint32_t st = pipe_status(len, type, blen1, 0);
             r = len | (type << 16) | (st << 24);
             const uint32_t ulen = st == LV_WAL_REC_OK ? len + 1u : 0u;
-            if (ulen >= kPipeAMin && kPipePiece != 0) {
-                // the pieces' keys: the first piece's length, then np - 1 of kPipePiece
-                const uint32_t np = pipe_npieces(ulen), first = ulen - (np - 1u) * kPipePiece;
-                atomicAdd(&g_lds[kPHistA + (sort_key(first > kPipeAMin ? first : kPipeAMin) & 63u)], 1u);
-                if (np > 1u) atomicAdd(&g_lds[kPHistA + (sort_key(kPipePiece) & 63u)], np - 1u);
-            } else if (ulen >= kPipeAMin)
+            if (ulen >= kPipeAMin)
                 atomicAdd(&g_lds[kPHistA + (sort_key(ulen) & 63u)], 1u);
             else
                 atomicAdd(&g_lds[kPHist + sort_key(ulen)], 1u);
@@ -345,19 +315,8 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
     if (t < nblk) {
         const uint32_t r = g_lds[kPRecA + t];
         if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK && (r & 0xffffu) + 1u >= kPipeAMin) {
-            const uint32_t ulen = (r & 0xffffu) + 1u;
-            if constexpr (kPipePiece != 0) {
-                const uint32_t np = pipe_npieces(ulen), first = ulen - (np - 1u) * kPipePiece;
-                const uint32_t slot = atomicAdd(&g_lds[kPHistA + (sort_key(first > kPipeAMin ? first : kPipeAMin) & 63u)], 1u);
-                g_lds[kPSortA + slot] = t;
-                if (np > 1u) {
-                    const uint32_t s1 = atomicAdd(&g_lds[kPHistA + (sort_key(kPipePiece) & 63u)], np - 1u);
-                    for (uint32_t k = 1; k < np; ++k) g_lds[kPSortA + s1 + k - 1u] = t | (k << 10);
-                }
-            } else {
-                const uint32_t slot = atomicAdd(&g_lds[kPHistA + (sort_key(ulen) & 63u)], 1u);
-                g_lds[kPSortA + slot] = t;
-            }
+            const uint32_t slot = atomicAdd(&g_lds[kPHistA + (sort_key((r & 0xffffu) + 1u) & 63u)], 1u);
+            g_lds[kPSortA + slot] = t;
         }
     }
     __syncthreads();
@@ -713,25 +672,10 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
         const uint32_t r = g_lds[kPRecA + bl];
         if (r != 0xffffffffu && (r >> 24) == LV_WAL_REC_OK && (r & 0xffffu) + 1u >= kPipeAMin) {
             const uint32_t li = g_lds[kPPre + bl];
-            uint32_t c = g_lds[kPCrcA + bl * kPipePieces];
-            if constexpr (kPipePiece != 0) {
-                // R(~0, p0 || p1 || ...) = sum_k Shift_{(np - 1 - k) 8 KiB}(X_k):
-                // Shift_8192 / Shift_16384 are base tables 13 / 14
-                const uint32_t np = pipe_npieces((r & 0xffffu) + 1u);
-                uint32_t raw = g_lds[kPCrcA + bl * kPipePieces + np - 1u];
-                for (uint32_t k = 0; k + 1u < np; ++k) {
-                    const uint32_t d = np - 1u - k;  // 8 KiB units after piece k: 1..3
-                    uint32_t x = g_lds[kPCrcA + bl * kPipePieces + k];
-                    if (d & 1u) x = tab_shift(a.tabs + 13u * 1024u, x);
-                    if (d & 2u) x = tab_shift(a.tabs + 14u * 1024u, x);
-                    raw ^= x;
-                }
-                c = ~raw;
-            }
             if (li < kPStageN)
-                g_lds[kPStage + li] = c;
+                g_lds[kPStage + li] = g_lds[kPCrcA + bl];
             else
-                crc[li] = c;
+                crc[li] = g_lds[kPCrcA + bl];
         }
     }
     __syncthreads();
@@ -792,7 +736,6 @@ int launch_wal_pipe(DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d
     a.count = d_count;
     a.cap = cap;
     a.err = reinterpret_cast<uint32_t *>(ws + lay.err);
-    a.tabs = c.base_tabs;
     a.trace = LVK_WAL_PIPE_TRACE ? reinterpret_cast<uint64_t *>(ws + lay.err + 16) : nullptr;
     hipLaunchKernelGGL(lvk::wal_pipe_kernel, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);
     return 0;
