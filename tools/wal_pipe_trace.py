@@ -42,6 +42,7 @@ log = np.empty(need.value, dtype=np.uint8)
 assert L.lv_wal_encode_host(payload.ctypes.data, offs.ctypes.data, sizes.ctypes.data, sizes.size, 0,
                             log.ctypes.data, log.size, ctypes.byref(need), 0) == 0
 d_log = torch.from_numpy(log).to("cuda:0")
+LW.set_scan_path(1)  # the one-launch scan (the library's default is the five-launch one)
 _, _, _, count = LW.scan_device(d_log, 0)
 torch.cuda.synchronize()
 cap = int(count.item())
