@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 5, final check on the shipped tree: the whole GPU suite, smoke, and
-# the driver's default bench line.  usage: tools/r05_final.sh OUTDIR
+# Final check on the shipped tree: the whole GPU suite, smoke, and
+# the driver's default bench line.  usage: tools/final_check.sh OUTDIR
 set -o pipefail
-out=${1:-gpurun_out/r05final}
+out=${1:-gpurun_out/final}
 root=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$root" && mkdir -p "$out"
 export TMPDIR=/tmp
