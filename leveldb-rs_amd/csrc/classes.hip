@@ -592,10 +592,10 @@ namespace lvh {
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s) {
     if (seeded)
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<true>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads), 0,
-                           s, P, c.image[2], ws);
+                           s, P, c.image[kAlImage], ws);
     else
         hipLaunchKernelGGL(lvk::crc32c_classes_kernel<false>, dim3(static_cast<uint32_t>(c.cus)), dim3(lvk::kThreads),
-                           0, s, P, c.image[2], ws);
+                           0, s, P, c.image[kAlImage], ws);
 }
 
 // ---- the batch hint (lv_crc32c_batch_device_hint) ----
@@ -684,10 +684,10 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
         g_kernel = join ? "crc32c_fused_small_kernel+combine_long_kernel" : "crc32c_fused_small_kernel";
         if (seed)
             hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<true>, dim3(static_cast<uint32_t>(c.cus)),
-                               dim3(lvk::kThreads), 0, s, P, c.image[2], ws, longs);
+                               dim3(lvk::kThreads), 0, s, P, c.image[kAlImage], ws, longs);
         else
             hipLaunchKernelGGL(lvk::crc32c_fused_small_kernel<false>, dim3(static_cast<uint32_t>(c.cus)),
-                               dim3(lvk::kThreads), 0, s, P, c.image[2], ws, longs);
+                               dim3(lvk::kThreads), 0, s, P, c.image[kAlImage], ws, longs);
     } else {
         // sorted path: the join launch also unsorts the class kernel's CRCs
         // (combine_long_kernel), so it always runs

@@ -38,6 +38,13 @@ constexpr int kGs[4] = {1, 4, 16, 64};
 // The table walk's image: the G = 16 one with region A's row shift
 // Shift_{256 kSstRows} (Shift_768 for three-row batches).
 constexpr int kTableImage = 4;
+// The image of the G = 16 aligned-row walks over length-sorted lists (class,
+// fused and one-launch WAL kernels): region A's row shift is Shift_{256 *
+// kAlRows} -- the G = 16 image's Shift_1024, or the table image's Shift_768
+// (kSstRows = 3) for 3 rows per batch.
+constexpr uint32_t kAlRowsH = LVK_ALIGNED_ROWS ? LVK_AL_ROWS : lvk::U;  // = lvk::kAlRows (lvk/sort.h)
+constexpr int kAlImage = kAlRowsH == 4 ? 2 : kTableImage;
+static_assert(kAlRowsH == 4 || kAlRowsH == lvk::kSstRows, "aligned rows: 4, or the table image's");
 constexpr int kImages = 5;
 
 // Host copy of the LDS image for each G (index into kGs), and the table

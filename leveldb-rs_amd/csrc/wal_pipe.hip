@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
     auto walk_first = [&]() {
         Params P{};
         P.n = nA;
-        sorted_stream<16>(P, PipeFirst{blk0}, lane, L, nextA(), nextA);
+        sorted_stream<16, PipeFirst, decltype(nextA), 4>(P, PipeFirst{blk0}, lane, L, nextA(), nextA);  // (plain merge: 4 rows)
     };
 
     // ---- 2. framer waves: the rest of every chain; the others: phase A ----
@@ -651,10 +651,10 @@ __global__ __launch_bounds__(kThreads) void wal_pipe_kernel(WalPipe a, const uin
             P.n = n1;
             sorted_stream<1>(P, r1, lane, L, next1(), next1);
             P.n = n16;
-            sorted_stream<16>(P, r16, lane, L, next16(), next16);
+            sorted_stream<16, PipeRest, decltype(next16), 4>(P, r16, lane, L, next16(), next16);
         } else {
             P.n = n16;
-            sorted_stream<16>(P, r16, lane, L, next16(), next16);
+            sorted_stream<16, PipeRest, decltype(next16), 4>(P, r16, lane, L, next16(), next16);
             P.n = n4;
             sorted_stream<4>(P, r4, lane, L, next4(), next4);
             P.n = n1;
@@ -737,7 +737,7 @@ int launch_wal_pipe(DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d
     a.cap = cap;
     a.err = reinterpret_cast<uint32_t *>(ws + lay.err);
     a.trace = LVK_WAL_PIPE_TRACE ? reinterpret_cast<uint64_t *>(ws + lay.err + 16) : nullptr;
-    hipLaunchKernelGGL(lvk::wal_pipe_kernel, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);
+    hipLaunchKernelGGL(lvk::wal_pipe_kernel, dim3(grid), dim3(lvk::kThreads), 0, s, a, c.image[2]);  // 4-row batches (merge_al<4, PLAIN>)
     return 0;
 }
 
