@@ -79,6 +79,11 @@ def main():
         for k in ("packed_u64", "packed_u32"):
             if k in h:
                 note += f"; {k} {h[k]['ms_avg'] * 1e3:.1f} us, frac {h[k]['roofline']['frac']}"
+        hb = h.get("roofline_hbm") or {}
+        if "frac_all_bytes" in hb:
+            note += f"; all bytes moved frac {hb['frac_all_bytes']}"
+        if h.get("roofline_valu"):
+            note += f"; VALU issue frac {h['roofline_valu']['frac']}"
         if h.get("cpu_baseline"):
             note += f"; cpu {h['cpu_baseline']['value']} Gkeys/s (1 core)"
         rows.append(f"| hash (key bytes) | {h['ms_avg'] * 1e3:.1f} us, frac {fr} | - | {note} |")
