@@ -48,7 +48,6 @@
     defined(LVK_PIPE_CHUNK_MB) || \
     defined(LVK_MEMCPY_THREADS) || \
     defined(LVK_PIPE_COPY_THREADS) || \
-    defined(LVK_PIPE_EARLY_FIRST) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
     defined(LVK_WAL_LOCAL) || \
@@ -164,9 +163,6 @@
 #endif
 #ifndef LVK_PIPE_COPY_THREADS  // host: the same in the pipelined WAL scan's worker (a Reader runs beside it)
 #define LVK_PIPE_COPY_THREADS 4
-#endif
-#ifndef LVK_PIPE_EARLY_FIRST  // host: the pipelined WAL scan publishes chunk 0 before copying chunk 1
-#define LVK_PIPE_EARLY_FIRST 1
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8

@@ -712,10 +712,6 @@ int pipe_run(lvgpu_internal::ScanPipe *p, const uint8_t *log, size_t bytes, int 
     };
     const size_t nch = p->chunks.size();
     int rc = LV_OK;
-    // Chunk 0 is collected and published before chunk 1 is copied, so the
-    // Reader starts one chunk copy earlier (it is the slower stage from then
-    // on); every later chunk k - 1 is collected after chunk k's copy, whose
-    // CPU time covers k - 1's upload and scan.
     for (size_t k = 0; k < nch && !rc; ++k) {
         PipeSlot &sl = slot[k & 1];
         sl.lo = k * kPipeChunk;
@@ -723,14 +719,9 @@ int pipe_run(lvgpu_internal::ScanPipe *p, const uint8_t *log, size_t bytes, int 
         const uint64_t nblocks = (sl.len + LV_WAL_BLOCK_SIZE - 1) / LV_WAL_BLOCK_SIZE;
         sl.cap = std::max<uint64_t>(sl.len / 256, nblocks * 8);
         rc = pipe_enqueue(sl, log, pinned);
-        if (rc) break;
-        const size_t done = LVK_PIPE_EARLY_FIRST && k == 0 ? 0 : k - 1;  // the chunk to collect now (k - 1; 0 at once)
-        if ((k > 0 || LVK_PIPE_EARLY_FIRST) && !(LVK_PIPE_EARLY_FIRST && k == 1) &&
-            !(rc = pipe_finish(slot[done & 1], &p->chunks[done])))
-            publish(done);
+        if (!rc && k > 0 && !(rc = pipe_finish(slot[(k - 1) & 1], &p->chunks[k - 1]))) publish(k - 1);
     }
-    if (!rc && (nch > 1 || !LVK_PIPE_EARLY_FIRST) && !(rc = pipe_finish(slot[(nch - 1) & 1], &p->chunks[nch - 1])))
-        publish(nch - 1);
+    if (!rc && !(rc = pipe_finish(slot[(nch - 1) & 1], &p->chunks[nch - 1]))) publish(nch - 1);
     // nothing of this scan is still reading the staging slots or scratch
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->stream2);
