@@ -92,9 +92,6 @@ def parse():
     p.add_argument("--long", action="store_true",
                    help="few long buffers through both device APIs (1,024 x 64 KiB, 64 x 16 MiB, 16 x 1 MiB, "
                         "1 x 16 MiB); one JSON line")
-    p.add_argument("--wal-path", type=int, default=0, choices=[0, 1, 2],
-                   help="--wal-device: lv_wal_scan_set_path (0 the library's choice, 1 the one-launch scan, "
-                        "2 the five-launch one)")
     p.add_argument("--wal-device", action="store_true",
                    help="SURVEY 8f row 1 in HBM: lv_wal_scan_device (framing + CRC) of a ~1 GiB log already on "
                         "the GPU; one JSON line with a roofline")
@@ -670,8 +667,6 @@ def wal_device_bench(args):
         raise SystemExit("encode failed: " + lvgpu.lib().lv_last_error().decode())
     del payload
     d_log = torch.from_numpy(log).to(dev)
-    if args.wal_path:
-        LW.set_scan_path(args.wal_path)
     # capacity from a first scan (a caller learns its log's record count once)
     _, _, _, count = LW.scan_device(d_log, 0)
     torch.cuda.synchronize()

@@ -54,21 +54,12 @@ int lv_wal_scan_wait(lv_wal_scan *scan);
  * host synchronisation: every 32 KiB block's header chain is walked as
  * read_physical_record frames it and every [type || payload] unit is
  * checksummed, in five launches on `stream` (framing, one global length sort,
- * the CRC kernel, the log-order write-back) -- or, with
- * lv_wal_scan_set_path(1), in one launch (every workgroup frames, sorts and
- * checksums its own blocks).  Records go to d_hdr_off / d_crc /
+ * the CRC kernel, the log-order write-back).  Records go to d_hdr_off / d_crc /
  * d_info in log order (the lv_wal_scan arrays below), at most `cap` of them;
  * *d_count (device memory) receives the number of records.  If that number
  * exceeds cap, nothing else is written: call again with a larger capacity.
- * (UINT64_MAX: the one-launch scan's workgroups could not all run at once --
- * another kernel held compute units for ~0.2 s; nothing was written.)
  * d_workspace: >= lv_wal_scan_workspace_bytes(bytes, cap) bytes, 16-B aligned. */
 size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap);
-/* Debug / test hook (calling thread): 0 (default) and 2 run the five-launch
- * scan, 1 the one-launch scan (LV_ERR_INVALID from the scan where it does
- * not apply: more than 1,024 blocks per compute unit).
- * Returns the previous setting, or LV_ERR_INVALID for another value. */
-int lv_wal_scan_set_path(int path);
 int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
                        size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream);
 /* Number of physical records reached by the blocks' header chains (a

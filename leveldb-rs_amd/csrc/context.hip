@@ -245,19 +245,6 @@ int stream_err(DevCtx &c, hipStream_t s, uint32_t **out) {
     return 0;
 }
 
-int stream_gran(DevCtx &c, hipStream_t s, uint64_t **out) {
-    StreamWs *w = find_ws(c, s, true);
-    std::lock_guard<std::mutex> lk(w->em);
-    if (!w->gran) {
-        constexpr size_t kBytes = kWalSyncWords * sizeof(uint64_t);
-        LV_HIP(hipMalloc(&w->gran, kBytes));
-        counters().allocs++;
-        LV_HIP(hipMemsetAsync(w->gran, 0, kBytes, s));
-    }
-    *out = w->gran;
-    return 0;
-}
-
 // lv_crc32c_batch_check: read and clear the stream's violation word.
 int check_hints(hipStream_t s, uint32_t *violations) {
     if (violations) *violations = 0;

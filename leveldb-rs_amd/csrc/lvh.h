@@ -38,8 +38,8 @@ constexpr int kGs[4] = {1, 4, 16, 64};
 // The table walk's image: the G = 16 one with region A's row shift
 // Shift_{256 kSstRows} (Shift_768 for three-row batches).
 constexpr int kTableImage = 4;
-// The image of the G = 16 aligned-row walks over length-sorted lists (class,
-// fused and one-launch WAL kernels): region A's row shift is Shift_{256 *
+// The image of the G = 16 aligned-row walks over length-sorted lists (class
+// and fused kernels): region A's row shift is Shift_{256 *
 // kAlRows} -- the G = 16 image's Shift_1024, or the table image's Shift_768
 // (kSstRows = 3) for 3 rows per batch.
 constexpr uint32_t kAlRowsH = LVK_ALIGNED_ROWS ? LVK_AL_ROWS : lvk::U;  // = lvk::kAlRows (lvk/sort.h)
@@ -66,10 +66,6 @@ struct StreamWs {
     std::mutex em;
     uint32_t *err = nullptr;
     uint32_t *herr = nullptr;
-    // the one-launch WAL scan's count granules and retire counter
-    // (wal_pipe.hip), zeroed once when made; every launch leaves them zeroed
-    // again (its last workgroup to retire clears them)
-    uint64_t *gran = nullptr;
 };
 
 struct DevCtx {
@@ -106,7 +102,6 @@ struct DevCtx {
 };
 
 constexpr size_t kStageBytes = 64ull << 20;  // pinned staging slot for pageable input
-constexpr size_t kWalSyncWords = 1024 + 2;  // the WAL scan's per-stream count granules + retire counter (u64 words)
 
 // lv_device_counters: per-device host-path traffic and allocations
 struct DevCounters {
@@ -167,8 +162,6 @@ inline void set_hint(lvk::Params &P, const HintCheck *hc, uint32_t dflt_len) {
 }
 // The violation word of (device, stream), allocated and zeroed on first use.
 int stream_err(DevCtx &c, hipStream_t s, uint32_t **out);
-// The stream's WAL-scan count granules (kWalSyncWords, made and zeroed on the stream once).
-int stream_gran(DevCtx &c, hipStream_t s, uint64_t **out);
 // Reads and clears the current device's violation word of stream s.
 int check_hints(hipStream_t s, uint32_t *violations);
 
@@ -192,13 +185,6 @@ int launch_binned(DevCtx &c, uint8_t *ws_bytes, const uint8_t *arena, const uint
 // Whether a batch with these host-side facts needs the long-buffer join
 // (lv_crc32c_batch_device_hint; classes.hip).
 bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus);
-// The one-launch device WAL scan (wal_pipe.hip): workspace bytes, whether a
-// log of `bytes` takes it on this device, and the launch (wal_pipe_kernel
-// alone: its count granules are the stream's, left zeroed by each launch).
-size_t wal_pipe_ws_bytes(uint64_t bytes, uint64_t cap);
-bool wal_pipe_applies(const DevCtx &c, uint64_t bytes);
-int launch_wal_pipe(DevCtx &c, const uint8_t *d_log, uint64_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc,
-                    uint32_t *d_info, uint64_t cap, uint64_t *d_count, uint8_t *ws, hipStream_t s);
 // The persistent class kernel over a sorted list (classes.hip).
 void launch_classes(const DevCtx &c, bool seeded, const lvk::Params &P, const uint32_t *ws, hipStream_t s);
 // One group-size kernel over a batch, offsets or strided (blocks.hip).

@@ -50,10 +50,6 @@
     defined(LVK_PIPE_COPY_THREADS) || \
     defined(LVK_WALK_EXACT) || \
     defined(LVK_WAL_UNSORT) || \
-    defined(LVK_WAL_LOCAL) || \
-    defined(LVK_WAL_PIPE_TRACE) || \
-    defined(LVK_PIPE_AMIN) || \
-    defined(LVK_PIPE_B_SMALL_FIRST) || \
     defined(LVK_TABLE_EXACT) || \
     defined(LVK_FUSED_EXACT))
 #error "LVK_* kernel switches select untested code paths; only experiment variants (LVK_EXPERIMENT_BUILD, tools/build_variant.sh) may set them"
@@ -166,18 +162,6 @@
 #endif
 #ifndef LVK_HASH_WGS_PER_CU  // hash: persistent workgroups (4 waves) per CU
 #define LVK_HASH_WGS_PER_CU 8
-#endif
-#ifndef LVK_WAL_LOCAL  // WAL scan: one persistent launch, each workgroup frames, sorts and walks its own blocks
-#define LVK_WAL_LOCAL 1
-#endif
-#ifndef LVK_PIPE_B_SMALL_FIRST  // WAL one-launch scan: phase B walks classes 1, 0 before class 2
-#define LVK_PIPE_B_SMALL_FIRST 0
-#endif
-#ifndef LVK_PIPE_AMIN  // WAL one-launch scan: smallest first-record unit walked in phase A (> 2048: class 2)
-#define LVK_PIPE_AMIN 2049
-#endif
-#ifndef LVK_WAL_PIPE_TRACE  // timing only: wal_pipe_kernel writes s_memrealtime stamps per workgroup to its workspace
-#define LVK_WAL_PIPE_TRACE 0
 #endif
 #ifndef LVK_WAL_UNSORT  // WAL scan: CRCs stored by sorted position, then written in log order (wal_unsort)
 #define LVK_WAL_UNSORT 1

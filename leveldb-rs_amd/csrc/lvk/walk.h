@@ -306,9 +306,8 @@ __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint3
 // is false when every group of the wave ends at lane 15 (e.g. aligned table
 // blocks): no early lanes, no rotation.
 // PLAIN: W1 / W2 from the plain combine tables 4 / 5 (Shift_256 / Shift_512)
-// instead of region B's Latin copies -- for a kernel that keeps region B's
-// 64 KiB of LDS for itself (wal_pipe_kernel; round 1 measured the plain
-// merge neutral on the class kernel).
+// instead of region B's Latin copies (round 1 measured the plain merge
+// neutral on the class kernel).
 template <uint32_t NU, bool PLAIN = false>
 __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a3p, const Lut &L, const RGeo &q,
                                              uint32_t gl, uint32_t lane, bool rot) {

@@ -403,20 +403,7 @@ static WalWs wal_ws_layout(uint64_t bytes, uint64_t cap) {
     return w;
 }
 
-static thread_local int g_wal_path = 0;  // lv_wal_scan_set_path
-
-int lv_wal_scan_set_path(int path) {
-    if (path < 0 || path > 2) return set_err(LV_ERR_INVALID, "path must be 0, 1 or 2");
-    const int prev = g_wal_path;
-    g_wal_path = path;
-    return prev;
-}
-
-size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) {
-    // either path's layout fits (the one-launch scan's, wal_pipe.hip, or the
-    // five-launch one's below)
-    return std::max<size_t>(wal_ws_layout(bytes, cap).total, wal_pipe_ws_bytes(bytes, cap));
-}
+size_t lv_wal_scan_workspace_bytes(size_t bytes, size_t cap) { return wal_ws_layout(bytes, cap).total; }
 
 int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, uint32_t *d_crc, uint32_t *d_info,
                        size_t cap, uint64_t *d_count, void *d_workspace, size_t workspace_bytes, void *stream) {
@@ -439,19 +426,10 @@ int lv_wal_scan_device(const uint8_t *d_log, size_t bytes, uint64_t *d_hdr_off, 
         return LV_OK;
     }
     uint8_t *wb = static_cast<uint8_t *>(d_workspace);
-    const bool pipe = wal_pipe_applies(*c, bytes);
-    if (g_wal_path == 1 && !pipe) return set_err(LV_ERR_INVALID, "the one-launch scan does not apply to this log");
-    // The five-launch scan is the default: the one-launch scan (wal_pipe.hip;
-    // every workgroup frames, sorts and checksums its own blocks) measured
-    // 0.622 of 8 TB/s against its 0.632 on the same box (216 vs 212.5 us per
-    // 1.075 GB call, profiles/r05/wal_paths/): its per-workgroup rounds end
-    // ragged (9 % of wave time idle at the end) and the slowest workgroup sets
-    // the launch.  lv_wal_scan_set_path(1) selects it (tests run both).
-    if (pipe && g_wal_path == 1) {
-        if (int rc = launch_wal_pipe(*c, d_log, bytes, d_hdr_off, d_crc, d_info, cap, d_count, wb, s)) return rc;
-        g_kernel = "wal_pipe_kernel";
-        return check_launch();
-    }
+    // (Round 5 measured a one-launch scan beside this one -- every workgroup
+    // framing, sorting and checksumming its own blocks -- at 0.622 of 8 TB/s
+    // against 0.632: its per-workgroup rounds ended ragged and the slowest
+    // workgroup set the launch, profiles/r05/wal_paths/.  Round 6 removed it.)
     uint32_t *ws = reinterpret_cast<uint32_t *>(wb);
     uint32_t *M = reinterpret_cast<uint32_t *>(wb + lay.m);
     uint64_t *wgrec = reinterpret_cast<uint64_t *>(wb + lay.wgrec);
@@ -531,10 +509,6 @@ int lvgpu_internal::scan_host_range(const uint8_t *log, size_t bytes, uint64_t b
             (rc = hip_err(hipStreamSynchronize(s), "sync")))
             break;
         lvgpu_internal::count_d2h(8);  // counted once it has arrived, on every attempt
-        if (count == ~0ull) {  // the one-launch scan's workgroups could not all run: once more
-            rc = lvgpu_internal::set_error(LV_ERR_NO_DEVICE, "WAL scan: workgroups not co-resident");
-            continue;
-        }
         if (count > cap) {  // more records than the guess: once more at the exact count
             cap = count;
             continue;
@@ -642,18 +616,17 @@ int pipe_enqueue(PipeSlot &sl, const uint8_t *log, bool pinned) {
 }
 
 // Waits for the slot's scan (once more at the exact count if the guess was
-// short, or if its workgroups were not co-resident), then its arrays back.
+// short), then its arrays back.
 int pipe_finish(PipeSlot &sl, lvgpu_internal::ScanChunk *out) {
     for (int attempt = 0;; ++attempt) {
         if (int rc = hip_err(hipStreamSynchronize(sl.s), "sync")) return rc;
         lvgpu_internal::count_d2h(8);
         const uint64_t count = *sl.hcnt;
-        if ((count == ~0ull || count > sl.cap) && attempt < 2) {
-            if (count != ~0ull) sl.cap = count;
+        if (count > sl.cap && attempt < 1) {
+            sl.cap = count;
             if (int rc = pipe_scan(sl)) return rc;
             continue;
         }
-        if (count == ~0ull) return lvgpu_internal::set_error(LV_ERR_NO_DEVICE, "WAL scan: workgroups not co-resident");
         if (count > sl.cap) return lvgpu_internal::set_error(LV_ERR_INVALID, "WAL scan failed");
         out->off.resize(count);
         out->crc.resize(count);

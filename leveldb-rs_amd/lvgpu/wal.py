@@ -53,8 +53,6 @@ def _bind():
     L.lv_wal_reader_last_record_offset.argtypes = [vp]
     L.lv_wal_reader_free.restype = None
     L.lv_wal_reader_free.argtypes = [vp]
-    L.lv_wal_scan_set_path.restype = ctypes.c_int
-    L.lv_wal_scan_set_path.argtypes = [ctypes.c_int]
     L.lv_wal_scan_workspace_bytes.restype = sz
     L.lv_wal_scan_workspace_bytes.argtypes = [sz, sz]
     L.lv_wal_scan_device.restype = ctypes.c_int
@@ -166,15 +164,6 @@ def scan_device(log, cap: int, workspace=None, stream=None):
     if rc != 0:
         _err("lv_wal_scan_device")
     return hdr, crc, info, count
-
-
-def set_scan_path(path: int) -> int:
-    """Debug / test hook (lv_wal_scan_set_path): 0 auto, 1 the one-launch
-    scan, 2 the five-launch scan; returns the previous setting."""
-    rc = _bind().lv_wal_scan_set_path(path)
-    if rc < 0:
-        _err("lv_wal_scan_set_path")
-    return rc
 
 
 def scan_workspace_bytes(nbytes: int, cap: int) -> int:

@@ -146,14 +146,11 @@ def test_encode_then_scan_then_read(gpu):
 
 
 SORTED = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel"
-PIPE = "wal_pipe_kernel"
 
 
 def _check_scan_device(log, cap=None, shift=0):
     """shift: the log's offset from a 16-B boundary (the scan needs 8-B
-    alignment).  Both device paths (lv_wal_scan_set_path): the one-launch
-    scan (every workgroup frames, sorts and checksums its own blocks) and the
-    five-launch one (global length sort, the default)."""
+    alignment)."""
     import lvgpu
     import lvgpu.wal as LW
     import torch
@@ -161,24 +158,20 @@ def _check_scan_device(log, cap=None, shift=0):
     cap = len(o) if cap is None else cap
     t = torch.frombuffer(bytes(shift) + bytes(log) + b"\0", dtype=torch.uint8).to("cuda:0")[shift:shift + len(log)]
     assert len(log) == 0 or t.data_ptr() % 16 == shift
-    # twice per path: a fresh workspace, then one left dirty (0xff): the scan
-    # reads nothing of the workspace it did not write first
+    # twice: a fresh workspace, then one left dirty (0xff): the scan reads
+    # nothing of the workspace it did not write first
     dirty = torch.full((LW.scan_workspace_bytes(len(log), cap),), 0xff, dtype=torch.uint8, device="cuda:0")
-    try:
-        for path, kern in ((1, PIPE), (2, SORTED + ("+wal_unsort" if cap else ""))):
-            LW.set_scan_path(path)
-            for ws in (None, dirty):
-                hdr, crc, info, count = LW.scan_device(t, cap, workspace=ws)
-                torch.cuda.synchronize()
-                assert lvgpu.last_kernel() == kern or len(log) == 0, (path, lvgpu.last_kernel())
-                n = int(count.item())
-                assert n == len(o), (path, n, len(o))
-                if n <= cap:
-                    assert hdr[:n].cpu().numpy().tolist() == o, path
-                    assert info[:n].cpu().numpy().view(np.uint32).tolist() == i, path
-                    assert crc[:n].cpu().numpy().view(np.uint32).tolist() == c, path
-    finally:
-        LW.set_scan_path(0)
+    kern = SORTED + ("+wal_unsort" if cap else "")
+    for ws in (None, dirty):
+        hdr, crc, info, count = LW.scan_device(t, cap, workspace=ws)
+        torch.cuda.synchronize()
+        assert lvgpu.last_kernel() == kern or len(log) == 0, lvgpu.last_kernel()
+        n = int(count.item())
+        assert n == len(o), (n, len(o))
+        if n <= cap:
+            assert hdr[:n].cpu().numpy().tolist() == o
+            assert info[:n].cpu().numpy().view(np.uint32).tolist() == i
+            assert crc[:n].cpu().numpy().view(np.uint32).tolist() == c
 
 
 @pytest.mark.parametrize("shift", [0, 8])
@@ -244,8 +237,7 @@ def test_scan_device_capacity(gpu):
 
 
 def test_scan_device_large_logs(gpu):
-    """Both device paths on logs of a block per CU and more (every workgroup
-    of the one-launch scan owns blocks): bench-like mixed records,
+    """The device scan on logs of a block per CU and more: bench-like mixed records,
     corruption, truncation, a zero tail, every block's first record a
     fragment, first records around the phase-A threshold (2,048 / 2,049-B
     units) followed by > 64 tiny records, too small a capacity, an 8-B-aligned

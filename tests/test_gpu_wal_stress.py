@@ -1,5 +1,5 @@
-"""Randomised parity sweep of the device WAL scan (lv_wal_scan_device, both
-paths: the five-launch default and the one-launch scan) against the oracle's
+"""Randomised parity sweep of the device WAL scan (lv_wal_scan_device)
+against the oracle's
 framing of log_reader.rs:271-331 (oracle.scan_log).  Each trial draws a log
 from one generator: 1-3,000 records of log-uniform sizes up to 2^8-2^16
 bytes (fragmented by the oracle Writer, log_writer.rs:67-80) after a random
@@ -20,7 +20,6 @@ pytestmark = pytest.mark.gpu
 B, H = W.BLOCK_SIZE, W.HEADER_SIZE
 TRIALS = int(os.environ.get("LVGPU_WAL_STRESS_TRIALS", "24"))
 SORTED = "wal_hist+sort_scan+wal_scatter+crc32c_classes_kernel"
-PIPE = "wal_pipe_kernel"
 
 
 def _log(rng):
@@ -68,17 +67,13 @@ def test_wal_scan_device_random(gpu, trial):
     cap = [n, n + int(rng.integers(1, 100)), max(n - 1, 0)][int(rng.integers(0, 3))]
     shift = int(rng.choice([0, 8]))
     t = torch.frombuffer(bytearray(bytes(shift) + log + b"\0"), dtype=torch.uint8).to(gpu)[shift:shift + len(log)]
-    try:
-        for path, kern in ((1, PIPE), (2, SORTED + ("+wal_unsort" if cap else ""))):
-            LW.set_scan_path(path)
-            hdr, crc, info, count = LW.scan_device(t, cap)
-            torch.cuda.synchronize()
-            assert lvgpu.last_kernel() == kern or len(log) == 0, (trial, path, lvgpu.last_kernel())
-            got = int(count.item())
-            assert got == n, (trial, path, got, n)
-            if n <= cap:
-                assert hdr[:n].cpu().numpy().tolist() == o, (trial, path)
-                assert info[:n].cpu().numpy().view(np.uint32).tolist() == i, (trial, path)
-                assert crc[:n].cpu().numpy().view(np.uint32).tolist() == c, (trial, path)
-    finally:
-        LW.set_scan_path(0)
+    kern = SORTED + ("+wal_unsort" if cap else "")
+    hdr, crc, info, count = LW.scan_device(t, cap)
+    torch.cuda.synchronize()
+    assert lvgpu.last_kernel() == kern or len(log) == 0, (trial, lvgpu.last_kernel())
+    got = int(count.item())
+    assert got == n, (trial, got, n)
+    if n <= cap:
+        assert hdr[:n].cpu().numpy().tolist() == o, trial
+        assert info[:n].cpu().numpy().view(np.uint32).tolist() == i, trial
+        assert crc[:n].cpu().numpy().view(np.uint32).tolist() == c, trial
