@@ -195,6 +195,17 @@ const char *lv_crc32c_last_kernel(void);
  * buffers and that cached host paths stop allocating.  0 or LV_ERR_INVALID. */
 int lv_device_counters(int device, uint64_t *out, size_t n);
 
+/* ---- page-locked host memory for callers' file buffers ------------------- */
+
+/* Page-locked (pinned) host memory: a caller that reads a log or table file
+ * into a buffer from lv_host_alloc hands the host entry points input the GPU
+ * reads by DMA directly -- no staging copy on the CPU (lv_wal_scan_host*,
+ * lv_crc32c_batch_host, lv_sst_verify_blocks_host detect pinned input).
+ * NULL on failure (lv_last_error).  Free with lv_host_free. */
+void *lv_host_alloc(size_t bytes);
+/* Frees lv_host_alloc memory (NULL is a no-op): 0 or an error code. */
+int lv_host_free(void *p);
+
 /* ---- synthetic data (bench / tests) ------------------------------------- */
 
 /* d_dst[k] = byte ((begin+k) & 7) of splitmix64(seed ^ ((begin+k) >> 3)) for

@@ -349,6 +349,24 @@ int lv_device_counters(int device, uint64_t *out, size_t n) {
     return LV_OK;
 }
 
+void *lv_host_alloc(size_t bytes) {
+    g_err.clear();
+    void *p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        set_err(static_cast<int>(e), std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+int lv_host_free(void *p) {
+    g_err.clear();
+    if (!p) return LV_OK;
+    LV_HIP(hipHostFree(p));
+    return LV_OK;
+}
+
 int lv_crc32c_batch_check(void *stream, uint32_t *violations) {
     g_err.clear();
     return check_hints(static_cast<hipStream_t>(stream), violations);

@@ -32,6 +32,7 @@
     defined(LVK_SEAL_FLUSH) || \
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
+    defined(LVK_SST_RUN) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_CLASS3_FIRST) || \
     defined(LVK_SMALL_ADAPT) || \
@@ -117,6 +118,9 @@
 #endif
 #ifndef LVK_SEAL_ROWS  // the seal's rows per batch: LVK_SST_ROWS, or 4 on the G = 16 image
 #define LVK_SEAL_ROWS LVK_SST_ROWS
+#endif
+#ifndef LVK_SST_RUN  // table walk: consecutive blocks per group (file-order runs; 1 = one block per round)
+#define LVK_SST_RUN 4
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

@@ -32,6 +32,22 @@ __device__ __forceinline__ bool sst_in_range(uint64_t o, uint64_t sz, uint64_t f
     return sz < 0xffffffffull && o <= file_bytes && sz <= file_bytes - o && file_bytes - o - sz >= 5u;
 }
 
+// File-order runs (round 6): a unit's first 256-B row is
+// the previous unit's last one (blocks follow each other in the file, 4-5 B
+// of trailer apart), and with one unit per group per round the two reads of
+// that line came from different waves ~17 rows apart -- two HBM fetches
+// (FETCH 1.061x the algorithmic bytes).  Now each group walks kSstRun
+// consecutive blocks in successive rounds: a wave round rho = R k + i gives
+// group g block R 4k + g k + i, so the edge line it needs first was loaded by
+// the same group one batch earlier (an L2 hit), and only 1 of k edges is
+// fetched twice.  k = 1 is the old order.
+constexpr uint32_t kSstRun = LVK_SST_RUN;
+
+__device__ __forceinline__ uint64_t sst_unit(uint64_t e) {  // e = rho * 4 + group
+    const uint64_t rho = e >> 2, g = e & 3u;
+    return (rho / kSstRun) * (4u * kSstRun) + g * kSstRun + rho % kSstRun;
+}
+
 template <bool SEAL, bool CRCOUT = false>
 struct TableUnits {
     const uint2 *handles;  // {offset, size} u64 pairs per block
@@ -39,6 +55,7 @@ struct TableUnits {
     uint32_t *status;      // verify: LV_SST_BLOCK_* per block
     uint32_t *crc_out;     // verify: optional crc32c(contents || type)
     uint64_t file_bytes;
+    uint64_t nblocks;      // the blocks (P.n: the run-padded entry count)
     // seal: 64 slots of {block, masked crc} (16 rounds of 4 blocks per flush;
     // the trailer stores are partial-line writes, and fewer, larger bursts of
     // them measured faster); verify: 64 slots of {block, status}, or with
@@ -56,8 +73,9 @@ struct TableUnits {
     static constexpr uint32_t kExact = SEAL ? 0u : LVK_TABLE_EXACT;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
-        const bool valid = e < P.n;
-        const uint64_t ec = valid ? e : P.n - 1;
+        const uint64_t u = sst_unit(e);
+        const bool valid = u < nblocks;
+        const uint64_t ec = valid ? u : nblocks - 1;
         const uint2 ho = handles[2 * ec], hs = handles[2 * ec + 1];  // u64 pairs: 8-B alignment is enough
         const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
         const bool ok = sst_in_range(o, sz, file_bytes);
@@ -159,13 +177,23 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
     const uint32_t lane = threadIdx.x & 63u;
     const Lut L = make_lut(lane);
     const uint64_t grid = gridDim.x;
-    auto pool = [&]() -> uint64_t {
+    // a wave claims kSstRun rounds at a time (its groups' runs of blocks)
+    auto claim = [&]() -> uint64_t {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
-        return blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0));
+        return (blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0))) * kSstRun;
     };
-    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(pool), SEAL ? kSealRows : kSstRows>(P, src, lane, L, pool(),
-                                                                                          pool);
+    uint64_t r0 = claim();
+    uint32_t i = 0;
+    auto next = [&]() -> uint64_t {
+        if (++i == kSstRun) {
+            i = 0;
+            r0 = claim();
+        }
+        return r0 + i;
+    };
+    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(next), SEAL ? kSealRows : kSstRows>(P, src, lane, L, r0,
+                                                                                          next);
 }
 
 }  // namespace lvk
@@ -179,23 +207,26 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     if (int rc = current_ctx(&c)) return rc;
     lvk::Params P{};
     P.base = reinterpret_cast<uint64_t>(d_file);
-    P.n = n;
+    constexpr uint64_t kRunUnits = 4ull * lvk::kSstRun;  // blocks per wave claim
+    const uint64_t claims = (n + kRunUnits - 1) / kRunUnits;
+    P.n = claims * kRunUnits;  // entries of the walk; those past the last block are empty lanes
     P.flags = 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, (n + 3) / 4))), block(lvk::kThreads);
+    const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, claims))), block(lvk::kThreads);
     if (seal) {
-        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes};
+        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes, n};
         g_kernel = "sst_blocks_kernel<seal>";
         // (4 rows per batch: Shift_1024 is the G = 16 image's own row shift)
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P,
                            c->image[lvk::kSealRows == 4 ? 2 : kTableImage], u);
     } else if (d_crc) {
-        lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes};
+        lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes,
+                                        n};
         g_kernel = "sst_blocks_kernel<verify,crc>";
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, true>), grid, block, 0, s, P, c->image[kTableImage], u);
     } else {
         lvk::TableUnits<false, false> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, nullptr,
-                                        file_bytes};
+                                        file_bytes, n};
         g_kernel = "sst_blocks_kernel<verify>";
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<false, false>), grid, block, 0, s, P, c->image[kTableImage], u);
     }

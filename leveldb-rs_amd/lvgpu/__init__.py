@@ -120,6 +120,10 @@ def lib() -> ctypes.CDLL:
     L.lv_device_counters.argtypes = [ctypes.c_int, vp, sz]
     L.lv_fill_splitmix.restype = ctypes.c_int
     L.lv_fill_splitmix.argtypes = [vp, u64, u64, u64, vp]
+    L.lv_host_alloc.restype = vp
+    L.lv_host_alloc.argtypes = [sz]
+    L.lv_host_free.restype = ctypes.c_int
+    L.lv_host_free.argtypes = [vp]
     _lib = L
     return L
 
@@ -362,6 +366,22 @@ def batch_multi(arena: bytes, off, length, seed=None, masked=False, ngpu: int = 
     else:
         _check(lib().lv_crc32c_batch_multi(*args, 1 if ngpu is None else ngpu))
     return out
+
+
+def host_alloc(nbytes: int):
+    """A page-locked host buffer (lv_host_alloc) as a numpy uint8 array, freed
+    (lv_host_free) when the array is released: read a log or table file into
+    it and the host entry points DMA it without a staging copy."""
+    import weakref
+
+    import numpy as np
+    L = lib()
+    p = L.lv_host_alloc(nbytes)
+    if not p:
+        raise LvError(f"lv_host_alloc({nbytes}): {L.lv_last_error().decode()}")
+    buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(p)
+    weakref.finalize(buf, L.lv_host_free, p)
+    return np.ctypeslib.as_array(buf)[:nbytes]
 
 
 def fill_splitmix(dst, begin: int, seed: int, stream=None):

@@ -32,9 +32,15 @@ def test_hash_rooflines_pick_the_binding_bound():
     assert roof is hbm and valu is None and roof["bound"] == "hbm"
     assert abs(hbm["frac"] - key / (ms * 1e-3) / 8e12) < 1e-3
     assert abs(hbm["frac_all_bytes"] - moved / (ms * 1e-3) / 8e12) < 1e-3
-    # a VALU count far below the issue rate: HBM (all bytes) binds
+    # a VALU count far below the issue rate: HBM binds
     roof, hbm, valu = b.hash_rooflines(key, ms, 1e6, moved)
-    assert roof is hbm and valu["frac"] < hbm["frac_all_bytes"]
+    assert roof is hbm and valu["frac"] < hbm["frac"]
+    # the rule compares the reported numbers: a VALU frac between
+    # the key-byte and all-byte HBM fracs makes VALU the roofline
+    peak = b.VALU_SIMDS * b.VALU_CLOCK_HZ / b.VALU_CYCLES * ms * 1e-3
+    mid = (hbm["frac"] + hbm["frac_all_bytes"]) / 2
+    roof, hbm, valu = b.hash_rooflines(key, ms, mid * peak, moved)
+    assert roof is valu and hbm["frac"] < valu["frac"] < hbm["frac_all_bytes"]
     # one at the issue peak: VALU binds
     peak = b.VALU_SIMDS * b.VALU_CLOCK_HZ / b.VALU_CYCLES * ms * 1e-3
     roof, hbm, valu = b.hash_rooflines(key, ms, peak, moved)

@@ -130,6 +130,32 @@ def test_pipelined_scan_reader_over_chunks(gpu):
     assert got[0] == got[1] and got[0][1] > 0
 
 
+def test_pipelined_scan_worker_error_surfaces(gpu):
+    """a pipelined scan whose worker fails (here: a device ordinal
+    past the last GPU) reports the worker's error from lv_wal_scan_wait and
+    from the accessors (count 0), and a Reader over it fails with that error
+    instead of returning end of input."""
+    import torch
+
+    import lvgpu
+    import lvgpu.wal as LW
+    log = LW.encode([bytes([i % 251]) * (100 + i) for i in range(50)])
+    bad_dev = torch.cuda.device_count() + 3
+    s = LW.Scan.host_pipelined(log, device=bad_dev)
+    with pytest.raises(lvgpu.LvError) as e:
+        s.wait()
+    assert "WAL scan" in str(e.value)
+    assert LW._bind().lv_wal_scan_count(s._h) == 0
+    s2 = LW.Scan.host_pipelined(log, device=bad_dev)
+    rd = LW.Reader(log, s2, W.ReportCollector())
+    with pytest.raises(lvgpu.LvError) as e2:
+        rd.read_record()
+    assert "WAL scan" in str(e2.value)
+    # the library still works on a valid device afterwards
+    r = LW.Reader(log, LW.Scan.host_pipelined(log))
+    assert r.read_record() == bytes([0]) * 100
+
+
 def test_encode_then_scan_then_read(gpu):
     """Round trip at scale: GPU encode -> GPU scan -> host reader returns the
     records, with no reports."""
