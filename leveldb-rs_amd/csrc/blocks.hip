@@ -156,9 +156,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_blocks_kernel(Params P, uint3
         const uint32_t nw = (1u << P.pshift) * 32u;
         for (uint32_t i = threadIdx.x; i < nw; i += kThreads) fm[(i >> 5) * 33 + (i & 31u)] = P.mats[i];
     }
-#if !LVK_EXP_NOSTAGE
     stage_tables(image);
-#endif
     uint32_t lbad = lq[0] | lq[1] | lq[2] | lq[3];
     if (lcheck)
         for (uint64_t b = lb0 + 4 * lstr; b < nblk; b += lstr) lbad |= P.len[b] ^ P.hlen;

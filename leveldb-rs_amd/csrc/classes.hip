@@ -17,7 +17,7 @@ namespace lvk {
 // per CU as on 16 (it is bound by per-buffer VALU work and random line
 // reads, not latency), and classes 2+3 run FASTER on 12 waves than on 16.
 constexpr uint32_t kSmallWaves = LVK_SMALL_WAVES;
-constexpr uint32_t kSmallRounds = LVK_SMALL_ROUNDS;  // small-class rounds per wave (LVK_SMALL_ADAPT)
+constexpr uint32_t kSmallRounds = LVK_SMALL_ROUNDS;  // small-class rounds per wave
 
 // The offsets API in ONE persistent launch over the length-sorted list, on
 // the G = 16 table image (staged once).  Waves [0, kSmallWaves) of every
@@ -70,19 +70,13 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
     // Round 4, with the CRCs stored by sorted position: kSmallRounds 52
     // (fewer small-class waves) over 26, C2 0.770 -> 0.773, C4 0.755 ->
     // 0.761, WAL unchanged; 13 and 104 lower (profiles/r04/small_rounds*/).
-#if LVK_SMALL_ALL
     uint32_t nsmall = n23 ? kSmallWaves : kWaves;
-#else
-    uint32_t nsmall = kSmallWaves;
-#endif
-#if LVK_SMALL_ADAPT
     if (n23) {
         const uint64_t rounds = (cls(4) + 63ull) / 64u + (cls(5) + 15ull) / 16u;
         const uint64_t per = static_cast<uint64_t>(kSmallRounds) * gridDim.x;
         const uint64_t ns = (rounds + per - 1) / per;
         nsmall = static_cast<uint32_t>(ns < 1 ? 1 : (ns > kSmallWaves ? kSmallWaves : ns));
     }
-#endif
     if (wave < nsmall) {
         const uint64_t sw = blockIdx.x * nsmall + wave, nsw = grid * nsmall;
         uint64_t k = 0;
@@ -94,7 +88,6 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         if (cls(5)) sorted_stream<4>(sub_list(P, cls(1), cls(5)), SortedList<SEEDED>{ident}, lane, L, sw, stride);
     }
     if (n23) {
-#if LVK_CLASS_STAGGER
         // A list of mostly long-buffer pieces (>= 3/4 of the entries), with
         // >= 64 KiB per wave, is the blocks kernel's long-block regime: waves
         // that start together stream their pieces in lockstep, which reads
@@ -103,7 +96,6 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         const uint64_t bytes = hostid ? 0u : (static_cast<uint64_t>(ws[kWsBytes + 1]) << 32) | ws[kWsBytes];
         if (4ull * np >= 3ull * (n23 + np) && bytes >= (64ull << 10) * grid * kWaves)
             for (uint32_t k = 0; k < wave * LVK_STAGGER; ++k) __builtin_amdgcn_s_sleep(32);
-#endif
         // Walk order of classes 2 + 3 (each sorted longest first): with both
         // present, the full rounds are rotated to start at class 3's first
         // round, so the pool ends on class 2's shortest buffers instead of a
@@ -111,7 +103,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_classes_kernel(Params P, cons
         // rotation is on the wave-uniform round index (scalar registers: an
         // entry remap in SortedList::load cost the class kernel 5 VGPRs of
         // spills and C3 via offsets 5 %).
-        const uint64_t rrot = (LVK_CLASS3_FIRST && cls(6) && cls(7)) ? n23 / 4u : 0u;  // K = 4 entries per round
+        const uint64_t rrot = (cls(6) && cls(7)) ? n23 / 4u : 0u;  // K = 4 entries per round
         const uint64_t s3 = cls(6) / 4u;
         auto pool = [&]() -> uint64_t {
             uint32_t k = 0;
@@ -382,11 +374,10 @@ template <bool SEEDED>
 struct FusedUnits {
     static constexpr uint32_t kFlush = 16;
     static constexpr bool kAlMid = true;
-    static constexpr bool kPlainMerge = false;
-    static constexpr bool kOneRound = LVK_FUSED_ONE_ROUND;  // sorted_stream: a one-round wave loads all batches at once
+    static constexpr bool kOneRound = true;  // sorted_stream: a one-round wave loads all batches at once
     // wait-count modes 1 / 2 (walk.h) measured 0.7-1.3 / 0.5-0.9 us slower on
     // the few-long-buffer calls (profiles/r04/new_ab/, mode2_ab/): masked
-    static constexpr uint32_t kExact = LVK_FUSED_EXACT;
+    static constexpr uint32_t kExact = 0;
     uint32_t nbuf;  // buffers (<= kFusedMax); P.n = units
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const bool valid = e < P.n;
@@ -495,7 +486,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fused_small_kernel(Params P, 
     // [b S, (b + 1) S), S = whole rounds, as many rounds per workgroup as the
     // round-robin pool gave it; a split buffer whose pieces all fall in one
     // workgroup's units is joined there, after the walk (no long record).
-    const bool onepass = LVK_FUSED_LOCAL_JOIN && nunits <= 4ull * kWaves * grid;
+    const bool onepass = nunits <= 4ull * kWaves * grid;
     const uint32_t S = onepass ? 4u * static_cast<uint32_t>((nunits + 4ull * grid - 1) / (4ull * grid)) : 1u;
     uint32_t pb = ceil_log2(total / 16384u);  // the batch's piece length (split_rule), for the join
     pb = pb > kFusedPieceLog2 ? pb : kFusedPieceLog2;
@@ -639,7 +630,7 @@ bool hint_needs_join(const lv_batch_hint &h, uint64_t n, uint32_t cus) {
     // no sort) goes without it
     if (n > lvk::kFusedMax) return !(h.uniform && nosplit);
     if (nosplit) return false;
-    if (!h.uniform || !LVK_FUSED_LOCAL_JOIN) return true;
+    if (!h.uniform) return true;
     const uint32_t m = host_split_rule(h.max_len, h.total_bytes, &p);
     const uint64_t nunits = n * m;
     const uint64_t grid = cus;

@@ -25,7 +25,7 @@
 // mask and a `more` branch, so the compiler could not count the loads in
 // flight and waited vmcnt(0) -- for the prefetch just issued -- at the top of
 // every set.  Every lane now loads its (clamped) metadata and the validity
-// select waits until the set is hashed (LVK_HASH_PREFETCH_EXACT): offsets
+// select waits until the set is hashed: offsets
 // API unchanged (0.515 vs 0.516), packed u32 keys 0.504 -> 0.542
 // (profiles/r04/hash_exact/).  A two-deep kernel with every load exact --
 // the next set's span in registers while this set hashes, 80 VGPRs, 6
@@ -36,7 +36,7 @@
 // its two dwords re-read after it -- and reading the 17-dword LDS window
 // unmasked: offsets 0.518 -> 0.53, packed u32 0.549 -> 0.575
 // (profiles/r04/hash_tail/, hash_ldsall/).  The multiply is not the bound:
-// a full-rate 24-bit one (LVK_EXP_HASH_MUL24, timing only) ran the same
+// a full-rate 24-bit one (a timing-only build, wrong hashes) ran the same
 // (profiles/r04/hash_mul/).
 // The grid is persistent (8 workgroups per CU): a wave walks sets of 64 keys,
 // requests the next set's metadata ahead, and stores each result one set
@@ -74,10 +74,7 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ uint32_t mix(uint32_t h, uint32_t w) {  // hash.rs:31-35
     h += w;
-    if constexpr (LVK_EXP_HASH_MUL24)  // timing only (wrong hashes): a full-rate 24-bit multiply
-        h = (h & 0xffffffu) * (kM & 0xffffffu);
-    else
-        h *= kM;
+    h *= kM;
     return h ^ (h >> 16);
 }
 
@@ -181,7 +178,6 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
     // stages the granules spanning its 64 keys through LDS with coalesced
     // 16-B loads, instead of 64 lanes gathering byte-aligned keys.  Waves
     // whose keys span more than kSpanBytes read keys straight from memory.
-#if LVK_HASH_SPAN_READLANE
     // Candidate span from the first and the last lane of the wave (keys are
     // usually packed in order); the wave stages it only if every key lies
     // inside it.  Two lane reads and one ballot instead of two 64-bit
@@ -192,12 +188,6 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
     const uint64_t lo16 = lo & ~15ull;
     const bool inside = !L || (o >= lo && o + L <= hi);
     const bool staged = act && hi > lo && hi - lo16 <= kSpanBytes && __all(inside);  // wave-uniform
-#else
-    const uint64_t lo = wave_min_u64(L ? o : ~0ull);
-    const uint64_t hi = wave_max_u64(L ? o + L : 0ull);
-    const uint64_t lo16 = lo & ~15ull;
-    const bool staged = lo != ~0ull && hi - lo16 <= kSpanBytes;  // wave-uniform
-#endif
     if (staged) {
         const uint32_t nch = static_cast<uint32_t>((hi - lo16 + 15) >> 4);
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -238,7 +228,7 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
             // bytes of w[j + 1] below 4 nw + bs, and the tail word is
             // re-read or masked to its diff bytes)
 #pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = (LVK_HASH_TAIL_READ && LVK_HASH_LDS_ALL) || j < ndw ? sd[j] : 0u;
+            for (uint32_t j = 0; j < kFastDw; ++j) w[j] = sd[j];
         } else {
             const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
             w[0] = d[0];
@@ -260,35 +250,24 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
         w[kFastDw] = 0u;
         uint32_t tw = 0;
         const uint32_t diff = L - 4 * nw;          // hash.rs:38-48
-        if constexpr (LVK_HASH_TAIL_READ) {
-            // The loop is VALU-bound (wave64: 4 cycles an op): capturing the
-            // tail word in it cost a compare and a select per word, so the
-            // tail's two dwords are read again after it (LDS or L1)
+        // The loop is VALU-bound (wave64: 4 cycles an op): capturing the
+        // tail word in it cost a compare and a select per word, so the
+        // tail's two dwords are read again after it (LDS or L1)
 #pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j)
-                if (j < nw) h = mix(h, funnel(w[j + 1], w[j], bs));
-            if (diff) {  // then nw < ndw
-                uint32_t t0, t1;
-                if (staged) {
-                    const uint32_t *sd = span + ((o - bs - lo16) >> 2);
-                    t0 = sd[nw];
-                    t1 = nw + 1 < ndw ? sd[nw + 1] : 0u;
-                } else {
-                    const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
-                    t0 = d[nw];
-                    t1 = nw + 1 < ndw ? d[nw + 1] : 0u;
-                }
-                tw = funnel(t1, t0, bs);
+        for (uint32_t j = 0; j < kFastDw; ++j)
+            if (j < nw) h = mix(h, funnel(w[j + 1], w[j], bs));
+        if (diff) {  // then nw < ndw
+            uint32_t t0, t1;
+            if (staged) {
+                const uint32_t *sd = span + ((o - bs - lo16) >> 2);
+                t0 = sd[nw];
+                t1 = nw + 1 < ndw ? sd[nw + 1] : 0u;
+            } else {
+                const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
+                t0 = d[nw];
+                t1 = nw + 1 < ndw ? d[nw + 1] : 0u;
             }
-        } else {
-#pragma unroll
-            for (uint32_t j = 0; j < kFastDw; ++j) {
-                const uint32_t wj = funnel(w[j + 1], w[j], bs);
-                if (j < nw)
-                    h = mix(h, wj);
-                else if (j == nw)
-                    tw = wj;
-            }
+            tw = funnel(t1, t0, bs);
         }
         if (diff) {
             if (diff >= 3) h += ((tw >> 16) & 0xffu) << 16;
@@ -319,22 +298,17 @@ struct OffsetsMeta {
     __device__ __forceinline__ MetaRaw load(uint64_t i, uint32_t n, uint32_t) const {
         const bool v = i < n;
         MetaRaw r;
-        if constexpr (LVK_HASH_PREFETCH_EXACT) {  // every lane loads (clamped; get() zeroes lanes past n)
-            const uint64_t ic = v ? i : n - 1u;
-            r.o = off[ic];
-            r.L = len[ic];
-            r.sd = seed ? seed[ic] : 0u;  // (wave-uniform)
-        } else {
-            r.o = v ? off[i] : 0u;
-            r.L = v ? len[i] : 0u;
-            r.sd = v && seed ? seed[i] : 0u;
-        }
+        // every lane loads (clamped; get() zeroes lanes past n)
+        const uint64_t ic = v ? i : n - 1u;
+        r.o = off[ic];
+        r.L = len[ic];
+        r.sd = seed ? seed[ic] : 0u;  // (wave-uniform)
         r.x = 0;
         return r;
     }
     __device__ __forceinline__ void get(const MetaRaw &r, uint64_t i, uint32_t n, uint32_t, uint64_t &o, uint32_t &L,
                                         uint32_t &sd) const {
-        const bool v = !LVK_HASH_PREFETCH_EXACT || i < n;
+        const bool v = i < n;
         o = v ? r.o : 0u;
         L = v ? r.L : 0u;
         sd = v ? r.sd : 0u;
@@ -353,16 +327,11 @@ struct PackedMeta {
     __device__ __forceinline__ MetaRaw load(uint64_t i, uint32_t n, uint32_t lane) const {
         const bool v = i < n;
         MetaRaw r;
-        if constexpr (LVK_HASH_PREFETCH_EXACT) {  // every lane loads (clamped; get() zeroes lanes past n)
-            const uint64_t ic = v ? i : n - 1u;
-            r.o = static_cast<uint64_t>(b[ic]);
-            r.x = static_cast<uint64_t>(b[ic + 1]);  // used by lane 63 and the last key
-            r.sd = seed ? seed[ic] : 0u;
-        } else {
-            r.o = v ? static_cast<uint64_t>(b[i]) : 0u;
-            r.x = v && (lane == 63u || i + 1 >= n) ? static_cast<uint64_t>(b[i + 1]) : 0u;
-            r.sd = v && seed ? seed[i] : 0u;
-        }
+        // every lane loads (clamped; get() zeroes lanes past n)
+        const uint64_t ic = v ? i : n - 1u;
+        r.o = static_cast<uint64_t>(b[ic]);
+        r.x = static_cast<uint64_t>(b[ic + 1]);  // used by lane 63 and the last key
+        r.sd = seed ? seed[ic] : 0u;
         r.L = 0;
         return r;
     }
@@ -401,7 +370,7 @@ __global__ void __launch_bounds__(256) hash_kernel(const uint8_t *__restrict__ b
     for (;;) {
         const uint64_t nxt = set + W;
         const bool more = nxt * 64u < n;  // wave-uniform
-        if (LVK_HASH_PREFETCH_EXACT || more) nx = meta.load(nxt * 64u + lane, n, lane);  // (clamped)
+        nx = meta.load(nxt * 64u + lane, n, lane);  // every lane, every set (clamped): exact waits
         const uint64_t i = set * 64u + lane;
         const bool valid = i < n;
         uint64_t o;

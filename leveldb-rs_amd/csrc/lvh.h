@@ -42,7 +42,7 @@ constexpr int kTableImage = 4;
 // and fused kernels): region A's row shift is Shift_{256 *
 // kAlRows} -- the G = 16 image's Shift_1024, or the table image's Shift_768
 // (kSstRows = 3) for 3 rows per batch.
-constexpr uint32_t kAlRowsH = LVK_ALIGNED_ROWS ? LVK_AL_ROWS : lvk::U;  // = lvk::kAlRows (lvk/sort.h)
+constexpr uint32_t kAlRowsH = LVK_AL_ROWS;  // = lvk::kAlRows (lvk/sort.h)
 constexpr int kAlImage = kAlRowsH == 4 ? 2 : kTableImage;
 static_assert(kAlRowsH == 4 || kAlRowsH == lvk::kSstRows, "aligned rows: 4, or the table image's");
 constexpr int kImages = 5;

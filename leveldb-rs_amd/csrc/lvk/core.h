@@ -159,16 +159,6 @@ __device__ __forceinline__ uint32_t comb_shift(uint32_t a, int k) {
 // W4K < 0: W4 = the Latin half of region A (Shift_{64G} for the image's G);
 // W4K = k >= 0: W4 = plain combine table k (Shift_{16*2^k}) -- how groups of
 // G = 1 and 4 run on a G = 16 image (Shift_64 = k 2, Shift_256 = k 4).
-// Experiment switches (wrong CRCs; timing studies only, never built into
-// the product library, tools/build_variant.sh): LVK_EXP_NOSHIFT drops the
-// row-shift lookups, LVK_EXP_NOFOLD all lookups (the load structure alone),
-// LVK_EXP_NOSTAGE the blocks kernel's table staging.
-// The LVK_EXP_* switches compute WRONG CRCs: a build that sets one must say
-// so explicitly (tools/build_variant.sh passes LVK_EXPERIMENT_BUILD=1 and
-// names the library a variant), so they can never reach the product library.
-// Sorted-walk studies: LVK_EXP_NOTAIL skips the tail granule's fold,
-// LVK_EXP_NOFIX the head/end fix-ups of a round's rows, LVK_EXP_NOMERGE the
-// merge lookups (rows XORed) and the lane rotation.
 // NU rows per batch; W4OFF = LDS offset of the Latin row-shift table (the
 // image's W4 = Shift_{64G}, or region B's W2 = Shift_{32G} for NU = 2).
 // SKIP (FIRST batches only): the leading rows that hold no buffer byte for
@@ -178,11 +168,6 @@ template <bool FIRST, int W4K = -1, uint32_t NU = U, uint32_t W4OFF = kRegionA +
 __device__ __forceinline__ void fold_batch(const uint4 (&v)[NU], uint32_t (&A)[NU], const Lut &L) {
     static_assert(SKIP == 0 || FIRST, "only a first batch skips rows");
     static_assert(SKIP < NU, "at least one row");
-#if LVK_EXP_NOFOLD  // experiment only: no lookups at all (load-structure bound)
-#pragma unroll
-    for (uint32_t i = 0; i < NU; ++i) A[i] = (FIRST ? 0u : A[i]) ^ xor3(v[i].x, v[i].y, v[i].z) ^ v[i].w;
-    return;
-#endif
     uint32_t s[NU], w[NU], w3[NU];
 #pragma unroll
     for (uint32_t i = 0; i < NU; ++i) s[i] = v[i].x;
@@ -194,12 +179,6 @@ __device__ __forceinline__ void fold_batch(const uint4 (&v)[NU], uint32_t (&A)[N
 #pragma unroll
         for (uint32_t i = 0; i < NU; ++i) {
             w[i] = comb_shift(A[i], W4K);
-            w3[i] = 0u;
-        }
-    } else if constexpr (!FIRST && LVK_EXP_NOSHIFT) {  // experiment only: wrong CRCs
-#pragma unroll
-        for (uint32_t i = 0; i < NU; ++i) {
-            w[i] = A[i];
             w3[i] = 0u;
         }
     } else if constexpr (!FIRST) {

@@ -20,7 +20,7 @@ __device__ __forceinline__ uint32_t len_class(uint32_t len) {
 }
 
 // Rows per batch of the G = 16 classes' aligned-row walk (sorted_stream).
-constexpr uint32_t kAlRows = LVK_ALIGNED_ROWS ? LVK_AL_ROWS : U;
+constexpr uint32_t kAlRows = LVK_AL_ROWS;
 
 __device__ __forceinline__ uint32_t sort_key(uint32_t len) {
     const uint32_t c = len_class(len);

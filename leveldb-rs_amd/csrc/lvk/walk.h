@@ -68,7 +68,7 @@ __device__ __forceinline__ RGeo load_rgeo(const Params &P, uint64_t e) {
     q.seed = SEEDED ? P.sseed[ec] : 0u;
     const bool piece = P.nplain < P.n && (v.w & kPieceFlag) && v.w != 0xffffffffu;
     const uint32_t slot = P.tmp && !piece && v.w != 0xffffffffu ? static_cast<uint32_t>(ec) : v.w;
-    q.bid = valid ? (LVK_EXP_SORTEDOUT ? static_cast<uint32_t>(ec) : slot) : 0xffffffffu;
+    q.bid = valid ? slot : 0xffffffffu;
     q.aux = 0;
     return q;
 }
@@ -135,7 +135,7 @@ __device__ __forceinline__ void fix_rbatch(const RGeo &q, uint32_t nbw, uint32_t
 }
 
 // Granules outside a buffer load from this zero block (load_rbatch_al, and
-// with LVK_WALK_EXACT every lane's tail).
+// in the exact wait-count mode every lane's tail).
 static __device__ __attribute__((aligned(256))) uint4 g_zero_granules[16];  // zero-initialised
 
 // The granule after the last whole granule (k = (alow+len) & 15 bytes of it
@@ -305,26 +305,13 @@ __device__ __forceinline__ void fix_rbatch_al(const RGeo &q, uint32_t nbw, uint3
 // (In the depth-2 form W2(W1(h0)^h1) ^ (W1(h2)^h3).)  `rot` (wave-uniform)
 // is false when every group of the wave ends at lane 15 (e.g. aligned table
 // blocks): no early lanes, no rotation.
-// PLAIN: W1 / W2 from the plain combine tables 4 / 5 (Shift_256 / Shift_512)
-// instead of region B's Latin copies (round 1 measured the plain merge
-// neutral on the class kernel).
-template <uint32_t NU, bool PLAIN = false>
+template <uint32_t NU>
 __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a3p, const Lut &L, const RGeo &q,
                                              uint32_t gl, uint32_t lane, bool rot) {
     const AGeo g = al_geo(q);
     const bool early = static_cast<int32_t>(gl) > g.e;
     uint32_t X;
-    if constexpr (LVK_EXP_NOMERGE) {
-        X = early ? a3p : 0u;
-#pragma unroll
-        for (uint32_t i = 0; i < NU; ++i) X ^= A[i];
-        return X;
-    } else if constexpr (PLAIN) {
-        static_assert(NU == 4, "plain merge: four rows per batch");
-        const uint32_t x01 = comb_shift(early ? a3p : A[0], 4) ^ (early ? A[0] : A[1]);
-        const uint32_t x23 = comb_shift(early ? A[1] : A[2], 4) ^ (early ? A[2] : A[3]);
-        X = comb_shift(x01, 5) ^ x23;
-    } else if constexpr (NU == 4) {
+    if constexpr (NU == 4) {
         const uint32_t x01 = lookup4<kRegionB>(early ? a3p : A[0], L) ^ (early ? A[0] : A[1]);
         const uint32_t x23 = lookup4<kRegionB>(early ? A[1] : A[2], L) ^ (early ? A[2] : A[3]);
         X = lookup4<kRegionB + kHalf>(x01, L) ^ x23;
@@ -349,7 +336,7 @@ __device__ __forceinline__ uint32_t merge_al(const uint32_t (&A)[NU], uint32_t a
 template <int G, uint32_t NU>
 __device__ __forceinline__ uint32_t round_pad(const RGeo &q, uint32_t nbw) {
     uint32_t padg;
-    if constexpr (LVK_ALIGNED_ROWS && G == 16) {
+    if constexpr (G == 16) {
         const int32_t p = static_cast<int32_t>(NU * nbw) - al_geo(q).re - 1;
         padg = p <= 0 ? 0u : static_cast<uint32_t>(p);
     } else {  // end-aligned rows: row i is empty for every lane iff ng - G*NU*nbw + G*(i+1) - 1 < 0
@@ -385,7 +372,7 @@ __device__ __forceinline__ void fold_first(const uint4 (&v)[NU], uint32_t (&A)[N
 // xor and mask: the tail bytes, then the short-buffer seed.
 __device__ __forceinline__ uint32_t finish_raw(const RGeo &q, uint32_t X, const uint4 &tail, uint32_t gl,
                                                const Lut &L) {
-    if (!LVK_EXP_NOTAIL) X = fold_tail(X, tail, q, L);
+    X = fold_tail(X, tail, q, L);
     if (gl == 0 && q.len < 4) {  // R(s, D) = R(0, D) ^ Shift_|D|(s) for short buffers
         uint32_t s = ~q.seed;
         for (uint32_t i = 0; i < q.len; ++i) s = byte_step(s, 0u);
@@ -403,9 +390,8 @@ template <bool SEEDED>
 struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
-    static constexpr bool kPlainMerge = false;  // merge_al: region B's Latin tables
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
-    static constexpr uint32_t kExact = LVK_WALK_EXACT;  // sorted_stream: wait-count mode (below)
+    static constexpr uint32_t kExact = 0;  // sorted_stream: wait-count mode (below)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         if (!ident) return load_rgeo<SEEDED>(P, e);
@@ -435,7 +421,7 @@ struct SortedList {
         // piece slots (flagged in the entry) occur only in the pieces' sub-list (P.nplain < P.n)
         if (P.nplain < P.n && (bi & kPieceFlag))
             P.part[bi & ~kPieceFlag] = cv;
-        else if (!LVK_EXP_NOOUT)
+        else
             (P.tmp && !ident ? P.tmp : P.out)[bi] = cv;  // (an identity list is in buffer order already)
     }
 };
@@ -451,9 +437,9 @@ struct SortedList {
 // exec-masked tail load, the next round's loads under `more`) makes the
 // fold of a batch wait with vmcnt(0..3) -- also for the prefetch issued
 // just before it.  Src::kExact selects the load form: 0 = masked loads;
-// 1 = the same unconditional loads every step (tail and trailer re-read,
-// the next round's entries and first batch always, clamped); 2 =
-// unconditional loads within each path.  Exact waits (vmcnt(8..5) in the
+// 2 = unconditional loads within each path (the next round's entries and
+// first batch always, clamped).  (Mode 1, the same loads every step with the
+// tail and trailer re-read, was measured and removed.)  Exact waits (vmcnt(8..5) in the
 // fold) measured, against mode 0 on one box (profiles/r04/walk_modes/,
 // mode2_ab/): class kernel mode 1 / 2 -- C3 via offsets -2.5 / -3 %, C2 0,
 // C4 -0.6 %, WAL scan +0.6 / -0.3 % -- so it keeps mode 0 (16 waves per CU
@@ -464,11 +450,11 @@ struct SortedList {
 template <int G, class Src, class Next, uint32_t ALR = kAlRows>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {
-    constexpr bool AL = LVK_ALIGNED_ROWS && G == 16;  // 256-B-aligned rows (merge_al)
-    // exact wait counts (below): Src::kExact 0 = masked loads, 1 = the same
-    // unconditional loads every step (tail / trailer re-read), 2 =
-    // unconditional loads within each path only
-    constexpr bool EX = Src::kExact != 0, RELOAD = Src::kExact == 1;
+    constexpr bool AL = G == 16;  // 256-B-aligned rows (merge_al)
+    // exact wait counts (below): Src::kExact 0 = masked loads, 2 =
+    // unconditional loads within each path
+    static_assert(Src::kExact == 0 || Src::kExact == 2, "wait-count mode 0 or 2");
+    constexpr bool EX = Src::kExact != 0;
     constexpr uint32_t NU = AL ? ALR : U;              // rows per batch
     // Latin row shift Shift_{16 G NU}: region A's second half (the image's W4
     // for NU = 4; Shift_768 in the table image for NU = 3) or region B's W2
@@ -520,7 +506,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             tail = load_rtail<EX>(q, gl);
             tr = src.trailer(q, gl);
             auto fold_j = [&](uint4(&v)[NU], uint32_t jj) {
-                if (!LVK_EXP_NOFIX && jj <= jfix) fix_rbatch_al<NU>(q, nbw, jj, gl, v);
+                if (jj <= jfix) fix_rbatch_al<NU>(q, nbw, jj, gl, v);
                 if (jj + 1u == nbw) a3p = jj == 0 ? 0u : A[NU - 1];
                 if (jj == 0)
                     fold_first<W4K, NU, W4OFF>(v, A, L, pad);
@@ -531,7 +517,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             if (nbw > 1u) fold_j(v1, 1);
             if (nbw > 2u) fold_j(v2, 2);
             if (nbw > 3u) fold_j(v3, 3);
-            uint32_t X = merge_al<NU, Src::kPlainMerge>(A, a3p, L, q, gl, lane, rot);
+            uint32_t X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
             X = finish_raw(q, X, tail, gl, L);
             if (gl == 0) src.stage(P, wave, grp, q, X, tr);
             __builtin_amdgcn_wave_barrier();
@@ -544,10 +530,6 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         const bool lastj = j + 1 == nbw;
         const bool more = rhon < nr;
         if (!lastj) {
-            if constexpr (RELOAD) {  // the same loads as the last step's (see the knob)
-                tail = load_rtail<EX>(q, gl);
-                tr = src.trailer(q, gl);
-            }
             if constexpr (AL)
                 load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt, Src::kAlMid ? jfix : 0xffffffffu);
             else
@@ -566,7 +548,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             }
         }
         if constexpr (AL) {
-            if (!LVK_EXP_NOFIX && j <= jfix) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
+            if (j <= jfix) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
         } else if (j <= jfix) {
             fix_rbatch<G>(q, nbw, j, gl, cur);
         }
@@ -583,7 +565,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         }
         uint32_t X;
         if constexpr (AL)
-            X = merge_al<NU, Src::kPlainMerge>(A, a3p, L, q, gl, lane, rot);
+            X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
         else
             X = merge_group<G, W1K, W2K>(A, L);
         X = finish_raw(q, X, tail, gl, L);

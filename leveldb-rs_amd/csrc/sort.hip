@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint64_t *__r
     const bool ident_key = tk == static_cast<uint32_t>(n);  // this thread's key holds every buffer
     const uint32_t kc = t / kBuckets, knb = kBuckets - 1 - t % kBuckets;
     const bool ident_ok = ident_key && (kc <= 1 || (kc == 2 && (knb <= 16 || n >= 16384)));
-    const bool ident = __syncthreads_or(LVK_IDENT && ident_ok);
+    const bool ident = __syncthreads_or(ident_ok);
     if (blockIdx.x == 0 && t % kBuckets == 0) {  // per-class [start, count) for the CRC kernel
         const uint32_t c = t / kBuckets;
         ws[kWsCls + c] = ks;

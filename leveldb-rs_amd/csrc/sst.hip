@@ -62,7 +62,6 @@ struct TableUnits {
     // crc_out 32 slots of four words
     static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
-    static constexpr bool kPlainMerge = false;
     static constexpr bool kOneRound = false;
     // Wait-count mode (walk.h sorted_stream): verify runs mode 2 (every load
     // unconditional within its path: 0.703 -> 0.723 against the session-start
@@ -70,7 +69,7 @@ struct TableUnits {
     // 2: 0.667 -> 0.639, and with its trailer stores unconditional too 0.667
     // -> 0.640, seal_exact/; mode 1, the tail and trailer re-read every step:
     // seal 0.67 -> 0.61, verify 0.69 -> 0.64; mode2_ab/, exact_ab/)
-    static constexpr uint32_t kExact = SEAL ? 0u : LVK_TABLE_EXACT;
+    static constexpr uint32_t kExact = SEAL ? 0u : 2u;
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const uint64_t u = sst_unit(e);
@@ -135,11 +134,7 @@ struct TableUnits {
         if constexpr (SEAL) {
             if (lane >= nslots) return;
             const uint32_t bi = g_oidx[wave][lane];
-            if (bi == 0xffffffffu || LVK_EXP_NOSEALWRITE) return;
-            if (LVK_EXP_SEAL_COMPACT) {  // timing only: the masked crc to a per-block word, no trailer
-                reinterpret_cast<uint32_t *>(P.base)[bi] = g_ocrc[wave][lane];  // overwrites the file's head
-                return;
-            }
+            if (bi == 0xffffffffu) return;
             const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
             const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
             uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))

@@ -165,9 +165,9 @@ def test_product_build_refuses_kernel_switches():
     import subprocess
     src = os.path.join(CSRC, "sort.hip")
     base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-E", "-o", os.devnull, src]
-    bad = subprocess.run(base + ["-DLVK_IDENT=0"], capture_output=True, text=True, timeout=300)
+    bad = subprocess.run(base + ["-DLVK_SST_RUN=1"], capture_output=True, text=True, timeout=300)
     assert bad.returncode != 0 and "LVK_* kernel switches" in bad.stderr
-    ok = subprocess.run(base + ["-DLVK_IDENT=0", "-DLVK_EXPERIMENT_BUILD=1"], capture_output=True, text=True,
+    ok = subprocess.run(base + ["-DLVK_SST_RUN=1", "-DLVK_EXPERIMENT_BUILD=1"], capture_output=True, text=True,
                         timeout=300)
     assert ok.returncode == 0, ok.stderr[-2000:]
 
