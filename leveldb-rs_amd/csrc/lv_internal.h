@@ -19,7 +19,7 @@ struct ScanChunk {
 // A scan still running (lv_wal_scan_host_pipelined): a worker thread scans
 // the log's chunks in order; readers wait for the chunk they need.
 struct ScanPipe {
-    uint64_t chunk_bytes = 0;
+    std::vector<uint64_t> lo;  // chunk k is log[lo[k], lo[k + 1]) (block-aligned; lo.back() = the log size)
     std::vector<ScanChunk> chunks;
     std::mutex m;
     std::condition_variable cv;

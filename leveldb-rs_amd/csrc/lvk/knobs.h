@@ -27,6 +27,7 @@
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_HASH_WGS_PER_CU) || \
     defined(LVK_PIPE_CHUNK_MB) || \
+    defined(LVK_PIPE_FIRST_MB) || \
     defined(LVK_MEMCPY_THREADS) || \
     defined(LVK_PIPE_COPY_THREADS) || \
     defined(LVK_WAL_UNSORT))
@@ -68,6 +69,9 @@
 #endif
 #ifndef LVK_PIPE_CHUNK_MB  // host: chunk of the pipelined WAL scan (MiB, block multiple)
 #define LVK_PIPE_CHUNK_MB 32
+#endif
+#ifndef LVK_PIPE_FIRST_MB  // host: the pipelined WAL scan's first chunk (MiB; the chunks double up to LVK_PIPE_CHUNK_MB)
+#define LVK_PIPE_FIRST_MB 2
 #endif
 #ifndef LVK_MEMCPY_THREADS  // host: threads of the pageable -> pinned staging copy
 #define LVK_MEMCPY_THREADS 8

@@ -119,8 +119,8 @@ struct lv_wal_reader {
             return true;
         }
         lvgpu_internal::ScanPipe &p = *scan->pipe;  // (the chunk arrays stay valid after a flatten)
-        const size_t k = static_cast<size_t>(hdr / p.chunk_bytes);
-        if (k >= p.chunks.size()) return false;
+        const size_t k = static_cast<size_t>(std::upper_bound(p.lo.begin(), p.lo.end(), hdr) - p.lo.begin()) - 1;
+        if (hdr >= p.lo.back() || k >= p.chunks.size()) return false;
         if (p.wait(k)) {
             lvgpu_internal::set_error(p.rc, ("WAL scan: " + p.err).c_str());
             return false;
@@ -130,8 +130,8 @@ struct lv_wal_reader {
         ch_crc = c.crc.data();
         ch_info = c.info.data();
         ch_n = c.off.size();
-        ch_lo = k * p.chunk_bytes;
-        ch_hi = ch_lo + p.chunk_bytes;
+        ch_lo = p.lo[k];
+        ch_hi = p.lo[k + 1];
         return true;
     }
 

@@ -557,8 +557,14 @@ extern "C" lv_wal_scan *lv_wal_scan_host(const uint8_t *log, size_t bytes, int d
 // next.  The worker keeps two chunks in flight on two streams: while the GPU
 // uploads and scans chunk k, the worker copies chunk k + 1 into the other
 // pinned staging slot (a pageable log) and then collects chunk k's arrays.
+// Round 6: the chunks ramp up from kPipeFirst, doubling to kPipeChunk, so
+// the Reader starts after a small first chunk instead of after a whole 32 MiB
+// one (and, for a pageable log, the CPU copy of the second one).
 constexpr uint64_t kPipeChunk = static_cast<uint64_t>(LVK_PIPE_CHUNK_MB) << 20;  // 32 MiB: 1,024 blocks
+constexpr uint64_t kPipeFirst = static_cast<uint64_t>(LVK_PIPE_FIRST_MB) << 20;  // 2 MiB
 static_assert(kPipeChunk % LV_WAL_BLOCK_SIZE == 0, "chunks are whole blocks");
+static_assert(kPipeFirst % LV_WAL_BLOCK_SIZE == 0 && kPipeFirst > 0 && kPipeFirst <= kPipeChunk,
+              "the first chunk is whole blocks, at most a full chunk");
 static_assert(kPipeChunk <= kStageBytes, "a chunk fits one staging slot");
 
 namespace {
@@ -687,8 +693,8 @@ int pipe_run(lvgpu_internal::ScanPipe *p, const uint8_t *log, size_t bytes, int 
     int rc = LV_OK;
     for (size_t k = 0; k < nch && !rc; ++k) {
         PipeSlot &sl = slot[k & 1];
-        sl.lo = k * kPipeChunk;
-        sl.len = std::min<uint64_t>(kPipeChunk, bytes - sl.lo);
+        sl.lo = p->lo[k];
+        sl.len = p->lo[k + 1] - sl.lo;
         const uint64_t nblocks = (sl.len + LV_WAL_BLOCK_SIZE - 1) / LV_WAL_BLOCK_SIZE;
         sl.cap = std::max<uint64_t>(sl.len / 256, nblocks * 8);
         rc = pipe_enqueue(sl, log, pinned);
@@ -711,8 +717,9 @@ extern "C" lv_wal_scan *lv_wal_scan_host_pipelined(const uint8_t *log, size_t by
     lv_wal_scan *scan = new lv_wal_scan();
     auto *p = new lvgpu_internal::ScanPipe();
     scan->pipe.reset(p);
-    p->chunk_bytes = kPipeChunk;
-    const size_t nch = static_cast<size_t>((bytes + kPipeChunk - 1) / kPipeChunk);
+    for (uint64_t at = 0, c = kPipeFirst; at < bytes; at += c, c = std::min(2 * c, kPipeChunk)) p->lo.push_back(at);
+    p->lo.push_back(bytes);
+    const size_t nch = p->lo.size() - 1;
     p->chunks.resize(nch);
     if (nch == 0) {
         p->flat = true;
