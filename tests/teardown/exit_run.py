@@ -9,6 +9,10 @@ import ctypes
 import os
 import sys
 
+try:
+    import torch  # noqa: F401  (the HIP runtime liblvgpu.so binds to, loaded first as lvgpu.lib() does)
+except ImportError:
+    pass
 spy = ctypes.CDLL(sys.argv[1], mode=os.RTLD_GLOBAL | os.RTLD_NOW)
 if sys.argv[2] == "bad":  # negative control: argv[3] is tests/teardown/bad_static.cc built as liblvgpu_*.so
     ctypes.CDLL(sys.argv[3]).lvgpu_bad_probe()

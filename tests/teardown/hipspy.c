@@ -3,8 +3,8 @@
  * ones made after the test armed it at interpreter exit -- i.e. from the
  * library's static destructors (__cxa_finalize), which run after Python's
  * atexit hooks and before this file's exit handler (registered first, so it
- * runs last).  Each wrapper forwards to the next definition (dlsym RTLD_NEXT):
- * the real runtime when one is loaded, or reports hipErrorNotInitialized. */
+ * runs last).  Each wrapper forwards to the runtime the library binds to
+ * (torch's, loaded first), or reports hipErrorNotInitialized without one. */
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <stdio.h>
@@ -41,6 +41,16 @@ __attribute__((constructor)) static void init(void) { atexit(report); }
 void hipspy_arm(void) { g_armed = 1; }
 long hipspy_calls(void) { return g_calls; }
 
+/* The runtime liblvgpu.so itself binds to (torch's copy, already loaded
+ * under the libamdhip64 soname), else the next definition. */
+static void *sym(const char *name) {
+    static void *rt = NULL;
+    if (!rt) rt = dlopen("libamdhip64.so.7", RTLD_NOLOAD | RTLD_NOW);
+    if (!rt) rt = dlopen("libamdhip64.so", RTLD_NOLOAD | RTLD_NOW);
+    void *f = rt ? dlsym(rt, name) : NULL;
+    return f ? f : dlsym(RTLD_NEXT, name);
+}
+
 typedef int (*fn1)(void *);
 typedef int (*fn2)(void *, size_t);
 typedef int (*fn3)(void **, size_t, unsigned);
@@ -48,7 +58,7 @@ typedef int (*fn3)(void **, size_t, unsigned);
 #define FWD1(name)                                                      \
     int name(void *p) {                                                 \
         note(#name, __builtin_return_address(0));                       \
-        fn1 f = (fn1)dlsym(RTLD_NEXT, #name);                           \
+        fn1 f = (fn1)sym(#name);                           \
         return f ? f(p) : 3; /* hipErrorNotInitialized */               \
     }
 FWD1(hipFree)
@@ -60,12 +70,12 @@ FWD1(hipEventSynchronize)
 
 int hipMalloc(void **p, size_t n) {
     note("hipMalloc", __builtin_return_address(0));
-    fn2 f = (fn2)dlsym(RTLD_NEXT, "hipMalloc");
+    fn2 f = (fn2)sym("hipMalloc");
     return f ? ((int (*)(void **, size_t))f)(p, n) : 3;
 }
 
 int hipHostMalloc(void **p, size_t n, unsigned flags) {
     note("hipHostMalloc", __builtin_return_address(0));
-    fn3 f = (fn3)dlsym(RTLD_NEXT, "hipHostMalloc");
+    fn3 f = (fn3)sym("hipHostMalloc");
     return f ? f(p, n, flags) : 3;
 }

@@ -15,4 +15,9 @@ for r in 1 2 3; do
   timeout -k 10 300 python3 bench.py --wal --cpu-seconds 0 > "$out/wal_prod_$r.json" 2>> "$out/err.txt" || exit 1
   LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_noramp.so timeout -k 10 300 python3 bench.py --wal --cpu-seconds 0 > "$out/wal_noramp_$r.json" 2>> "$out/err.txt" || exit 1
 done
+bash tools/build_variant.sh rows2 -DLVK_SST_ROWS=2 >> "$out/build.txt" 2>&1 || exit 1
+for r in 1 2; do
+  timeout -k 10 200 python3 bench.py --table --cpu-seconds 0 > "$out/table_prod_$r.json" 2>> "$out/err.txt" || exit 1
+  LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_rows2.so timeout -k 10 200 python3 bench.py --table --cpu-seconds 0 > "$out/table_rows2_$r.json" 2>> "$out/err.txt" || exit 1
+done
 echo pass3 done
