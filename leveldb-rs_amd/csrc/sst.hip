@@ -295,7 +295,111 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
             total += static_cast<uint32_t>(pen[i] - pst[i] + 1);
         }
         const uint32_t steps = wave_max_u32(total, 16);
-        // current unit (cursor c) and prefetch cursor (p): unit index, row
+        uint32_t A = 0, S = 0;
+        bool sw = false, h1 = false, h2 = false;
+        uint4 T1 = make_uint4(0, 0, 0, 0), T2 = T1;
+        // granule load of row r for this lane (zeros outside the file or past the plan)
+        auto load_row = [&](int32_t r, bool on) -> uint4 {
+            const int32_t q16 = r * 256 + static_cast<int32_t>(gl) * 16;
+            const bool in = on && q16 + 16 > a.fbeg && q16 < a.fend;
+            return load16(in ? a.origin + static_cast<uint32_t>(q16) : reinterpret_cast<uint64_t>(&g_zero_granules[gl]));
+        };
+        // The row step every path shares: fix-up, snapshot, fold, tail capture.
+        // cA / cAn: starts of the current and next unit, cGe: the current unit's
+        // last whole granule (all origin-relative), s0 / s0n their seed words.
+        auto fold_row = [&](const uint4 &vr, int32_t row, int32_t cA, int32_t cAn, int32_t cGe, uint32_t s0,
+                            uint32_t s0n, bool act) {
+            const int32_t q = row * 16 + static_cast<int32_t>(gl);
+            const bool onNext = q > cGe;
+            uint4 v = vr;
+            const int32_t at = onNext ? cAn : cA;
+            if (__any(act && q * 16 < at + 4)) {  // bytes before a unit's start, or its first 4
+                const int32_t rel = q * 16 - at;
+                const uint32_t sd = onNext ? s0n : s0;
+                v.x = fix_word(v.x, rel, sd);
+                v.y = fix_word(v.y, rel + 4, sd);
+                v.z = fix_word(v.z, rel + 8, sd);
+                v.w = fix_word(v.w, rel + 12, sd);
+            }
+            const bool swn = onNext && !sw;  // this lane's first granule past the unit
+            S = swn ? A : S;
+            A = swn ? 0u : A;
+            sw = sw || onNext;
+            A = lookup4x<kRegionA + kHalf>(A, r0_granule(v, L), L);  // Shift_256(A) ^ R(0, v)
+            if (__any(act && (q == cGe + 1 || q == cGe + 2))) {
+                if (q == cGe + 1) {
+                    T1 = vr;
+                    h1 = true;
+                }
+                if (q == cGe + 2) {
+                    T2 = vr;
+                    h2 = true;
+                }
+            }
+        };
+        // unit slot k's state: the 16 snapshots and the raw granules
+        auto emit = [&](uint32_t k) {
+            uint32_t *su = st + (grp * 4u + k) * kStateWords;
+            su[gl] = sw ? S : A;
+            if (h1) {
+                su[16] = T1.x;
+                su[17] = T1.y;
+                su[18] = T1.z;
+                su[19] = T1.w;
+            }
+            if (h2) {
+                su[20] = T2.x;
+                su[21] = T2.y;
+                su[22] = T2.z;
+                su[23] = T2.w;
+            }
+            h1 = h2 = sw = false;
+        };
+        if (__all(pok[0] && pch[1] && pch[2] && pch[3])) {
+            // Every group's four blocks follow each other (the bench's and a
+            // table's layout): one row range per group, the units a queue.
+            const int32_t rlast = (pge[3] + 2) >> 4;
+            int32_t row = pa[0] >> 8, prow = row;
+            int32_t qa0 = pa[0], qa1 = pa[1], qa2 = pa[2], qa3 = pa[3];
+            int32_t qg0 = pge[0], qg1 = pge[1], qg2 = pge[2], qg3 = pge[3];
+            int32_t cEnd = (qg0 >> 4) + 1;
+            uint32_t k = 0;
+            uint4 ring[kStreamRing];
+#pragma unroll
+            for (uint32_t i = 0; i < kStreamRing; ++i, ++prow) ring[i] = load_row(prow, prow <= rlast);
+            auto fstep = [&](uint4 &slot) {
+                const uint4 vr = slot;
+                slot = load_row(prow, prow <= rlast);
+                ++prow;
+                // (chained blocks are >= 1 KiB: both seed words are ~0)
+                fold_row(vr, row, qa0, qa1, qg0, 0xffffffffu, 0xffffffffu, k < 4u);
+                if (__any(row == cEnd)) {
+                    if (row == cEnd) {
+                        emit(k);
+                        ++k;
+                        qa0 = qa1;
+                        qa1 = qa2;
+                        qa2 = qa3;
+                        qa3 = kFar;
+                        qg0 = qg1;
+                        qg1 = qg2;
+                        qg2 = qg3;
+                        cEnd = k < 3u ? (qg0 >> 4) + 1 : (k == 3u ? rlast : -1);
+                    }
+                }
+                ++row;
+            };
+            for (uint32_t t = 0; t < steps; t += kStreamRing) {  // wave-uniform
+#pragma unroll
+                for (uint32_t i = 0; i < kStreamRing; ++i) {
+                    if (t + i >= steps) break;
+                    fstep(ring[i]);
+                }
+            }
+        } else {
+        // The general plan: any block that does not follow its predecessor is
+        // a stream of its own.  Current unit (cursor c) and prefetch cursor
+        // (p): unit index, row
         // (v[i] for a run-time i as selects of copies: an indexed read of the
         // array put the arrays in scratch)
         const int32_t pa0 = pa[0], pa1 = pa[1], pa2 = pa[2], pa3 = pa[3];
@@ -317,12 +421,6 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
         skip(ci);
         int pi = ci;
         int32_t prow = pi < 4 ? SST_SEL(ps, pi) : 0;
-        // granule load of row r for this lane (zeros outside the file or past the plan)
-        auto load_row = [&](int32_t r, bool on) -> uint4 {
-            const int32_t q16 = r * 256 + static_cast<int32_t>(gl) * 16;
-            const bool in = on && q16 + 16 > a.fbeg && q16 < a.fend;
-            return load16(in ? a.origin + static_cast<uint32_t>(q16) : reinterpret_cast<uint64_t>(&g_zero_granules[gl]));
-        };
         auto pf_next = [&]() -> uint4 {  // the prefetch cursor's row, then advance it
             const bool on = pi < 4;
             const uint4 v = load_row(prow, on);
@@ -355,57 +453,14 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
             }
         };
         load_cur();
-        uint32_t A = 0, S = 0;
-        bool sw = false, h1 = false, h2 = false;
-        uint4 T1 = make_uint4(0, 0, 0, 0), T2 = T1;
         auto step = [&](uint4 &slot) {
             const uint4 vr = slot;
             slot = pf_next();
             const bool act = ci < 4;
-            const int32_t q = row * 16 + static_cast<int32_t>(gl);
-            const bool onNext = q > cGe;
-            uint4 v = vr;
-            const int32_t at = onNext ? cAn : cA;
-            if (__any(act && q * 16 < at + 4)) {  // bytes before a unit's start, or its first 4
-                const int32_t rel = q * 16 - at;
-                const uint32_t s0 = onNext ? cS0n : cS0;
-                v.x = fix_word(v.x, rel, s0);
-                v.y = fix_word(v.y, rel + 4, s0);
-                v.z = fix_word(v.z, rel + 8, s0);
-                v.w = fix_word(v.w, rel + 12, s0);
-            }
-            const bool swn = onNext && !sw;  // this lane's first granule past the unit
-            S = swn ? A : S;
-            A = swn ? 0u : A;
-            sw = sw || onNext;
-            A = lookup4x<kRegionA + kHalf>(A, r0_granule(v, L), L);  // Shift_256(A) ^ R(0, v)
-            if (__any(act && (q == cGe + 1 || q == cGe + 2))) {
-                if (q == cGe + 1) {
-                    T1 = vr;
-                    h1 = true;
-                }
-                if (q == cGe + 2) {
-                    T2 = vr;
-                    h2 = true;
-                }
-            }
+            fold_row(vr, row, cA, cAn, cGe, cS0, cS0n, act);
             if (__any(act && row == cEnd)) {
                 if (act && row == cEnd) {  // group-uniform: unit ci is done for every lane
-                    uint32_t *su = st + (grp * 4u + static_cast<uint32_t>(ci)) * kStateWords;
-                    su[gl] = sw ? S : A;
-                    if (h1) {
-                        su[16] = T1.x;
-                        su[17] = T1.y;
-                        su[18] = T1.z;
-                        su[19] = T1.w;
-                    }
-                    if (h2) {
-                        su[20] = T2.x;
-                        su[21] = T2.y;
-                        su[22] = T2.z;
-                        su[23] = T2.w;
-                    }
-                    h1 = h2 = sw = false;
+                    emit(static_cast<uint32_t>(ci));
                     const bool ch = chained(ci + 1);
                     if (!ch) A = 0u;
                     ++ci;
@@ -425,6 +480,7 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
             }
         }
 #undef SST_SEL
+        }
         __builtin_amdgcn_wave_barrier();
         // lane u < 16 finishes unit u of the claim
         if (lane < 16 && um < a.n) {
