@@ -355,24 +355,41 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
             }
             h1 = h2 = sw = false;
         };
-        if (__all(pok[0] && pch[1] && pch[2] && pch[3])) {
+        const int32_t rfirst = pa[0] >> 8, rlast = (pge[3] + 2) >> 4;
+        if (__all(pok[0] && pch[1] && pch[2] && pch[3] && rfirst * 256 >= a.fbeg && (rlast + 1) * 256 <= a.fend)) {
             // Every group's four blocks follow each other (the bench's and a
-            // table's layout): one row range per group, the units a queue.
-            const int32_t rlast = (pge[3] + 2) >> 4;
-            int32_t row = pa[0] >> 8, prow = row;
+            // table's layout) and its rows lie inside the file: one row range
+            // per group, the units a queue, rows loaded unguarded.
+            int32_t row = rfirst, prow = row;
             int32_t qa0 = pa[0], qa1 = pa[1], qa2 = pa[2], qa3 = pa[3];
             int32_t qg0 = pge[0], qg1 = pge[1], qg2 = pge[2], qg3 = pge[3];
             int32_t cEnd = (qg0 >> 4) + 1;
             uint32_t k = 0;
+            const uint64_t zero = reinterpret_cast<uint64_t>(&g_zero_granules[gl]);
+            uint64_t pp = a.origin + static_cast<uint32_t>(row * 256) + 16u * gl;  // row prow's granule
             uint4 ring[kStreamRing];
 #pragma unroll
-            for (uint32_t i = 0; i < kStreamRing; ++i, ++prow) ring[i] = load_row(prow, prow <= rlast);
+            for (uint32_t i = 0; i < kStreamRing; ++i, ++prow, pp += 256) ring[i] = load16(prow <= rlast ? pp : zero);
             auto fstep = [&](uint4 &slot) {
-                const uint4 vr = slot;
-                slot = load_row(prow, prow <= rlast);
-                ++prow;
+                // (the slot is refilled after its row is folded: no copy of it
+                // is kept live across the new load)
+                auto refill = [&]() {
+                    slot = load16(prow <= rlast ? pp : zero);
+                    ++prow;
+                    pp += 256;
+                };
+                // Rows strictly inside a block -- after the run's first row and
+                // before the row of the block's last whole granule -- need no
+                // fix-up, switch, capture or emit: the plain Horner step.
+                if (!__any(row == rfirst || row >= (qg0 >> 4))) {
+                    A = lookup4x<kRegionA + kHalf>(A, r0_granule(slot, L), L);
+                    refill();
+                    ++row;
+                    return;
+                }
                 // (chained blocks are >= 1 KiB: both seed words are ~0)
-                fold_row(vr, row, qa0, qa1, qg0, 0xffffffffu, 0xffffffffu, k < 4u);
+                fold_row(slot, row, qa0, qa1, qg0, 0xffffffffu, 0xffffffffu, k < 4u);
+                refill();
                 if (__any(row == cEnd)) {
                     if (row == cEnd) {
                         emit(k);
