@@ -378,10 +378,11 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
                     ++prow;
                     pp += 256;
                 };
-                // Rows strictly inside a block -- after the run's first row and
+                // Rows strictly inside a block -- after the run's first two
+                // rows (its first block's seed bytes may reach the second) and
                 // before the row of the block's last whole granule -- need no
                 // fix-up, switch, capture or emit: the plain Horner step.
-                if (!__any(row == rfirst || row >= (qg0 >> 4))) {
+                if (!__any(row <= rfirst + 1 || row >= (qg0 >> 4))) {
                     A = lookup4x<kRegionA + kHalf>(A, r0_granule(slot, L), L);
                     refill();
                     ++row;
