@@ -367,30 +367,49 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
             uint32_t k = 0;
             const uint64_t zero = reinterpret_cast<uint64_t>(&g_zero_granules[gl]);
             uint64_t pp = a.origin + static_cast<uint32_t>(row * 256) + 16u * gl;  // row prow's granule
+            // (nothing of the previous claim -- its status stores -- is left in
+            // flight, so the ring's wait counts are exact from the first row)
+            __builtin_amdgcn_s_waitcnt(0);
             uint4 ring[kStreamRing];
 #pragma unroll
             for (uint32_t i = 0; i < kStreamRing; ++i, ++prow, pp += 256) ring[i] = load16(prow <= rlast ? pp : zero);
+            // One row per step.  Every use of the slot's granule comes before
+            // its one refill, so each ring slot keeps its registers (a refill
+            // on two paths, or a copy of a slot past its refill, made the
+            // compiler copy loads still in flight and wait for them all).
             auto fstep = [&](uint4 &slot) {
-                // (the slot is refilled after its row is folded: no copy of it
-                // is kept live across the new load)
-                auto refill = [&]() {
-                    slot = load16(prow <= rlast ? pp : zero);
-                    ++prow;
-                    pp += 256;
-                };
-                // Rows strictly inside a block -- after the run's first two
-                // rows (its first block's seed bytes may reach the second) and
-                // before the row of the block's last whole granule -- need no
-                // fix-up, switch, capture or emit: the plain Horner step.
-                if (!__any(row <= rfirst + 1 || row >= (qg0 >> 4))) {
-                    A = lookup4x<kRegionA + kHalf>(A, r0_granule(slot, L), L);
-                    refill();
-                    ++row;
-                    return;
+                const int32_t q = row * 16 + static_cast<int32_t>(gl);
+                const bool onNext = q > qg0;  // past the current block's last whole granule
+                const int32_t at = onNext ? qa1 : qa0;
+                uint4 v = slot;
+                if (__any(k < 4u && q * 16 < at + 4)) {  // bytes before a block's start, or its first 4
+                    // (chained blocks are >= 1 KiB: the seed word is ~0)
+                    const int32_t rel = q * 16 - at;
+                    v.x = fix_word(v.x, rel, 0xffffffffu);
+                    v.y = fix_word(v.y, rel + 4, 0xffffffffu);
+                    v.z = fix_word(v.z, rel + 8, 0xffffffffu);
+                    v.w = fix_word(v.w, rel + 12, 0xffffffffu);
                 }
-                // (chained blocks are >= 1 KiB: both seed words are ~0)
-                fold_row(slot, row, qa0, qa1, qg0, 0xffffffffu, 0xffffffffu, k < 4u);
-                refill();
+                const uint32_t f = r0_granule(v, L);
+                if (__any(k < 4u && (q == qg0 + 1 || q == qg0 + 2))) {
+                    if (q == qg0 + 1) {
+                        T1 = slot;
+                        h1 = true;
+                    }
+                    if (q == qg0 + 2) {
+                        T2 = slot;
+                        h2 = true;
+                    }
+                }
+                slot = load16(prow <= rlast ? pp : zero);
+                ++prow;
+                pp += 256;
+                uint32_t wa = lookup4<kRegionA + kHalf>(A, L);  // Shift_256(A)
+                const bool swn = onNext && !sw;  // this lane's first granule past the block: snapshot, restart
+                S = swn ? A : S;
+                wa = swn ? 0u : wa;
+                sw = sw || onNext;
+                A = wa ^ f;
                 if (__any(row == cEnd)) {
                     if (row == cEnd) {
                         emit(k);
@@ -407,13 +426,20 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
                 }
                 ++row;
             };
-            for (uint32_t t = 0; t < steps; t += kStreamRing) {  // wave-uniform
+            // exits leave the loop: only the path through all kStreamRing steps
+            // returns to its head (an exit back to the head made the compiler
+            // wait for every load there)
+            // (the compiler still waits for every load at the loop's head: two
+            // passes over the ring per iteration halve those waits)
+            for (uint32_t t = 0;;) {
+                static_assert(kStreamRing == 8, "the ring's steps are spelled out");
 #pragma unroll
-                for (uint32_t i = 0; i < kStreamRing; ++i) {
-                    if (t + i >= steps) break;
-                    fstep(ring[i]);
+                for (uint32_t i = 0; i < 2 * kStreamRing; ++i) {
+                    fstep(ring[i % kStreamRing]);
+                    if (++t >= steps) goto done;
                 }
             }
+        done:;
         } else {
         // The general plan: any block that does not follow its predecessor is
         // a stream of its own.  Current unit (cursor c) and prefetch cursor
