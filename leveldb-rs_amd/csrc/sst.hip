@@ -251,16 +251,88 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
     const Lut L = make_lut(lane);
     uint32_t *const st = g_lds + kRegionB / 4 + wave * kStatePerWave;
     const uint64_t nclaims = (a.n + kClaimUnits - 1) / kClaimUnits;
-    for (;;) {
+    // Lane u < 16 finishes unit u of a claim whose walk is done (its states
+    // in st): Horner over the 16 snapshots from the lane furthest from the
+    // block's last whole granule, the tail fold, then the compare or trailer.
+    auto finish = [&](uint64_t fum, bool fok, int32_t fua, int32_t fub) {
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 16 && fum < a.n) {
+            const uint32_t *su = st + lane * kStateWords;
+            uint32_t crc = 0, stv = LV_SST_BLOCK_OUT_OF_RANGE;
+            if (fok) {
+                const int32_t ge = (fub >> 4) - 1;
+                const uint32_t e = static_cast<uint32_t>(ge) & 15u;
+                uint32_t X = 0;
+#pragma unroll
+                for (uint32_t t2 = 0; t2 < 16; ++t2) X = comb_shift(X, 0) ^ su[(e + 1u + t2) & 15u];
+                const uint4 t1 = make_uint4(su[16], su[17], su[18], su[19]);
+                RGeo g;
+                g.a = a.origin + static_cast<uint32_t>(fua);
+                g.len = static_cast<uint32_t>(fub - fua);
+                g.seed = 0;
+                g.bid = 0;
+                g.aux = 0;
+                X = finish_raw(g, X, t1, 0u, L);
+                if constexpr (SEAL) {
+                    const uint32_t ty = a.types ? a.types[fum] : 0u;
+                    crc = mask_crc(~byte_step(X, ty));
+                    uint8_t *p = reinterpret_cast<uint8_t *>(a.origin + static_cast<uint32_t>(fub));  // type, LE32(mask(crc))
+                    p[0] = static_cast<uint8_t>(ty);
+                    p[1] = static_cast<uint8_t>(crc);
+                    p[2] = static_cast<uint8_t>(crc >> 8);
+                    p[3] = static_cast<uint8_t>(crc >> 16);
+                    p[4] = static_cast<uint8_t>(crc >> 24);
+                } else {
+                    crc = ~X;
+                    const uint32_t k = static_cast<uint32_t>(fub) & 15u;  // the stored CRC: bytes k..k+3 of T1 || T2
+                    const uint32_t w[8] = {su[16], su[17], su[18], su[19], su[20], su[21], su[22], su[23]};
+                    const uint32_t d = k >> 2, sh = (k & 3u) * 8u;
+                    uint32_t lo = 0, hi = 0;
+#pragma unroll
+                    for (uint32_t i = 0; i < 7; ++i)
+                        if (i == d) {
+                            lo = w[i];
+                            hi = w[i + 1];
+                        }
+                    const uint32_t stored = sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
+                    const uint32_t r = stored - 0xa282ead8u;  // unmask, crc32c.rs:59-63
+                    stv = ((r >> 17) | (r << 15)) == crc ? LV_SST_BLOCK_OK : LV_SST_BLOCK_CHECKSUM_MISMATCH;
+                }
+            }
+            if constexpr (!SEAL) {
+                a.status[fum] = stv;
+                if (CRCOUT && a.crc_out) a.crc_out[fum] = fok ? crc : 0u;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // the states are read before the next walk writes them
+    };
+    // Claims are pipelined: the next claim's handles are requested when a walk
+    // starts, and a claim's unit finish runs after the next claim's first rows
+    // are requested, so neither round trip sits between two walks.
+    auto take = [&]() -> uint64_t {
         uint32_t kc = 0;
         if (lane == 0) kc = atomicAdd(&g_lds[kPoolWord], 1u);
-        const uint64_t claim = blockIdx.x + gridDim.x * static_cast<uint64_t>(__shfl(kc, 0));
-        if (claim >= nclaims) break;  // wave-uniform
+        return blockIdx.x + gridDim.x * static_cast<uint64_t>(__shfl(kc, 0));
+    };
+    // lane l < 16 loads block c * kClaimUnits + l (group l / 4, run position
+    // l % 4); the others load a copy
+    auto handles_of = [&](uint64_t c, uint2 &h0, uint2 &h1) {
+        const uint64_t u = c * kClaimUnits + (lane & 15u), uc = u < a.n ? u : a.n - 1;
+        h0 = a.handles[2 * uc];
+        h1 = a.handles[2 * uc + 1];
+    };
+    uint64_t claim = take();
+    if (claim >= nclaims) return;  // wave-uniform
+    uint2 ho, hs, hon, hsn;
+    handles_of(claim, ho, hs);
+    uint64_t prv_um = 0;
+    bool prv_ok = false, have_prv = false;
+    int32_t prv_a = 0, prv_b = 0;
+    for (;;) {
         const uint64_t u0 = claim * kClaimUnits;
-        // lane l < 16 loads block u0 + l (group l / 4, run position l % 4); the
-        // others load a copy
-        const uint64_t um = u0 + (lane & 15u), uc = um < a.n ? um : a.n - 1;
-        const uint2 ho = a.handles[2 * uc], hs = a.handles[2 * uc + 1];
+        const uint64_t um = u0 + (lane & 15u);
+        const uint64_t next = take();
+        handles_of(next < nclaims ? next : claim, hon, hsn);
         const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
         const bool uok = um < a.n && sst_in_range(o, sz, a.file_bytes);
         const int32_t ua = uok ? a.fbeg + static_cast<int32_t>(o) : 0;
@@ -367,12 +439,10 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
             uint32_t k = 0;
             const uint64_t zero = reinterpret_cast<uint64_t>(&g_zero_granules[gl]);
             uint64_t pp = a.origin + static_cast<uint32_t>(row * 256) + 16u * gl;  // row prow's granule
-            // (nothing of the previous claim -- its status stores -- is left in
-            // flight, so the ring's wait counts are exact from the first row)
-            __builtin_amdgcn_s_waitcnt(0);
             uint4 ring[kStreamRing];
 #pragma unroll
             for (uint32_t i = 0; i < kStreamRing; ++i, ++prow, pp += 256) ring[i] = load16(prow <= rlast ? pp : zero);
+            if (have_prv) finish(prv_um, prv_ok, prv_a, prv_b);  // under the first rows' round trip
             // One row per step.  Every use of the slot's granule comes before
             // its one refill, so each ring slot keeps its registers (a refill
             // on two paths, or a copy of a slot past its refill, made the
@@ -381,16 +451,8 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
                 const int32_t q = row * 16 + static_cast<int32_t>(gl);
                 const bool onNext = q > qg0;  // past the current block's last whole granule
                 const int32_t at = onNext ? qa1 : qa0;
-                uint4 v = slot;
-                if (__any(k < 4u && q * 16 < at + 4)) {  // bytes before a block's start, or its first 4
-                    // (chained blocks are >= 1 KiB: the seed word is ~0)
-                    const int32_t rel = q * 16 - at;
-                    v.x = fix_word(v.x, rel, 0xffffffffu);
-                    v.y = fix_word(v.y, rel + 4, 0xffffffffu);
-                    v.z = fix_word(v.z, rel + 8, 0xffffffffu);
-                    v.w = fix_word(v.w, rel + 12, 0xffffffffu);
-                }
-                const uint32_t f = r0_granule(v, L);
+                // the raw granules first, then the fix-up in place (the slot is
+                // dead after its fold: no copy of it)
                 if (__any(k < 4u && (q == qg0 + 1 || q == qg0 + 2))) {
                     if (q == qg0 + 1) {
                         T1 = slot;
@@ -401,6 +463,15 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
                         h2 = true;
                     }
                 }
+                if (__any(k < 4u && q * 16 < at + 4)) {  // bytes before a block's start, or its first 4
+                    // (chained blocks are >= 1 KiB: the seed word is ~0)
+                    const int32_t rel = q * 16 - at;
+                    slot.x = fix_word(slot.x, rel, 0xffffffffu);
+                    slot.y = fix_word(slot.y, rel + 4, 0xffffffffu);
+                    slot.z = fix_word(slot.z, rel + 8, 0xffffffffu);
+                    slot.w = fix_word(slot.w, rel + 12, 0xffffffffu);
+                }
+                const uint32_t f = r0_granule(slot, L);
                 slot = load16(prow <= rlast ? pp : zero);
                 ++prow;
                 pp += 256;
@@ -481,6 +552,7 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
         uint4 ring[kStreamRing];
 #pragma unroll
         for (uint32_t s = 0; s < kStreamRing; ++s) ring[s] = pf_next();
+        if (have_prv) finish(prv_um, prv_ok, prv_a, prv_b);
         // current unit's values
         int32_t row = ci < 4 ? SST_SEL(ps, ci) : 0;
         int32_t cA = 0, cGe = -1, cEnd = -1, cAn = kFar;
@@ -525,58 +597,17 @@ __global__ __launch_bounds__(kThreads) void sst_stream_kernel(SstStream a, const
         }
 #undef SST_SEL
         }
-        __builtin_amdgcn_wave_barrier();
-        // lane u < 16 finishes unit u of the claim
-        if (lane < 16 && um < a.n) {
-            const uint32_t *su = st + lane * kStateWords;
-            uint32_t crc = 0, stv = LV_SST_BLOCK_OUT_OF_RANGE;
-            if (uok) {
-                const int32_t ge = (ub >> 4) - 1;
-                const uint32_t e = static_cast<uint32_t>(ge) & 15u;
-                uint32_t X = 0;
-#pragma unroll
-                for (uint32_t t2 = 0; t2 < 16; ++t2) X = comb_shift(X, 0) ^ su[(e + 1u + t2) & 15u];
-                const uint4 t1 = make_uint4(su[16], su[17], su[18], su[19]);
-                RGeo g;
-                g.a = a.origin + static_cast<uint32_t>(ua);
-                g.len = static_cast<uint32_t>(ub - ua);
-                g.seed = 0;
-                g.bid = 0;
-                g.aux = 0;
-                X = finish_raw(g, X, t1, 0u, L);
-                if constexpr (SEAL) {
-                    const uint32_t ty = a.types ? a.types[um] : 0u;
-                    crc = mask_crc(~byte_step(X, ty));
-                    uint8_t *p = reinterpret_cast<uint8_t *>(a.origin + static_cast<uint32_t>(ub));  // type, LE32(mask(crc))
-                    p[0] = static_cast<uint8_t>(ty);
-                    p[1] = static_cast<uint8_t>(crc);
-                    p[2] = static_cast<uint8_t>(crc >> 8);
-                    p[3] = static_cast<uint8_t>(crc >> 16);
-                    p[4] = static_cast<uint8_t>(crc >> 24);
-                } else {
-                    crc = ~X;
-                    const uint32_t k = static_cast<uint32_t>(ub) & 15u;  // the stored CRC: bytes k..k+3 of T1 || T2
-                    const uint32_t w[8] = {su[16], su[17], su[18], su[19], su[20], su[21], su[22], su[23]};
-                    const uint32_t d = k >> 2, sh = (k & 3u) * 8u;
-                    uint32_t lo = 0, hi = 0;
-#pragma unroll
-                    for (uint32_t i = 0; i < 7; ++i)
-                        if (i == d) {
-                            lo = w[i];
-                            hi = w[i + 1];
-                        }
-                    const uint32_t stored = sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
-                    const uint32_t r = stored - 0xa282ead8u;  // unmask, crc32c.rs:59-63
-                    stv = ((r >> 17) | (r << 15)) == crc ? LV_SST_BLOCK_OK : LV_SST_BLOCK_CHECKSUM_MISMATCH;
-                }
-            }
-            if constexpr (!SEAL) {
-                a.status[um] = stv;
-                if (CRCOUT && a.crc_out) a.crc_out[um] = uok ? crc : 0u;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();  // the states are read before the next claim writes them
+        prv_um = um;
+        prv_ok = uok;
+        prv_a = ua;
+        prv_b = ub;
+        have_prv = true;
+        if (next >= nclaims) break;  // wave-uniform
+        claim = next;
+        ho = hon;
+        hs = hsn;
     }
+    if (have_prv) finish(prv_um, prv_ok, prv_a, prv_b);
 }
 
 }  // namespace lvk
