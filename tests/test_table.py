@@ -180,8 +180,7 @@ def test_gpu_trailer_fixture(gpu, tfix, arena):
 @pytest.mark.gpu
 def test_gpu_table_one_launch_any_order(gpu):
     """Seal and verify are one kernel launch that walks the handles in the
-    order given (no length sort; blocks that follow each other in the file are
-    streamed together, every other one alone): shuffled handles, sizes 0-70,000 B mixed
+    order given (no length sort): shuffled handles, sizes 0-70,000 B mixed
     (several rows-per-round shapes in one wave), a count that is not a
     multiple of the 4 blocks of a wave round, random types, crc output."""
     import lvgpu
@@ -196,16 +195,16 @@ def test_gpu_table_one_launch_any_order(gpu):
     d = torch.frombuffer(bytearray(file), dtype=torch.uint8).to(gpu)
     h = torch.tensor(handles, dtype=torch.int64, device=gpu)
     LT.seal_blocks(d, h, torch.from_numpy(types).to(gpu))
-    assert lvgpu.last_kernel() == "sst_stream_kernel<seal>"
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<seal>"
     want = _oracle_seal(file, handles, types.tolist())
     assert d.cpu().numpy().tobytes() == want
     st, crc = LT.verify_blocks(d, h, out_crc=True)
-    assert lvgpu.last_kernel() == "sst_stream_kernel<verify,crc>"
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<verify,crc>"
     assert st.cpu().numpy().tolist() == [0] * len(handles)
     got = crc.cpu().numpy().view(np.uint32).tolist()
     assert got == [W.value(want[o:o + sz + 1]) for o, sz in handles]
     st = LT.verify_blocks(d, h)  # status only: the two-word staging
-    assert lvgpu.last_kernel() == "sst_stream_kernel<verify>"
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<verify>"
     assert st.cpu().numpy().tolist() == [0] * len(handles)
 
 
@@ -233,10 +232,10 @@ def test_gpu_seal_without_types(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shift", [0, 3, 200])
-def test_gpu_table_stream_file_order(gpu, shift):
-    """The continuous walk over blocks that follow each other (the bench's
-    layout: 4096 + U[0, 256) B blocks with their 5-B trailers, in file order)
-    with the file at an offset from a 256-B boundary, a block count that is
+def test_gpu_table_file_order(gpu, shift):
+    """Blocks that follow each other (the bench's layout: 4096 + U[0, 256) B
+    blocks with their 5-B trailers, in file order, walked in runs of four per
+    group) with the file at an offset from a 256-B boundary, a block count that is
     not a multiple of a claim's 16, runs broken by a long block, a short one
     and an out-of-range handle, and corrupted bytes: seal == oracle, verify
     statuses (mismatch exactly where corrupted) and CRCs == oracle."""
@@ -257,7 +256,7 @@ def test_gpu_table_stream_file_order(gpu, shift):
     h = torch.tensor(np.array(hl, dtype=np.uint64).view(np.int64), device=gpu)
     tl = np.concatenate([types[:130], [0], types[130:]]).astype(np.uint8)
     LT.seal_blocks(d, h, torch.from_numpy(tl).to(gpu))
-    assert lvgpu.last_kernel() == "sst_stream_kernel<seal>"
+    assert lvgpu.last_kernel() == "sst_blocks_kernel<seal>"
     assert d.cpu().numpy().tobytes() == want
     bad = sorted(int(x) for x in rng.choice(len(handles), size=12, replace=False))
     for k in bad:
