@@ -242,6 +242,56 @@ def measure_traffic(args, shard_rank=0, shard_world=1):
     return t, "rocprofv3 --pmc FETCH_SIZE (x2 gfx950 correction), per step: sum over the call's kernels of each kernel's mean"
 
 
+def pmc_per_kernel(bench_args, counter):
+    """Child process: one rocprofv3 --pmc pass of `counter` (FETCH_SIZE or
+    WRITE_SIZE, kernel counters only, its own run) over bench.py with
+    `bench_args`; returns {kernel: mean bytes per launch} for the lvk::
+    kernels (FETCH_SIZE doubled per the gfx950 correction, WRITE_SIZE as read:
+    MI355X_MICROARCH.md §HBM), or (None, reason)."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return None, "skipped (running under rocprofv3)"
+    out = tempfile.mkdtemp(prefix="lvgpu_pmc_", dir="/tmp")
+    cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+           sys.executable, os.path.abspath(__file__)] + bench_args
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       timeout=300, check=True)
+    except Exception as e:  # noqa: BLE001 - report, never fail the bench on the profiler
+        shutil.rmtree(out, ignore_errors=True)
+        return None, f"rocprofv3 pass failed: {e}"
+    per = {}
+    for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+        per.update(read_pmc_per_kernel(f, counter))
+    shutil.rmtree(out, ignore_errors=True)
+    if not per:
+        return None, "no lvk:: kernel in the pass"
+    return per, f"rocprofv3 --pmc {counter}, mean per launch"
+
+
+def read_pmc_per_kernel(path, counter):
+    """{kernel: mean bytes per launch} of `counter` over the lvk:: kernels of a
+    rocprofv3 counter CSV (fill kernels excluded; FETCH_SIZE KiB doubled for
+    gfx950's half-counted wide reads, WRITE_SIZE KiB as read)."""
+    import collections
+    import csv
+    scale = 2.0 * 1024.0 if counter == "FETCH_SIZE" else 1024.0
+    per = collections.defaultdict(list)
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            name = row.get("Kernel_Name", "")
+            if "lvk::" in name and "fill_" not in name and row.get("Counter_Name") == counter:
+                per[name.split("(")[0].replace("void ", "")].append(float(row["Counter_Value"]) * scale)
+    return {k: sum(v) / len(v) for k, v in per.items()}
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -721,6 +771,24 @@ def wal_device_bench(args):
     variant = os.environ.get("LVGPU_EXPERIMENT") == "1"
     if not variant:  # the oracle's verify of the whole log, untimed (the cpu_baseline below times it)
         wal_oracle_check(log, cap)
+    # HBM traffic per call: FETCH_SIZE and WRITE_SIZE per kernel,
+    # each in its own child pass over the same log and scan
+    traffic = None
+    if args.traffic == "auto":
+        child = ["--wal-device", "--steps", "10", "--warmup", "5", "--cpu-seconds", "0", "--traffic", "off",
+                 "--no-settle"] + (["--blocks", str(args.blocks)] if args.blocks else [])
+        fetch, fsrc = pmc_per_kernel(child, "FETCH_SIZE")
+        write, wsrc = pmc_per_kernel(child, "WRITE_SIZE")
+        if isinstance(fetch, dict):
+            traffic = {"fetch_bytes_per_call": round(sum(fetch.values())),
+                       "fetch_over_log_bytes": round(sum(fetch.values()) / log.size, 4),
+                       "per_kernel_fetch": {k: round(v) for k, v in fetch.items()},
+                       "source": fsrc + " (x2 gfx950 correction); the call's kernels summed"}
+            if isinstance(write, dict):
+                traffic["write_bytes_per_call"] = round(sum(write.values()))
+                traffic["per_kernel_write"] = {k: round(v) for k, v in write.items()}
+        else:
+            traffic = {"error": fsrc}
     cpu = wal_cpu_baseline(log, args.cpu_seconds, cap) if args.cpu_seconds > 0 and not variant else None
     gbs = log.size / (avg * 1e-3) / 1e9
     res = {"metric": "device-resident WAL verify scan (framing + CRC of every record), HBM", "unit": "GB/s",
@@ -728,7 +796,9 @@ def wal_device_bench(args):
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_avg": round(avg, 4), "ms_p50": round(p50, 4),
                         "bytes_per_call": int(log.size),
-                        "kernels": lvgpu.last_kernel()},
+                        "kernels": lvgpu.last_kernel(),
+                        "traffic": None if not traffic else traffic.get("fetch_bytes_per_call"),
+                        "traffic_detail": traffic},
            "api": "lv_wal_scan_device", "parity": parity, "cpu_baseline": cpu,
            "timing": "HIP events around each call (all of its kernels), mean after settle + warmup",
            "data": "synthetic: Random(301).skewed(17) record sizes, random payload, encoded by lv_wal_encode_host"}

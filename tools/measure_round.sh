@@ -48,7 +48,7 @@ p c4 --workload c4 --api offsets &&
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/$out/prof_wal" -o wal -- \
    python3 "$root/bench.py" --wal-device --steps 50 --warmup 20 --cpu-seconds 0) > "$out/prof_wal.log" 2>&1 &&
 python3 tools/kstats_steady.py "$(ls "$out/prof_wal"/*kernel_trace.csv | head -n 1)" 50 "$out/prof_wal_steady.json" > /dev/null &&
-bash tools/prof_8f.sh "$out/prof8f" table hash &&
+bash tools/prof_8f.sh "$out/prof8f" table hash wal &&
 bash tools/prof_long.sh "$out/prof_long" &&
 LVGPU_BENCH_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-seconds 2 > "$out/gloo2.json" 2> "$out/gloo2.err" &&
 for d in "$out"/prof_*/; do find "$d" -name '*kernel_trace.csv' -size +1M -delete; done; }
