@@ -242,7 +242,7 @@ def measure_traffic(args, shard_rank=0, shard_world=1):
     return t, "rocprofv3 --pmc FETCH_SIZE (x2 gfx950 correction), per step: sum over the call's kernels of each kernel's mean"
 
 
-def pmc_per_kernel(bench_args, counter):
+def pmc_per_kernel(bench_args, counter, keep=None, last=None):
     """Child process: one rocprofv3 --pmc pass of `counter` (FETCH_SIZE or
     WRITE_SIZE, kernel counters only, its own run) over bench.py with
     `bench_args`; returns {kernel: mean bytes per launch} for the lvk::
@@ -269,17 +269,19 @@ def pmc_per_kernel(bench_args, counter):
         return None, f"rocprofv3 pass failed: {e}"
     per = {}
     for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
-        per.update(read_pmc_per_kernel(f, counter))
+        per.update(read_pmc_per_kernel(f, counter, keep, last))
     shutil.rmtree(out, ignore_errors=True)
     if not per:
         return None, "no lvk:: kernel in the pass"
     return per, f"rocprofv3 --pmc {counter}, mean per launch"
 
 
-def read_pmc_per_kernel(path, counter):
+def read_pmc_per_kernel(path, counter, keep=None, last=None):
     """{kernel: mean bytes per launch} of `counter` over the lvk:: kernels of a
     rocprofv3 counter CSV (fill kernels excluded; FETCH_SIZE KiB doubled for
-    gfx950's half-counted wide reads, WRITE_SIZE KiB as read)."""
+    gfx950's half-counted wide reads, WRITE_SIZE KiB as read).  `keep`: only
+    these kernel names; `last`: only each name's last `last` launches (by
+    dispatch id), so set-up calls before the timed ones do not count."""
     import collections
     import csv
     scale = 2.0 * 1024.0 if counter == "FETCH_SIZE" else 1024.0
@@ -288,8 +290,14 @@ def read_pmc_per_kernel(path, counter):
         for row in csv.DictReader(fh):
             name = row.get("Kernel_Name", "")
             if "lvk::" in name and "fill_" not in name and row.get("Counter_Name") == counter:
-                per[name.split("(")[0].replace("void ", "")].append(float(row["Counter_Value"]) * scale)
-    return {k: sum(v) / len(v) for k, v in per.items()}
+                k = name.split("(")[0].replace("void ", "")
+                if keep is None or k in keep:
+                    per[k].append((int(row.get("Dispatch_Id") or 0), float(row["Counter_Value"]) * scale))
+    out = {}
+    for k, v in per.items():
+        v = [x for _, x in sorted(v)][-last:] if last else [x for _, x in v]
+        out[k] = sum(v) / len(v)
+    return out
 
 
 def _cpu_model():
@@ -777,8 +785,12 @@ def wal_device_bench(args):
     if args.traffic == "auto":
         child = ["--wal-device", "--steps", "10", "--warmup", "5", "--cpu-seconds", "0", "--traffic", "off",
                  "--no-settle"] + (["--blocks", str(args.blocks)] if args.blocks else [])
-        fetch, fsrc = pmc_per_kernel(child, "FETCH_SIZE")
-        write, wsrc = pmc_per_kernel(child, "WRITE_SIZE")
+        # the scan's five kernels, the timed launches only (the log's encode
+        # ran the seeded batch path on the same device first)
+        keep = {"lvk::wal_hist", "lvk::sort_scan", "lvk::wal_scatter", "lvk::crc32c_classes_kernel<false>",
+                "lvk::wal_unsort"}
+        fetch, fsrc = pmc_per_kernel(child, "FETCH_SIZE", keep, 10)
+        write, wsrc = pmc_per_kernel(child, "WRITE_SIZE", keep, 10)
         if isinstance(fetch, dict):
             traffic = {"fetch_bytes_per_call": round(sum(fetch.values())),
                        "fetch_over_log_bytes": round(sum(fetch.values()) / log.size, 4),

@@ -51,14 +51,16 @@ def test_read_pmc_per_kernel(tmp_path):
     """The --wal-device traffic pass: per-kernel means of one counter, fill
     kernels and other counters ignored, FETCH_SIZE doubled (gfx950)."""
     b = _bench()
-    rows = ["Kernel_Name,Counter_Name,Counter_Value",
-            '"void lvk::wal_hist(unsigned char const*, unsigned long)",FETCH_SIZE,100',
-            '"void lvk::wal_hist(unsigned char const*, unsigned long)",FETCH_SIZE,300',
-            '"void lvk::wal_scatter(unsigned char const*)",FETCH_SIZE,50',
-            '"void lvk::fill_bytes(unsigned char*)",FETCH_SIZE,999',
-            '"void lvk::wal_scatter(unsigned char const*)",WRITE_SIZE,7']
+    rows = ["Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value",
+            '1,"void lvk::wal_hist(unsigned char const*, unsigned long)",FETCH_SIZE,100',
+            '5,"void lvk::wal_hist(unsigned char const*, unsigned long)",FETCH_SIZE,300',
+            '2,"void lvk::wal_scatter(unsigned char const*)",FETCH_SIZE,50',
+            '3,"void lvk::fill_bytes(unsigned char*)",FETCH_SIZE,999',
+            '4,"void lvk::wal_scatter(unsigned char const*)",WRITE_SIZE,7']
     p = tmp_path / "c.csv"
     p.write_text("\n".join(rows) + "\n")
     assert b.read_pmc_per_kernel(str(p), "FETCH_SIZE") == {"lvk::wal_hist": 2.0 * 1024 * 200,
                                                            "lvk::wal_scatter": 2.0 * 1024 * 50}
     assert b.read_pmc_per_kernel(str(p), "WRITE_SIZE") == {"lvk::wal_scatter": 7.0 * 1024}
+    # keep / last: the named kernels' last launches only
+    assert b.read_pmc_per_kernel(str(p), "FETCH_SIZE", {"lvk::wal_hist"}, 1) == {"lvk::wal_hist": 2.0 * 1024 * 300}
