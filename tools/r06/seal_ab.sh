@@ -2,6 +2,7 @@
 # Round 6 (2nd): the seal's wait-count mode under the file-order runs
 # (LVK_SEAL_EXACT=2: every load unconditional, as verify runs) against the
 # product (masked loads), interleaved, plus the table GPU tests on the variant.
+# (The knob lived in commit c6b7f0d only; check that commit out to rerun.)
 set -o pipefail
 out=${1:-gpurun_out/r06seal}
 mkdir -p "$out"
