@@ -92,6 +92,10 @@ def parse():
     p.add_argument("--long", action="store_true",
                    help="few long buffers through both device APIs (1,024 x 64 KiB, 64 x 16 MiB, 16 x 1 MiB, "
                         "1 x 16 MiB); one JSON line")
+    p.add_argument("--variants", action="store_true",
+                   help="SURVEY 8d's config variants through the offsets API: C2 with the writer's seeds "
+                        "type_crc[t] over payload only (masked), C2 heavy (uniform 0-32761 B payloads, 16 GiB), "
+                        "C4 misaligned (L - r, r in [0, 31]); one JSON line")
     p.add_argument("--wal-device", action="store_true",
                    help="SURVEY 8f row 1 in HBM: lv_wal_scan_device (framing + CRC) of a ~1 GiB log already on "
                         "the GPU; one JSON line with a roofline")
@@ -180,6 +184,125 @@ def wal_unit_lengths(n):
             if left <= 0:
                 break
     return out
+
+
+def wal_units_typed(n):
+    """(fragment length, record type) of the first n physical records the
+    reference writer emits for Random(301).skewed(17) records
+    (log_writer.rs:62-110: FULL 1, FIRST 2, MIDDLE 3, LAST 4), i.e. the
+    writer's CRC calls extend(type_crc[t], fragment) (log_writer.rs:123)."""
+    import numpy as np
+    units = wal_unit_lengths(n).astype(np.int64) - 1  # fragment bytes
+    # a record's fragments are consecutive; the type follows from whether a
+    # fragment is its record's first / last, which the generator replays
+    B, H = 32768, 7
+    types = np.empty(n, dtype=np.uint32)
+    m, state, block_off = 0, 301 & 0x7FFFFFFF, 0
+
+    def nxt():
+        nonlocal state
+        prod = state * 16807
+        v = ((prod >> 31) + (prod & 2147483647)) & 0xFFFFFFFF
+        if v > 2147483647:
+            v -= 2147483647
+        state = v
+        return v
+    while m < n:
+        r = 1 << (nxt() % 18)
+        left, begin = nxt() % r, True
+        while m < n:
+            if B - block_off < H:
+                block_off = 0
+            frag = min(left, B - block_off - H)
+            end = frag == left
+            types[m] = 1 if begin and end else 2 if begin else 4 if end else 3
+            assert frag == units[m]
+            m += 1
+            block_off += H + frag
+            left -= frag
+            begin = False
+            if end:
+                break
+    return units.astype(np.uint32), types
+
+
+def variants_bench(args):
+    """SURVEY 8d's config variants, each through lv_crc32c_batch_device (sort
+    + class kernel) in HBM: (a) C2 as the WAL writer calls it --
+    mask(extend(type_crc[t], fragment)) over the payload alone, seeds in a
+    device array, LV_CRC_MASK (log_writer.rs:112-125); (b) C2 heavy: 1,048,576
+    units of 1 + U[0, 32761] bytes (16 GiB); (c) C4 misaligned: the C4 lengths
+    L - r, r uniform in [0, 31], byte-packed.  HIP-event mean per call after
+    settle + warmup; the first and last 1,000 buffers of each checked against
+    the oracle (seeds and mask included)."""
+    import numpy as np
+    import torch
+    import lvgpu
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    lvgpu.device_init()
+    L = W.lib()
+    type_crc = np.array([lvgpu.value(bytes([t])) for t in range(5)], dtype=np.uint32)  # log_writer.rs:136-142
+    rng = np.random.default_rng(0x5EED)
+    cases = []
+    u, t = wal_units_typed(1048576)
+    cases.append(("c2_writer_seeded_masked", u, type_crc[t], True,
+                  "C2 fragments (payload only) with seed type_crc[t] and LV_CRC_MASK: the writer's call"))
+    cases.append(("c2_heavy", (1 + rng.integers(0, 32762, 1048576)).astype(np.uint32), None, False,
+                  "1,048,576 units of 1 + U[0, 32761] B (mean 16,382 B), byte-packed"))
+    kk = np.arange(1, 2049, dtype=np.float64)
+    cdf = np.cumsum(kk ** -1.1)
+    cdf /= cdf[-1]
+    k = np.minimum(np.searchsorted(cdf, np.random.default_rng(0xC0FFEE).random(1048576), side="right") + 1, 2048)
+    c4 = (32 * k - rng.integers(0, 32, k.size)).astype(np.uint32)
+    cases.append(("c4_misaligned", c4, None, False, "C4 lengths L - r, r ~ U[0, 31], byte-packed"))
+    steps, warm = max(20, min(args.steps, 100)), max(10, min(args.warmup, 50))
+    rows = []
+    for name, lens, seeds, masked, desc in cases:
+        n = lens.size
+        offs = np.zeros(n, dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        total = int(offs[-1] + lens[-1])
+        arena = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        lvgpu.fill_splitmix(arena, 0, PAYLOAD_SEED)
+        o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+        ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+        sd = None if seeds is None else torch.from_numpy(seeds.view(np.int32)).to(dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        ws = torch.empty(lvgpu.workspace_bytes(n), dtype=torch.uint8, device=dev)
+        fn = lambda: lvgpu.batch_ws(arena, o, ln, ws, seed=sd, out=out, masked=masked)  # noqa: E731
+        p50, avg = _event_times(torch, fn, steps, warm)
+        out.fill_(0)
+        fn()
+        kern = lvgpu.last_kernel()
+        got = out.cpu().numpy().view(np.uint32)
+        for lo, hi in ((0, 1000), (n - 1000, n)):
+            a0, a1 = int(offs[lo]), int(offs[hi - 1] + lens[hi - 1])
+            host = arena[a0:a1].cpu().numpy()
+            ho = (offs[lo:hi] - a0).astype(np.uint64)
+            hl = np.ascontiguousarray(lens[lo:hi])
+            hs = None if seeds is None else np.ascontiguousarray(seeds[lo:hi])
+            want = np.zeros(hi - lo, dtype=np.uint32)
+            L.oracle_batch(host.ctypes.data, ho.ctypes.data, hl.ctypes.data,
+                           None if hs is None else hs.ctypes.data, want.ctypes.data, hi - lo, 1 if masked else 0)
+            if not np.array_equal(got[lo:hi], want):
+                raise SystemExit(f"variants parity check failed ({name}, buffers {lo}..{hi})")
+        gbs = total / (avg * 1e-3) / 1e9
+        rows.append({"variant": name, "config": desc, "buffers": n, "payload_bytes": total,
+                     "GB_per_s": round(gbs, 1), "GiB_per_s": round(total / (avg * 1e-3) / 2**30, 2),
+                     "frac_of_8TBps": round(gbs / HBM_PEAK_GBS, 4), "ms_avg": round(avg, 4),
+                     "ms_p50": round(p50, 4), "kernels": kern,
+                     "parity": "first and last 1,000 buffers == oracle_batch (seeds, mask)"})
+        print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+        del arena, o, ln, sd, out, ws
+        torch.cuda.empty_cache()
+    res = {"metric": "SURVEY 8d config variants, device-resident batched CRC32C (offsets API)", "unit": "GB/s",
+           "results": rows, "timing": "HIP events around each call (every kernel of the call), mean after "
+           "settle + warmup", "data": "synthetic splitmix64 payload in HBM"}
+    print(json.dumps(res), flush=True)
+    return res
 
 
 def read_pmc_traffic(path):
@@ -1424,6 +1547,8 @@ def main():
         return long_bench(args)
     if args.wal_device:
         return wal_device_bench(args)
+    if args.variants:
+        return variants_bench(args)
     world, rank, local = shard.world_from_env(args.gpus)
     # --as-rank/--as-world: a single process rebuilds rank R's shard of a
     # W-rank job (the PMC child pass of measure_traffic runs this way).

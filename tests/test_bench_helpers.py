@@ -64,3 +64,29 @@ def test_read_pmc_per_kernel(tmp_path):
     assert b.read_pmc_per_kernel(str(p), "WRITE_SIZE") == {"lvk::wal_scatter": 7.0 * 1024}
     # keep / last: the named kernels' last launches only
     assert b.read_pmc_per_kernel(str(p), "FETCH_SIZE", {"lvk::wal_hist"}, 1) == {"lvk::wal_hist": 2.0 * 1024 * 300}
+
+
+def test_wal_units_typed_match_the_oracle_writer():
+    """bench.py --variants' C2 writer case: fragment lengths and record types
+    of the first physical records equal what the oracle Writer
+    (log_writer.rs:62-110) lays out for the same Random(301).skewed(17)
+    records, and the header CRC is mask(extend(type_crc[t], fragment))."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wal_oracle as W
+    b = _bench()
+    m = 1500
+    u, t = b.wal_units_typed(m)
+    r, log = W.Random(301), bytearray()
+    w = W.Writer(log)
+    while True:
+        w.add_record(bytes(r.skewed(17)))
+        if len(log) > int(u.sum()) + 7 * m:
+            break
+    phys = W.wal_physical_records(bytes(log))[:m]
+    assert np.array_equal(np.array([p[1] for p in phys]), u)
+    assert np.array_equal(np.array([p[2] for p in phys]), t)
+    tc = [W.value(bytes([k])) for k in range(5)]
+    for o, ln, ty in phys[:200]:
+        assert W.decode_fixed_32(bytes(log[o:o + 4])) == W.mask(W.extend(tc[ty], bytes(log[o + 7:o + 7 + ln])))
