@@ -40,6 +40,7 @@ timeout -k 10 300 python3 bench.py --table > "$out/table.json" 2> "$out/table.er
 timeout -k 10 300 python3 bench.py --hash > "$out/hash.json" 2> "$out/hash.err" &&
 timeout -k 10 300 python3 bench.py --sweep > "$out/sweep.json" 2> "$out/sweep.err" &&
 timeout -k 10 300 python3 bench.py --wal-device > "$out/wal_device.json" 2> "$out/wal_device.err" &&
+timeout -k 10 300 python3 bench.py --variants > "$out/variants.json" 2> "$out/variants.err" &&
 timeout -k 10 300 python3 bench.py --long > "$out/long.json" 2> "$out/long.err"; }
 prof_part() {
 p c3 &&

@@ -108,6 +108,11 @@ def main():
                   if "offsets_hint" in r else "")
             rows.append(f"| {r['blocks']} x {r['block_bytes']} B | strided {r['strided']['us_avg']} us{med('strided')}, "
                         f"offsets {r['offsets']['us_avg']} us{med('offsets')}{hn} | - | {r['offsets']['kernels']} |")
+    va = load(os.path.join(out, "variants.json"))
+    if va:
+        for r in va["results"]:
+            rows.append(f"| variant {r['variant']} | {r['ms_avg'] * 1e3:.1f} us, frac {r['frac_of_8TBps']} | - | "
+                        f"{r['GiB_per_s']} GiB/s; {r['kernels']} |")
     g = load(os.path.join(out, "gloo2.json"))
     if g:
         c5 = g.get("c5_strong") or {}
