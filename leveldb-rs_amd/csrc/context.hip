@@ -6,15 +6,8 @@
 // synthetic payload generator.
 #include <hip/hip_runtime.h>
 
-#include <pthread.h>
-#include <sched.h>
-
 #include <algorithm>
-#include <cctype>
-#include <cstdlib>
 #include <cstring>
-#include <fstream>
-#include <string>
 #include <thread>
 
 #include "../../include/lvgpu/crc32c.h"
@@ -137,71 +130,7 @@ bool is_pinned(const void *p) {
     return a.type == hipMemoryTypeHost;
 }
 
-// The CPUs local to each device that the process may use (cached on first
-// use): /sys/bus/pci/devices/<bus id>/local_cpulist within sched_getaffinity.
-namespace {
-struct LocalCpus {
-    bool known = false, ok = false;
-    cpu_set_t set;
-};
-LocalCpus g_local_cpus[64];
-std::mutex g_local_cpus_m;
-
-bool parse_cpulist(const std::string &s, cpu_set_t *out) {  // "0-63,128-191"
-    CPU_ZERO(out);
-    size_t i = 0;
-    while (i < s.size()) {
-        char *end = nullptr;
-        const long a = std::strtol(s.c_str() + i, &end, 10);
-        if (end == s.c_str() + i || a < 0) return false;
-        i = end - s.c_str();
-        long b = a;
-        if (i < s.size() && s[i] == '-') {
-            b = std::strtol(s.c_str() + i + 1, &end, 10);
-            if (end == s.c_str() + i + 1 || b < a) return false;
-            i = end - s.c_str();
-        }
-        for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(static_cast<int>(c), out);
-        while (i < s.size() && (s[i] == ',' || std::isspace(static_cast<unsigned char>(s[i])))) ++i;
-    }
-    return CPU_COUNT(out) > 0;
-}
-
-bool device_local_cpus(int device, cpu_set_t *out) {
-    if (device < 0 || device >= 64) return false;
-    std::lock_guard<std::mutex> lk(g_local_cpus_m);
-    LocalCpus &lc = g_local_cpus[device];
-    if (!lc.known) {
-        lc.known = true;
-        const char *env = std::getenv("LVGPU_THREAD_AFFINITY");
-        char bdf[64] = {0};
-        cpu_set_t local, allowed;
-        if (!(env && env[0] == '0') && hipDeviceGetPCIBusId(bdf, sizeof bdf, device) == hipSuccess) {
-            std::string id(bdf);
-            for (auto &ch : id) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-            std::ifstream f("/sys/bus/pci/devices/" + id + "/local_cpulist");
-            std::string line;
-            if (std::getline(f, line) && parse_cpulist(line, &local) &&
-                sched_getaffinity(0, sizeof allowed, &allowed) == 0) {
-                CPU_AND(&lc.set, &local, &allowed);
-                lc.ok = CPU_COUNT(&lc.set) > 0;
-            }
-        } else {
-            (void)hipGetLastError();
-        }
-    }
-    if (lc.ok) *out = lc.set;
-    return lc.ok;
-}
-}  // namespace
-
-void bind_thread_to_device(int device) {
-    cpu_set_t s;
-    if (device_local_cpus(device, &s)) (void)pthread_setaffinity_np(pthread_self(), sizeof s, &s);
-}
-
-// memcpy split over up to 8 host threads (pageable -> pinned staging), each
-// on the current device's socket (bind_thread_to_device).
+// memcpy split over up to 8 host threads (pageable -> pinned staging).
 void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, unsigned threads) {
     unsigned nt = std::thread::hardware_concurrency();
     nt = nt == 0 ? 1 : (nt > threads ? threads : nt);
@@ -209,18 +138,13 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, unsigned threads
         std::memcpy(dst, src, bytes);
         return;
     }
-    int dev = -1;
-    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
     std::vector<std::thread> th;
     const size_t per = (bytes + nt - 1) / nt;
     for (unsigned t = 0; t < nt; ++t) {
         const size_t lo = t * per;
         if (lo >= bytes) break;
         const size_t len = bytes - lo < per ? bytes - lo : per;
-        th.emplace_back([=] {
-            bind_thread_to_device(dev);
-            std::memcpy(dst + lo, src + lo, len);
-        });
+        th.emplace_back([=] { std::memcpy(dst + lo, src + lo, len); });
     }
     for (auto &x : th) x.join();
 }

@@ -139,7 +139,6 @@ int lv_crc32c_batch_multi_devices(const uint8_t *h_arena, size_t arena_bytes, co
     for (int r = 0; r < ndev; ++r) {
         if (b[r] == b[r + 1]) continue;
         th.emplace_back([&, r] {
-            lvh::bind_thread_to_device(devices[r]);  // each device's packing and staging on its socket
             const size_t lo = b[r], cnt = b[r + 1] - b[r];
             uint64_t first = UINT64_MAX, last = 0, payload = 0;
             for (size_t i = lo; i < lo + cnt; ++i) {

@@ -10,15 +10,6 @@
 #include <thread>
 #include <vector>
 
-namespace lvh {
-// Binds the calling host thread to the CPUs local to `device` (its PCI
-// function's local_cpulist, within the process's allowed CPUs), as the
-// library's own worker and copy threads do: a copy or a scan worker on the
-// GPU's socket moves host memory without crossing the socket link.  No-op if
-// the topology is unknown or LVGPU_THREAD_AFFINITY=0.  (context.hip)
-void bind_thread_to_device(int device);
-}  // namespace lvh
-
 namespace lvgpu_internal {
 // One block-aligned chunk of a pipelined scan (offsets are log offsets).
 struct ScanChunk {

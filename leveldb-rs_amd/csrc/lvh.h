@@ -117,7 +117,6 @@ int grow_pinned(uint8_t **p, size_t *cap, size_t need);
 bool is_pinned(const void *p);
 // memcpy split over up to 8 host threads (pageable -> pinned staging).
 void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes, unsigned threads = LVK_MEMCPY_THREADS);
-
 // The calling thread's current device's context, initialised on first use.
 int current_ctx(DevCtx **out);
 // Buffers-per-group choice for a known (uniform) length.

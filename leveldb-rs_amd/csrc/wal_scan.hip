@@ -726,7 +726,6 @@ extern "C" lv_wal_scan *lv_wal_scan_host_pipelined(const uint8_t *log, size_t by
         return scan;
     }
     p->worker = std::thread([p, log, bytes, device] {
-        lvh::bind_thread_to_device(device);  // the worker and its copy threads on the GPU's socket
         const int rc = pipe_run(p, log, bytes, device);
         if (rc) {
             std::lock_guard<std::mutex> lk(p->m);
