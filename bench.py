@@ -92,6 +92,10 @@ def parse():
     p.add_argument("--long", action="store_true",
                    help="few long buffers through both device APIs (1,024 x 64 KiB, 64 x 16 MiB, 16 x 1 MiB, "
                         "1 x 16 MiB); one JSON line")
+    p.add_argument("--host-placement", default="gpu-local", choices=["gpu-local", "float"],
+                   help="--wal: confine the process to the CPUs local to the GPU (its PCI function's "
+                        "local_cpulist, as numactl --cpunodebind would) before the log is allocated, or leave it "
+                        "where the OS puts it")
     p.add_argument("--variants", action="store_true",
                    help="SURVEY 8d's config variants through the offsets API: C2 with the writer's seeds "
                         "type_crc[t] over payload only (masked), C2 heavy (uniform 0-32761 B payloads, 16 GiB), "
@@ -1266,13 +1270,46 @@ def hash_bench(args):
     return res
 
 
+def confine_to_gpu_socket(device=0):
+    """The calling process's CPUs -> the allowed CPUs local to `device` (its
+    PCI function's local_cpulist), before it allocates host memory, so the log
+    pages, the Reader and the library's copy threads share the GPU's socket:
+    the placement a deployment gives a recovery process (numactl
+    --cpunodebind).  Returns what was done.  (Round 6, profiles/r06/numa/:
+    binding only the library's own threads, with the caller floating, made
+    the host paths slower -- the caller's memory decides -- so the placement
+    is the caller's, here the bench's.)"""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return {"placement": "float", "reason": "no PCI bus id"}
+        bdf = buf.value.decode().lower()
+        text = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
+    except Exception as e:  # noqa: BLE001 - report, never fail the bench on topology
+        return {"placement": "float", "reason": f"topology unavailable: {e}"}
+    local = set()
+    for part in text.split(","):
+        a, _, b = part.partition("-")
+        local.update(range(int(a), int(b or a) + 1))
+    allowed = os.sched_getaffinity(0)
+    cpus = local & allowed
+    if not cpus:
+        return {"placement": "float", "reason": "no allowed CPU local to the GPU"}
+    os.sched_setaffinity(0, cpus)
+    return {"placement": "gpu-local", "gpu_pci": bdf, "cpus": len(cpus), "of_allowed": len(allowed)}
+
+
 def wal_bench(args):
     """SURVEY 8f rows 1-2 end to end from host memory: group-commit encode
     (lv_wal_encode_host: layout + one GPU CRC batch) and whole-log verify
     (lv_wal_scan_host: H2D, block framing, one CRC batch, D2H), then the host
     Reader over the scan.  Records: logical sizes Random(301).skewed(17)
     (log_writer.rs:456-458, 567), random payload, until ~1 GiB.  The first
-    2000 physical records' CRCs are checked against the oracle."""
+    2000 physical records' CRCs are checked against the oracle.  The process
+    is first confined to the GPU's socket (--host-placement, default
+    gpu-local; confine_to_gpu_socket)."""
+    placement = confine_to_gpu_socket() if args.host_placement == "gpu-local" else {"placement": "float"}
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import lvgpu
@@ -1379,7 +1416,7 @@ def wal_bench(args):
     gib = out.size / 2**30
     print(json.dumps({"metric": "WAL group-commit encode and whole-log verify, host memory end to end",
                       "unit": "GiB/s of log", "log_bytes": int(out.size), "records": int(sizes.size),
-                      "physical_records": int(o.size),
+                      "physical_records": int(o.size), "host_placement": placement,
                       "encode": {"GiB_per_s": round(gib / t_enc, 2), "ms": round(t_enc * 1e3, 2),
                                  "api": "lv_wal_encode_host"},
                       "scan": {"GiB_per_s": round(gib / t_scan, 2), "ms": round(t_scan * 1e3, 2),
