@@ -173,17 +173,10 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
     const Lut L = make_lut(lane);
     const uint64_t grid = gridDim.x;
     // a wave claims kSstRun rounds at a time (its groups' runs of blocks)
-#if LVK_SST_XCD
-    // (variant) workgroups of one XCD (b % 8 on the 8-XCD part) take adjacent
-    // claims, so the row two neighbouring claims share is read into one L2
-    const uint64_t wg = grid % 8u == 0 ? (blockIdx.x % 8u) * (grid / 8u) + blockIdx.x / 8u : blockIdx.x;
-#else
-    const uint64_t wg = blockIdx.x;
-#endif
     auto claim = [&]() -> uint64_t {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&g_lds[kPoolWord], 1u);
-        return (wg + grid * static_cast<uint64_t>(__shfl(k, 0))) * kSstRun;
+        return (blockIdx.x + grid * static_cast<uint64_t>(__shfl(k, 0))) * kSstRun;
     };
     uint64_t r0 = claim();
     uint32_t i = 0;
