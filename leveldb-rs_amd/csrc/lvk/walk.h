@@ -392,7 +392,6 @@ struct SortedList {
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
     static constexpr uint32_t kExact = 0;  // sorted_stream: wait-count mode (below)
-    static constexpr uint32_t kHalves = 1;  // results stored by flush() (2: published to a writer wave)
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         if (!ident) return load_rgeo<SEEDED>(P, e);
@@ -570,21 +569,13 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         else
             X = merge_group<G, W1K, W2K>(A, L);
         X = finish_raw(q, X, tail, gl, L);
-        // slots: rounds per flush x groups per wave <= 64; a source with
-        // kHalves == 2 stages into two alternating halves and publishes each
-        // to another wave (the seal's trailer writer) instead of storing it
+        // slots: rounds per flush x groups per wave <= 64
         constexpr uint32_t kF = Src::kFlush * K <= 64 ? Src::kFlush : 64 / K;
-        constexpr uint32_t kH = Src::kHalves;
-        static_assert(kH == 1 || (kH == 2 && 2 * kF * K <= 64), "one or two halves of staging slots");
-        const uint32_t half = kH == 2 ? static_cast<uint32_t>(c / kF) & 1u : 0u;
-        const uint32_t slot = half * kF * K + (c % kF) * K + grp;
+        const uint32_t slot = (c % kF) * K + grp;
         if (gl == 0) src.stage(P, wave, slot, q, X, tr);
         if ((c + 1) % kF == 0 || !more) {
             __builtin_amdgcn_wave_barrier();
-            if constexpr (kH == 2)
-                src.publish(wave, lane, (c % kF + 1) * K, half);
-            else
-                src.flush(P, wave, lane, (c % kF + 1) * K);
+            src.flush(P, wave, lane, (c % kF + 1) * K);
             __builtin_amdgcn_wave_barrier();
         }
         if (!more) return true;

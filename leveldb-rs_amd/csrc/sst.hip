@@ -48,23 +48,6 @@ __device__ __forceinline__ uint64_t sst_unit(uint64_t e) {  // e = rho * 4 + gro
     return (rho / kSstRun) * (4u * kSstRun) + g * kSstRun + rho % kSstRun;
 }
 
-// (variant LVK_SEAL_WRITER) The seal's trailer writer: waves 0..14 walk and
-// publish their staged {block, masked crc} slots in halves of kSealHalf; wave
-// 15 writes the trailers, so no trailer store sits in a walker's in-order
-// vmcnt queue and the stores spread over the launch instead of bunching at
-// each wave's end.  Counters in combine table 5 (Shift_512, unused by the
-// G = 16 walk), after the pool word.
-constexpr bool kSealWriter = LVK_SEAL_WRITER != 0;
-constexpr uint32_t kSealWalkers = kWaves - 1;
-constexpr uint32_t kSealRoundsPerHalf = 4;
-constexpr uint32_t kSealHalf = kSealRoundsPerHalf * 4;  // slots per half: rounds x groups
-constexpr uint32_t kSealPub = kPoolWord + 1;            // [16] halves published per walker
-constexpr uint32_t kSealCon = kSealPub + 16;            // [16] halves consumed by the writer
-constexpr uint32_t kSealDone = kSealCon + 16;           // [16] walker finished
-constexpr uint32_t kSealCnt = kSealDone + 16;           // [16][2] slots in each published half
-constexpr uint32_t kSealWords = kSealCnt + 32 - kSealPub;
-static_assert(kSealCnt + 32 <= (kComb + 6 * 4096) / 4, "seal counters inside combine table 5");
-
 template <bool SEAL, bool CRCOUT = false>
 struct TableUnits {
     const uint2 *handles;  // {offset, size} u64 pairs per block
@@ -77,8 +60,7 @@ struct TableUnits {
     // the trailer stores are partial-line writes, and fewer, larger bursts of
     // them measured faster); verify: 64 slots of {block, status}, or with
     // crc_out 32 slots of four words
-    static constexpr uint32_t kFlush = SEAL ? (kSealWriter ? kSealRoundsPerHalf : LVK_SEAL_FLUSH) : !CRCOUT ? 16 : 8;
-    static constexpr uint32_t kHalves = SEAL && kSealWriter ? 2 : 1;
+    static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
     static constexpr bool kOneRound = false;
     // Wait-count mode (walk.h sorted_stream): verify runs mode 2 (every load
@@ -148,32 +130,6 @@ struct TableUnits {
             if (CRCOUT) g_ocrc[wave][32 + slot] = ok ? crc : 0u;
         }
     }
-    // (writer variant) a walker hands half `half` (nslots slots) to the
-    // writer, then waits until the writer has taken the other half, which it
-    // stages into next (published one flush ago: normally long taken)
-    __device__ __forceinline__ void publish(uint32_t wave, uint32_t lane, uint32_t nslots, uint32_t half) const {
-        if (lane == 0) {
-            g_lds[kSealCnt + 2 * wave + half] = nslots;
-            const uint32_t p = g_lds[kSealPub + wave] + 1u;  // only this wave writes it
-            __hip_atomic_store(&g_lds[kSealPub + wave], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t pub = __hip_atomic_load(&g_lds[kSealPub + wave], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (__hip_atomic_load(&g_lds[kSealCon + wave], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + 1u < pub)
-            __builtin_amdgcn_s_sleep(2);
-    }
-    // the trailer of block bi: type byte, then LE32(mask(crc))
-    __device__ __forceinline__ void write_trailer(const Params &P, uint32_t bi, uint32_t m) const {
-        const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
-        const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
-        uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);
-        const uint32_t f = types ? types[bi] : 0u;
-        p[0] = static_cast<uint8_t>(f);
-        p[1] = static_cast<uint8_t>(m);
-        p[2] = static_cast<uint8_t>(m >> 8);
-        p[3] = static_cast<uint8_t>(m >> 16);
-        p[4] = static_cast<uint8_t>(m >> 24);
-    }
     __device__ __forceinline__ void flush(const Params &P, uint32_t wave, uint32_t lane, uint32_t nslots) const {
         if constexpr (SEAL) {
             if (lane >= nslots) return;
@@ -207,71 +163,13 @@ struct TableUnits {
 };
 
 
-// (writer variant) The last wave of the workgroup: takes published halves,
-// up to four walkers' at a time (16 lanes each), and writes their trailers;
-// leaves once every walker is done and taken.
-__device__ __forceinline__ void seal_writer(const Params &P, const TableUnits<true> &src, uint32_t lane) {
-    uint32_t mycon = 0;  // lane w < kSealWalkers: halves of walker w taken
-    for (;;) {
-        const bool lw = lane < kSealWalkers;
-        // done first, then pub: a walker publishes its last half before it sets done
-        const uint32_t dn = lw ? __hip_atomic_load(&g_lds[kSealDone + lane], __ATOMIC_ACQUIRE,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP) : 1u;
-        const uint32_t pb = lw ? __hip_atomic_load(&g_lds[kSealPub + lane], __ATOMIC_ACQUIRE,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
-        uint64_t rb = __ballot(lw && pb > mycon);
-        if (!rb) {
-            if (__all(dn != 0u && pb == mycon)) break;
-            __builtin_amdgcn_s_sleep(4);
-            continue;
-        }
-        int w0 = -1, w1 = -1, w2 = -1, w3 = -1;  // up to four ready walkers (scalar selects, no array)
-        w0 = __ffsll(static_cast<long long>(rb)) - 1;
-        rb &= rb - 1;
-        if (rb) {
-            w1 = __ffsll(static_cast<long long>(rb)) - 1;
-            rb &= rb - 1;
-        }
-        if (rb) {
-            w2 = __ffsll(static_cast<long long>(rb)) - 1;
-            rb &= rb - 1;
-        }
-        if (rb) w3 = __ffsll(static_cast<long long>(rb)) - 1;
-        const uint32_t j = lane >> 4, s = lane & 15u;
-        const int w = j == 0 ? w0 : j == 1 ? w1 : j == 2 ? w2 : w3;
-        const uint32_t cw = static_cast<uint32_t>(__shfl(static_cast<int>(mycon), w < 0 ? 0 : w));
-        const uint32_t h = cw & 1u;
-        const uint32_t n = w >= 0 ? g_lds[kSealCnt + 2 * static_cast<uint32_t>(w) + h] : 0u;
-        const bool on = w >= 0 && s < n;
-        const uint32_t sl = h * kSealHalf + s;
-        const uint32_t bi = on ? g_oidx[w < 0 ? 0 : w][sl] : 0xffffffffu;
-        const uint32_t mc = on ? g_ocrc[w < 0 ? 0 : w][sl] : 0u;
-        const int me = static_cast<int>(lane);
-        const bool took = lw && (me == w0 || me == w1 || me == w2 || me == w3);
-        if (took) ++mycon;
-        // the slots are in registers: hand the half back
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (took) __hip_atomic_store(&g_lds[kSealCon + lane], mycon, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (bi != 0xffffffffu) src.write_trailer(P, bi, mc);
-    }
-}
-
 template <bool SEAL, bool CRCOUT>
 __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
                                                               TableUnits<SEAL, CRCOUT> src) {
     stage_tables(image);
     if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
-    if constexpr (SEAL && kSealWriter) {
-        for (uint32_t k = threadIdx.x; k < kSealWords; k += kThreads) g_lds[kSealPub + k] = 0;
-    }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    if constexpr (SEAL && kSealWriter) {
-        if ((threadIdx.x >> 6) == kSealWalkers) {  // wave-uniform
-            seal_writer(P, src, lane);
-            return;
-        }
-    }
     const Lut L = make_lut(lane);
     const uint64_t grid = gridDim.x;
     // a wave claims kSstRun rounds at a time (its groups' runs of blocks)
@@ -291,12 +189,6 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
     };
     sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(next), SEAL ? kSealRows : kSstRows>(P, src, lane, L, r0,
                                                                                           next);
-    if constexpr (SEAL && kSealWriter) {
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0)
-            __hip_atomic_store(&g_lds[kSealDone + (threadIdx.x >> 6)], 1u, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
 }
 
 }  // namespace lvk
