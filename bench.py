@@ -158,48 +158,18 @@ def build_workload(torch, lvgpu, name, dev, rank, blocks=None):
 def wal_unit_lengths(n):
     """CRC unit lengths (1 + fragment) of the WAL the reference writer produces for
     records of size Random(301).skewed(17) (log_writer.rs:62-110, random.rs:66-69)."""
-    import numpy as np
-    B, H = 32768, 7
-    out = np.empty(n, dtype=np.uint32)
-    m = 0
-    state = 301 & 0x7FFFFFFF
-    block_off = 0
-
-    def nxt():
-        nonlocal state
-        prod = state * 16807
-        s = ((prod >> 31) + (prod & 2147483647)) & 0xFFFFFFFF
-        if s > 2147483647:
-            s -= 2147483647
-        state = s
-        return s
-    while m < n:
-        r = 1 << (nxt() % 18)
-        left = nxt() % r
-        while m < n:
-            if B - block_off < H:
-                block_off = 0
-            avail = B - block_off - H
-            frag = min(left, avail)
-            out[m] = frag + 1
-            m += 1
-            block_off += H + frag
-            left -= frag
-            if left <= 0:
-                break
-    return out
+    return wal_units_typed(n)[0] + 1
 
 
 def wal_units_typed(n):
     """(fragment length, record type) of the first n physical records the
     reference writer emits for Random(301).skewed(17) records
-    (log_writer.rs:62-110: FULL 1, FIRST 2, MIDDLE 3, LAST 4), i.e. the
-    writer's CRC calls extend(type_crc[t], fragment) (log_writer.rs:123)."""
+    (log_writer.rs:62-110: FULL 1, FIRST 2, MIDDLE 3, LAST 4; trailers of
+    < 7 B skipped), i.e. the writer's CRC calls extend(type_crc[t], fragment)
+    (log_writer.rs:123).  The Park-Miller generator is random.rs:19-70."""
     import numpy as np
-    units = wal_unit_lengths(n).astype(np.int64) - 1  # fragment bytes
-    # a record's fragments are consecutive; the type follows from whether a
-    # fragment is its record's first / last, which the generator replays
     B, H = 32768, 7
+    frags = np.empty(n, dtype=np.uint32)
     types = np.empty(n, dtype=np.uint32)
     m, state, block_off = 0, 301 & 0x7FFFFFFF, 0
 
@@ -219,15 +189,15 @@ def wal_units_typed(n):
                 block_off = 0
             frag = min(left, B - block_off - H)
             end = frag == left
+            frags[m] = frag
             types[m] = 1 if begin and end else 2 if begin else 4 if end else 3
-            assert frag == units[m]
             m += 1
             block_off += H + frag
             left -= frag
             begin = False
             if end:
                 break
-    return units.astype(np.uint32), types
+    return frags, types
 
 
 def variants_bench(args):
