@@ -23,7 +23,6 @@
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
     defined(LVK_SST_RUN) || \
-    defined(LVK_SST_DEPTH) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_HASH_WGS_PER_CU) || \
@@ -61,9 +60,6 @@
 #endif
 #ifndef LVK_SST_RUN  // table walk: consecutive blocks per group (file-order runs; 1 = one block per round)
 #define LVK_SST_RUN 4
-#endif
-#ifndef LVK_SST_DEPTH  // table walk: register slots (2: one batch in flight while one folds; 3: two)
-#define LVK_SST_DEPTH 2
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

@@ -600,108 +600,6 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     }
 }
 
-// Depth-3 form of the G = 16 aligned-row walk (the table walk, Src::kDepth
-// = 3): three register slots, so TWO batches are in flight while one folds.
-// With three-row batches a group keeps 768 B in flight per batch; at one
-// batch ahead a CU's sixteen waves hold 48 KiB, which at ~2 us of loaded
-// latency caps the chip near 6.3 TB/s -- the table walk's bound (losing one
-// of the sixteen waves cost the seal 8 %, profiles/r06/seal_writer/).  Every
-// step issues exactly one batch load, into the slot two folds ahead: the
-// batch after next in the linear order of this round's batches then the next
-// round's.  Rounds count at least two batches here (a one-batch round gets a
-// leading all-padding batch, folded as zeros), so that batch always lies in
-// this round or the next, whose entries are loaded one round ahead.  The
-// entries and batches past the list are clamped loads never folded.
-template <class Src, class Next, uint32_t NU>
-__device__ __forceinline__ void sorted_stream3(const Params &P, const Src &src, uint32_t lane, const Lut &L,
-                                               uint64_t rho, Next next) {
-    constexpr uint32_t G = 16, K = 4;
-    constexpr bool EX = Src::kExact != 0;
-    constexpr uint32_t W4OFF = NU >= 3 ? kRegionA + kHalf : kRegionB + kHalf;
-    const uint32_t gl = lane % G, grp = lane / G;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t nr = (P.n + K - 1) / K;
-    if (rho >= nr) return;
-    auto nbw_of = [&](const RGeo &g) -> uint32_t {
-        const uint32_t nb = round_nbw_al<NU>(al_geo(g));
-        return nb < 2u ? 2u : nb;
-    };
-    uint64_t rhon = next();
-    RGeo q = src.load(P, rho * K + grp);
-    RGeo qn = src.load(P, rhon * K + grp);  // (src.load clamps past the list)
-    uint32_t nbw = nbw_of(q);
-    bool rot = __any(al_geo(q).e != 15);
-    uint32_t jfix = round_jfix_al<NU>(q, nbw);
-    uint32_t pad = round_pad<G, NU>(q, nbw);
-    uint32_t nbwn = 2;  // the next round's batch count, from its entries when its first batch is issued
-    // linear batch t (t < nbw + 2): batch t of q, else batch t - nbw of qn
-    auto issue = [&](uint32_t t, uint4(&dst)[NU]) {
-        const bool in0 = t < nbw;  // wave-uniform
-        RGeo g;
-        g.a = in0 ? q.a : qn.a;
-        g.len = in0 ? q.len : qn.len;
-        g.seed = in0 ? q.seed : qn.seed;
-        g.bid = 0;
-        g.aux = 0;
-        load_rbatch_al<NU>(g, in0 ? nbw : nbwn, in0 ? t : t - nbw, gl, dst);
-    };
-    uint4 tail;
-    uint2 tr;
-    uint4 s0[NU], s1[NU], s2[NU];
-    load_rbatch_al<NU>(q, nbw, 0, gl, s0);
-    load_rbatch_al<NU>(q, nbw, 1, gl, s1);  // nbw >= 2
-    uint32_t A[NU];
-    uint32_t a3p = 0;
-    uint32_t c = 0;
-    uint32_t j = 0;
-    auto step = [&](uint4(&cur)[NU], uint4(&dst)[NU]) -> bool {
-        const bool lastj = j + 1 == nbw;
-        const bool more = rhon < nr;
-        if (j + 2 == nbw) nbwn = nbw_of(qn);  // (qn's entries were requested a round ago)
-        issue(j + 2, dst);
-        if (lastj) {
-            tail = load_rtail<EX>(q, gl);  // consumed after this batch's fold
-            tr = src.trailer(q, gl);
-        }
-        if (j <= jfix) fix_rbatch_al<NU>(q, nbw, j, gl, cur);
-        if (lastj) a3p = j == 0 ? 0u : A[NU - 1];
-        if (j == 0)
-            fold_first<-1, NU, W4OFF>(cur, A, L, pad);
-        else
-            fold_batch<false, -1, NU, W4OFF>(cur, A, L);
-        if (!lastj) {
-            ++j;
-            return false;
-        }
-        uint32_t X = merge_al<NU>(A, a3p, L, q, gl, lane, rot);
-        X = finish_raw(q, X, tail, gl, L);
-        constexpr uint32_t kF = Src::kFlush * K <= 64 ? Src::kFlush : 64 / K;
-        const uint32_t slot = (c % kF) * K + grp;
-        if (gl == 0) src.stage(P, wave, slot, q, X, tr);
-        if ((c + 1) % kF == 0 || !more) {
-            __builtin_amdgcn_wave_barrier();
-            src.flush(P, wave, lane, (c % kF + 1) * K);
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (!more) return true;
-        ++c;
-        q = qn;
-        nbw = nbwn;
-        rot = __any(al_geo(q).e != 15);
-        jfix = round_jfix_al<NU>(q, nbw);
-        pad = round_pad<G, NU>(q, nbw);
-        rhon = next();
-        qn = src.load(P, rhon * K + grp);
-        j = 0;
-        return false;
-    };
-    for (;;) {
-        if (step(s0, s2)) break;
-        if (step(s1, s0)) break;
-        if (step(s2, s1)) break;
-    }
-}
-
 // The sorted sub-list [start, start+count) followed by `pieces` piece
 // entries (the long-buffer split; they sit right after the n sorted entries,
 // i.e. after the last class).

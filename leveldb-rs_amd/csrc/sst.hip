@@ -70,7 +70,6 @@ struct TableUnits {
     // -> 0.640, seal_exact/; mode 1, the tail and trailer re-read every step:
     // seal 0.67 -> 0.61, verify 0.69 -> 0.64; mode2_ab/, exact_ab/)
     static constexpr uint32_t kExact = SEAL ? 0u : 2u;
-    static constexpr uint32_t kDepth = LVK_SST_DEPTH;  // batches in flight + 1 (walk.h sorted_stream3)
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const uint64_t u = sst_unit(e);
@@ -188,12 +187,8 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
         }
         return r0 + i;
     };
-    if constexpr (TableUnits<SEAL, CRCOUT>::kDepth == 3)
-        sorted_stream3<TableUnits<SEAL, CRCOUT>, decltype(next), SEAL ? kSealRows : kSstRows>(P, src, lane, L, r0,
-                                                                                             next);
-    else
-        sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(next), SEAL ? kSealRows : kSstRows>(P, src, lane, L, r0,
-                                                                                              next);
+    sorted_stream<16, TableUnits<SEAL, CRCOUT>, decltype(next), SEAL ? kSealRows : kSstRows>(P, src, lane, L, r0,
+                                                                                          next);
 }
 
 }  // namespace lvk
