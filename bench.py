@@ -1240,6 +1240,17 @@ def hash_bench(args):
     return res
 
 
+def parse_cpulist(text):
+    """The CPUs of a sysfs cpulist ("0-63,128-191") as a set."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
 def confine_to_gpu_socket(device=0):
     """The calling process's CPUs -> the allowed CPUs local to `device` (its
     PCI function's local_cpulist), before it allocates host memory, so the log
@@ -1258,10 +1269,7 @@ def confine_to_gpu_socket(device=0):
         text = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
     except Exception as e:  # noqa: BLE001 - report, never fail the bench on topology
         return {"placement": "float", "reason": f"topology unavailable: {e}"}
-    local = set()
-    for part in text.split(","):
-        a, _, b = part.partition("-")
-        local.update(range(int(a), int(b or a) + 1))
+    local = parse_cpulist(text)
     allowed = os.sched_getaffinity(0)
     cpus = local & allowed
     if not cpus:

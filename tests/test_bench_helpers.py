@@ -90,3 +90,11 @@ def test_wal_units_typed_match_the_oracle_writer():
     tc = [W.value(bytes([k])) for k in range(5)]
     for o, ln, ty in phys[:200]:
         assert W.decode_fixed_32(bytes(log[o:o + 4])) == W.mask(W.extend(tc[ty], bytes(log[o + 7:o + 7 + ln])))
+
+
+def test_parse_cpulist():
+    """bench.py --wal's placement reads the GPU's local_cpulist."""
+    b = _bench()
+    assert b.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert b.parse_cpulist("64-127,192-255") == set(range(64, 128)) | set(range(192, 256))
+    assert b.parse_cpulist("") == set()
