@@ -381,6 +381,12 @@ __device__ __forceinline__ uint32_t finish_raw(const RGeo &q, uint32_t X, const 
     return X;
 }
 
+// s_waitcnt immediate that waits for vmcnt <= n only (gfx9 encoding:
+// vmcnt bits 3:0 and 15:14, expcnt 6:4 and lgkmcnt 11:8 at their maxima).
+constexpr int vmcnt_only(uint32_t n) {
+    return static_cast<int>((n & 15u) | ((n >> 4) << 14) | (7u << 4) | (15u << 8));
+}
+
 // Entry source and result sink of the sorted walk: the offsets API's
 // length-sorted list.  load() reads entry e; trailer() issues any extra
 // per-unit loads with the tail load; stage() parks a unit's result in the
@@ -392,6 +398,8 @@ struct SortedList {
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
     static constexpr uint32_t kExact = 0;  // sorted_stream: wait-count mode (below)
+    static constexpr bool kCurWait = false;  // sorted_stream: explicit wait for the batch it folds
+    static constexpr uint32_t kTrailerLoads = 0;
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         if (!ident) return load_rgeo<SEEDED>(P, e);
@@ -546,6 +554,17 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
                     load_rbatch<G>(qn, nbwn, 0, gl, nxt);
                 }
             }
+        }
+        if constexpr (Src::kCurWait) {
+            // (exact loads only) every memory operation but this step's own
+            // -- the batch after this one, and on the last step the tail and
+            // trailer before it -- is done, so `cur` has landed: an explicit
+            // wait the compiler's counters then trust, where its own merge
+            // over the loop's paths waited for the new batch too
+            // (one immediate for both paths: on the last step it also waits
+            // for the tail, as the verify walk's own counts do)
+            static_assert(Src::kExact != 0, "the explicit wait needs exact load counts");
+            __builtin_amdgcn_s_waitcnt(vmcnt_only(NU));
         }
         if constexpr (AL) {
             if (j <= jfix) fix_rbatch_al<NU>(q, nbw, j, gl, cur);

@@ -69,7 +69,9 @@ struct TableUnits {
     // 2: 0.667 -> 0.639, and with its trailer stores unconditional too 0.667
     // -> 0.640, seal_exact/; mode 1, the tail and trailer re-read every step:
     // seal 0.67 -> 0.61, verify 0.69 -> 0.64; mode2_ab/, exact_ab/)
-    static constexpr uint32_t kExact = SEAL ? 0u : 2u;
+    static constexpr uint32_t kExact = SEAL ? (LVK_SEAL_CURWAIT ? 2u : 0u) : 2u;
+    static constexpr bool kCurWait = SEAL && LVK_SEAL_CURWAIT;  // (variant) walk.h sorted_stream
+    static constexpr uint32_t kTrailerLoads = SEAL ? 0u : 2u;   // loads trailer() issues per lane
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const uint64_t u = sst_unit(e);
