@@ -397,8 +397,8 @@ struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
-    static constexpr uint32_t kExact = 0;  // sorted_stream: wait-count mode (below)
-    static constexpr bool kCurWait = false;  // sorted_stream: explicit wait for the batch it folds
+    static constexpr uint32_t kExact = LVK_CLASS_CURWAIT ? 2 : 0;  // sorted_stream: wait-count mode (below)
+    static constexpr bool kCurWait = LVK_CLASS_CURWAIT;  // sorted_stream: explicit wait for the batch it folds
     static constexpr uint32_t kTrailerLoads = 0;
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {

@@ -63,15 +63,18 @@ struct TableUnits {
     static constexpr uint32_t kFlush = SEAL ? LVK_SEAL_FLUSH : !CRCOUT ? 16 : 8;
     static constexpr bool kAlMid = false;  // measured -0.7 % here (load_rbatch_al)
     static constexpr bool kOneRound = false;
-    // Wait-count mode (walk.h sorted_stream): verify runs mode 2 (every load
-    // unconditional within its path: 0.703 -> 0.723 against the session-start
-    // build, profiles/r04/final_ab/), the seal keeps the masked loads (mode
-    // 2: 0.667 -> 0.639, and with its trailer stores unconditional too 0.667
-    // -> 0.640, seal_exact/; mode 1, the tail and trailer re-read every step:
-    // seal 0.67 -> 0.61, verify 0.69 -> 0.64; mode2_ab/, exact_ab/)
-    static constexpr uint32_t kExact = SEAL ? (LVK_SEAL_CURWAIT ? 2u : 0u) : 2u;
-    static constexpr bool kCurWait = SEAL && LVK_SEAL_CURWAIT;  // (variant) walk.h sorted_stream
-    static constexpr uint32_t kTrailerLoads = SEAL ? 0u : 2u;   // loads trailer() issues per lane
+    // Wait-count mode (walk.h sorted_stream): both run mode 2, every load
+    // unconditional within its path (verify: 0.703 -> 0.723 in round 4,
+    // profiles/r04/final_ab/).  The seal also waits explicitly for the batch
+    // it folds (kCurWait): with mode 2 alone the compiler's merge over the
+    // loop's paths still waited vmcnt(0) in the head batches' fix-up, i.e. for
+    // the prefetch as well, and the seal ran slower than with masked loads
+    // (0.628 vs 0.669, profiles/r06/seal_exact/); with the explicit wait
+    // 0.683-0.688 against 0.665-0.669 (profiles/r06/seal_curwait/).  The
+    // verify walk's own counts are already exact.
+    static constexpr uint32_t kExact = 2u;
+    static constexpr bool kCurWait = SEAL || LVK_VERIFY_CURWAIT;  // walk.h sorted_stream: explicit wait for the folded batch
+    static constexpr uint32_t kTrailerLoads = SEAL ? 0u : 2u;  // loads trailer() issues per lane
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
         const uint64_t u = sst_unit(e);

@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round 6 (2nd): exact loads + an explicit wait for the folded batch in the
+# class kernel's walk (LVK_CLASS_CURWAIT=1: C2, C4, C3 via offsets, the WAL
+# scan) and in the SST verify walk (LVK_VERIFY_CURWAIT=1), each against the
+# product (the seal already ships it), interleaved; the GPU tests of the
+# offsets API, the WAL scan and the table on each variant first.
+set -o pipefail
+out=${1:-gpurun_out/r06ccw}
+mkdir -p "$out"
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$root"
+export TMPDIR=/tmp
+bash tools/build_variant.sh ccw -DLVK_CLASS_CURWAIT=1 > "$out/build.txt" 2>&1 || exit 1
+bash tools/build_variant.sh vcw -DLVK_VERIFY_CURWAIT=1 >> "$out/build.txt" 2>&1 || exit 1
+VD=$root/leveldb-rs_amd/lib/variants
+LVGPU_STRESS_TRIALS=300 LVGPU_WAL_STRESS_TRIALS=200 LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_ccw.so timeout -k 10 400 python3 -u -m pytest tests/test_gpu_batch.py tests/test_gpu_stress.py tests/test_gpu_wal.py tests/test_gpu_wal_stress.py -x -q -m gpu --timeout 120 --timeout-method thread > "$out/pytest_ccw.txt" 2>&1 || { tail -5 "$out/pytest_ccw.txt"; exit 1; }
+LVGPU_SST_STRESS_TRIALS=300 LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_vcw.so timeout -k 10 300 python3 -u -m pytest tests/test_table.py tests/test_gpu_table_stress.py -x -q --timeout 120 --timeout-method thread > "$out/pytest_vcw.txt" 2>&1 || { tail -5 "$out/pytest_vcw.txt"; exit 1; }
+tail -1 "$out/pytest_ccw.txt"; tail -1 "$out/pytest_vcw.txt"
+B="--cpu-seconds 0 --traffic off --c5-strong off"
+for r in 1 2; do
+  for v in prod ccw; do
+    if [ $v = prod ]; then E=""; else E="LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_ccw.so"; fi
+    env $E timeout -k 10 300 python3 bench.py --workload c2 --api offsets $B > "$out/c2_${v}_$r.json" 2>> "$out/err.txt" || exit 1
+    env $E timeout -k 10 300 python3 bench.py --workload c4 --api offsets $B > "$out/c4_${v}_$r.json" 2>> "$out/err.txt" || exit 1
+    env $E timeout -k 10 300 python3 bench.py --workload c3 --api offsets $B > "$out/c3o_${v}_$r.json" 2>> "$out/err.txt" || exit 1
+    env $E timeout -k 10 300 python3 bench.py --wal-device --cpu-seconds 0 --traffic off > "$out/wal_${v}_$r.json" 2>> "$out/err.txt" || exit 1
+  done
+  for v in prod vcw; do
+    if [ $v = prod ]; then E=""; else E="LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_vcw.so"; fi
+    env $E timeout -k 10 200 python3 bench.py --table --cpu-seconds 0 > "$out/table_${v}_$r.json" 2>> "$out/err.txt" || exit 1
+  done
+done
+python3 - "$out" <<'PY'
+import glob, json, os, sys
+out = sys.argv[1]
+for f in sorted(glob.glob(os.path.join(out, "*.json"))):
+    d = json.loads(open(f).read().splitlines()[-1])
+    if "seal" in d:
+        print(os.path.basename(f), "seal", d["seal"]["frac_of_8TBps"], "verify", d["verify"]["frac_of_8TBps"])
+    else:
+        print(os.path.basename(f), d["roofline"]["frac"])
+PY
