@@ -397,8 +397,11 @@ struct SortedList {
     static constexpr uint32_t kFlush = 16;  // 64 slots of one word pair
     static constexpr bool kAlMid = true;    // plain addresses in middle batches (load_rbatch_al)
     static constexpr bool kOneRound = false;  // sorted_stream's one-round path (FusedUnits)
-    static constexpr uint32_t kExact = LVK_CLASS_CURWAIT ? 2 : 0;  // sorted_stream: wait-count mode (below)
-    static constexpr bool kCurWait = LVK_CLASS_CURWAIT;  // sorted_stream: explicit wait for the batch it folds
+    static constexpr uint32_t kExact = 0;  // sorted_stream: wait-count mode (below)
+    // sorted_stream: explicit wait for the batch it folds (with kExact 2:
+    // C2 flat, C4 -0.4 %, C3 via offsets -2.5 %, the WAL scan flat,
+    // profiles/r06/curwait/; the seal keeps it)
+    static constexpr bool kCurWait = false;
     static constexpr uint32_t kTrailerLoads = 0;
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
@@ -452,9 +455,13 @@ struct SortedList {
 // mode2_ab/): class kernel mode 1 / 2 -- C3 via offsets -2.5 / -3 %, C2 0,
 // C4 -0.6 %, WAL scan +0.6 / -0.3 % -- so it keeps mode 0 (16 waves per CU
 // hide the exposed round trip); SST verify mode 2 +2.8 % (0.703 -> 0.723,
-// final_ab/), the seal -4 % (mode 0); the fused small-batch kernel +0.5-1.3
-// us (mode 0).  (Round 2 issued the same loads in every step by re-reading
-// the entries each batch as well: 4-5 % slower from extra loads and spills.)
+// final_ab/), the seal -4 % (it kept mode 0 until round 6, when mode 2 with
+// Src::kCurWait -- one explicit s_waitcnt for the folded batch after this
+// step's loads -- took it 0.665-0.669 -> 0.683-0.688: the compiler's own
+// merge had still waited vmcnt(0) in the head batches' fix-up, i.e. for the
+// prefetch too); the fused small-batch kernel +0.5-1.3 us (mode 0).
+// (Round 2 issued the same loads in every step by re-reading the entries
+// each batch as well: 4-5 % slower from extra loads and spills.)
 template <int G, class Src, class Next, uint32_t ALR = kAlRows>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {

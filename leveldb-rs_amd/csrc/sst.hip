@@ -71,9 +71,10 @@ struct TableUnits {
     // the prefetch as well, and the seal ran slower than with masked loads
     // (0.628 vs 0.669, profiles/r06/seal_exact/); with the explicit wait
     // 0.683-0.688 against 0.665-0.669 (profiles/r06/seal_curwait/).  The
-    // verify walk's own counts are already exact.
+    // verify walk's own counts are already exact (the explicit wait there
+    // measured flat, profiles/r06/curwait/).
     static constexpr uint32_t kExact = 2u;
-    static constexpr bool kCurWait = SEAL || LVK_VERIFY_CURWAIT;  // walk.h sorted_stream: explicit wait for the folded batch
+    static constexpr bool kCurWait = SEAL;  // walk.h sorted_stream: explicit wait for the folded batch
     static constexpr uint32_t kTrailerLoads = SEAL ? 0u : 2u;  // loads trailer() issues per lane
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {

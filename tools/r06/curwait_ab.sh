@@ -3,6 +3,7 @@
 # class kernel's walk (LVK_CLASS_CURWAIT=1: C2, C4, C3 via offsets, the WAL
 # scan) and in the SST verify walk (LVK_VERIFY_CURWAIT=1), each against the
 # product (the seal already ships it), interleaved; the GPU tests of the
+# (The class and verify knobs lived in commit dfa3b3a only.)
 # offsets API, the WAL scan and the table on each variant first.
 set -o pipefail
 out=${1:-gpurun_out/r06ccw}

@@ -2,6 +2,7 @@
 # Round 6 (2nd): the seal with exact loads and an explicit wait for the batch
 # it folds (LVK_SEAL_CURWAIT=1; the compiler waited vmcnt(0) in the head
 # batches' fix-up paths, i.e. also for the prefetch) against the product.
+# (Its knob became the product in the next commit; LVK_SEAL_CURWAIT no longer exists.)
 set -o pipefail
 out=${1:-gpurun_out/r06cw}
 mkdir -p "$out"
