@@ -552,7 +552,6 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     // the end of the step before it (exact loads, aligned rows only)
     constexpr bool PRE = AL && EX && (LVK_WALK_PREADDR != 0);
     uint64_t pa[NU];
-    uint64_t ta = 0;  // (PRE) the tail granule's address, for the round's last step
     // the step after step j loads batch j + 2 of this round, or the next
     // round's batch 0 when j + 2 == nbw (nbwn from qn, loaded a round ago)
     auto plan = [&](uint32_t jn) {  // jn: the step about to run
@@ -562,10 +561,6 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             } else {
                 nbwn = round_nbw_al<NU>(al_geo(qn));
                 rbatch_addrs_al<NU>(qn, nbwn, 0, gl, pa);
-                // every lane loads (the zero block but the tail's owner)
-                const bool on = gl == 0 && ((q.alow() + q.len) & 15u);
-                ta = on ? q.abase() + (static_cast<uint64_t>(q.ng()) << 4)
-                        : reinterpret_cast<uint64_t>(&g_zero_granules[gl & 15u]);
             }
         }
     };
@@ -618,7 +613,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         if constexpr (PRE) {
             load_addrs<NU>(pa, nxt);  // first: no address arithmetic before it
             if (lastj) {
-                tail = load16_rt(ta);
+                tail = load_rtail<EX>(q, gl);
                 tr = src.trailer(q, gl);
             }
         } else if (!lastj) {
