@@ -376,7 +376,6 @@ struct FusedUnits {
     static constexpr bool kAlMid = true;
     static constexpr bool kOneRound = true;  // sorted_stream: a one-round wave loads all batches at once
     static constexpr bool kCurWait = false;
-    static constexpr bool kLaunder = false;
     static constexpr uint32_t kTrailerLoads = 0;
     // wait-count modes 1 / 2 (walk.h) measured 0.7-1.3 / 0.5-0.9 us slower on
     // the few-long-buffer calls (profiles/r04/new_ab/, mode2_ab/): masked

@@ -23,10 +23,6 @@
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
     defined(LVK_SST_RUN) || \
-    defined(LVK_WALK_PREADDR) || \
-    defined(LVK_WALK_ENTRYWAIT) || \
-    defined(LVK_WALK_NOMERGE) || \
-    defined(LVK_WALK_LAUNDER) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_HASH_WGS_PER_CU) || \
@@ -64,18 +60,6 @@
 #endif
 #ifndef LVK_SST_RUN  // table walk: consecutive blocks per group (file-order runs; 1 = one block per round)
 #define LVK_SST_RUN 4
-#endif
-#ifndef LVK_WALK_LAUNDER  // (variant) walk.h launder_geo: bit 0 the table walk, bit 1 the class kernel's
-#define LVK_WALK_LAUNDER 0
-#endif
-#ifndef LVK_WALK_NOMERGE  // (variant) walk.h: keep the two unrolled steps apart
-#define LVK_WALK_NOMERGE 0
-#endif
-#ifndef LVK_WALK_ENTRYWAIT  // (variant) walk.h: the entry loads land before the loop
-#define LVK_WALK_ENTRYWAIT 0
-#endif
-#ifndef LVK_WALK_PREADDR  // (variant) walk.h: next batch addresses computed a step ahead (exact-load sources)
-#define LVK_WALK_PREADDR 0
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

@@ -2,8 +2,6 @@
 // and of file-ordered units (SST blocks): geometry, the 256-B-aligned row
 // batches, fix-ups, merge and the sorted_stream loop with its Src policies.
 #pragma once
-#include <type_traits>
-
 #include "sort.h"
 
 namespace lvk {
@@ -276,27 +274,6 @@ __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint
     }
 }
 
-// (variant LVK_WALK_PREADDR) The row addresses load_rbatch_al would load,
-// computed ahead, and the loads from them.
-template <uint32_t NU>
-__device__ __forceinline__ void rbatch_addrs_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
-                                                uint64_t (&ad)[NU]) {
-    const AGeo g = al_geo(q);
-    const uint64_t ab = q.abase();
-    const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
-#pragma unroll
-    for (uint32_t i = 0; i < NU; ++i) {
-        const int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
-        ad[i] = (d < 0 || d > dmax) ? reinterpret_cast<uint64_t>(&g_zero_granules[gl]) : ab + (static_cast<uint32_t>(d) << 4);
-    }
-}
-
-template <uint32_t NU>
-__device__ __forceinline__ void load_addrs(const uint64_t (&ad)[NU], uint4 (&v)[NU]) {
-#pragma unroll
-    for (uint32_t i = 0; i < NU; ++i) v[i] = load16(ad[i]);
-}
-
 // Head fix-up (as fix_rbatch); granules outside [0, dmax] were loaded from
 // the zero block.
 template <uint32_t NU>
@@ -404,16 +381,6 @@ __device__ __forceinline__ uint32_t finish_raw(const RGeo &q, uint32_t X, const 
     return X;
 }
 
-// A round's geometry, re-defined in place by an empty asm: the loads that
-// produced it (the entries, a round ago) are waited for here, once, and the
-// registers it leaves carry no pending load, so the next rounds' address
-// arithmetic never waits on them (LVK_WALK_LAUNDER, variant).
-__device__ __forceinline__ void launder_geo(RGeo &q) {
-    uint32_t lo = static_cast<uint32_t>(q.a), hi = static_cast<uint32_t>(q.a >> 32);
-    asm volatile("" : "+v"(lo), "+v"(hi), "+v"(q.len), "+v"(q.seed), "+v"(q.bid), "+v"(q.aux));
-    q.a = (static_cast<uint64_t>(hi) << 32) | lo;
-}
-
 // s_waitcnt immediate that waits for vmcnt <= n only (gfx9 encoding:
 // vmcnt bits 3:0 and 15:14, expcnt 6:4 and lgkmcnt 11:8 at their maxima).
 constexpr int vmcnt_only(uint32_t n) {
@@ -435,7 +402,6 @@ struct SortedList {
     // C2 flat, C4 -0.4 %, C3 via offsets -2.5 %, the WAL scan flat,
     // profiles/r06/curwait/; the seal keeps it)
     static constexpr bool kCurWait = false;
-    static constexpr bool kLaunder = LVK_WALK_LAUNDER & 2;  // (variant) launder_geo at each round
     static constexpr uint32_t kTrailerLoads = 0;
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
@@ -520,7 +486,6 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     uint64_t rhon = next();
 
     RGeo q = src.load(P, rho * K + grp);
-    if constexpr (Src::kLaunder) launder_geo(q);
     // (AL) some group of the round ends before lane 15.  The row geometry
     // (al_geo) is recomputed from q where it is used: fewer live registers.
     bool rot = AL && __any(al_geo(q).e != 15);
@@ -537,34 +502,10 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         load_rbatch_al<NU>(q, nbw, 0, gl, slot0);
     else
         load_rbatch<G>(q, nbw, 0, gl, slot0);
-#if LVK_WALK_ENTRYWAIT
-    // (variant) the entry loads (this round's and the next round's geometry)
-    // land before the loop: a register they wrote and the loop reuses is
-    // then not "pending" on the loop's entry edge, which made the compiler
-    // wait vmcnt(0) at the top of every step
-    if constexpr (EX) __builtin_amdgcn_s_waitcnt(vmcnt_only(AL ? NU : U));
-#endif
     uint32_t A[NU];
     uint32_t a3p = 0;  // (AL) the last row's accumulator before the last batch
     uint32_t c = 0;  // rounds finished (output staging slot)
     uint32_t j = 0;
-    // (variant) the addresses of the batch the next step loads, computed at
-    // the end of the step before it (exact loads, aligned rows only)
-    constexpr bool PRE = AL && EX && (LVK_WALK_PREADDR != 0);
-    uint64_t pa[NU];
-    // the step after step j loads batch j + 2 of this round, or the next
-    // round's batch 0 when j + 2 == nbw (nbwn from qn, loaded a round ago)
-    auto plan = [&](uint32_t jn) {  // jn: the step about to run
-        if constexpr (PRE) {
-            if (jn + 1u < nbw) {
-                rbatch_addrs_al<NU>(q, nbw, jn + 1u, gl, pa);
-            } else {
-                nbwn = round_nbw_al<NU>(al_geo(qn));
-                rbatch_addrs_al<NU>(qn, nbwn, 0, gl, pa);
-            }
-        }
-    };
-    plan(0);
     if constexpr (AL && Src::kOneRound && NU == 4) {
         // The wave's only round, <= 4 batches (a batch of <= 1,024 one-round
         // units: the pieces of a few long buffers): every batch's loads are
@@ -600,23 +541,10 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         }
     }
 
-    auto step = [&](auto parity, uint4(&cur)[NU], uint4(&nxt)[NU]) -> bool {
-#if LVK_WALK_NOMERGE
-        // (variant) the two unrolled steps must stay two: identical bodies
-        // were merged into one, with the slots copied through registers the
-        // next batch lands in -- a wait for it at every step's top
-        if constexpr (decltype(parity)::value) asm volatile("; walk step, slot 1");
-        else asm volatile("; walk step, slot 0");
-#endif
+    auto step = [&](uint4(&cur)[NU], uint4(&nxt)[NU]) -> bool {
         const bool lastj = j + 1 == nbw;
         const bool more = rhon < nr;
-        if constexpr (PRE) {
-            load_addrs<NU>(pa, nxt);  // first: no address arithmetic before it
-            if (lastj) {
-                tail = load_rtail<EX>(q, gl);
-                tr = src.trailer(q, gl);
-            }
-        } else if (!lastj) {
+        if (!lastj) {
             if constexpr (AL)
                 load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt, Src::kAlMid ? jfix : 0xffffffffu);
             else
@@ -659,7 +587,6 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             fold_batch<false, W4K, NU, W4OFF>(cur, A, L);
         if (!lastj) {
             ++j;
-            plan(j);
             return false;
         }
         uint32_t X;
@@ -680,7 +607,6 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         if (!more) return true;
         ++c;
         q = qn;
-        if constexpr (Src::kLaunder) launder_geo(q);
         nbw = nbwn;
         if constexpr (AL) {
             rot = __any(al_geo(q).e != 15);
@@ -692,12 +618,11 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         rhon = next();
         if (EX || rhon < nr) qn = src.load(P, rhon * K + grp);  // (src.load clamps)
         j = 0;
-        plan(0);
         return false;
     };
     for (;;) {
-        if (step(std::integral_constant<int, 0>{}, slot0, slot1)) break;
-        if (step(std::integral_constant<int, 1>{}, slot1, slot0)) break;
+        if (step(slot0, slot1)) break;
+        if (step(slot1, slot0)) break;
     }
 }
 

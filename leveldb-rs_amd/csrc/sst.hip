@@ -75,7 +75,6 @@ struct TableUnits {
     // measured flat, profiles/r06/curwait/).
     static constexpr uint32_t kExact = 2u;
     static constexpr bool kCurWait = SEAL;  // walk.h sorted_stream: explicit wait for the folded batch
-    static constexpr bool kLaunder = LVK_WALK_LAUNDER & 1;  // (variant) walk.h launder_geo
     static constexpr uint32_t kTrailerLoads = SEAL ? 0u : 2u;  // loads trailer() issues per lane
 
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
