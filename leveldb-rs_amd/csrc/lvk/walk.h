@@ -401,7 +401,7 @@ struct SortedList {
     // sorted_stream: explicit wait for the batch it folds (with kExact 2:
     // C2 flat, C4 -0.4 %, C3 via offsets -2.5 %, the WAL scan flat,
     // profiles/r06/curwait/; the seal keeps it)
-    static constexpr bool kCurWait = LVK_CLASS_WAIT0;  // (variant) with masked loads
+    static constexpr bool kCurWait = false;
     static constexpr uint32_t kTrailerLoads = 0;
     bool ident;  // the list is the identity (kWsIdent): entry e is buffer e of off/len/seed
     __device__ __forceinline__ RGeo load(const Params &P, uint64_t e) const {
@@ -570,8 +570,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             // over the loop's paths waited for the new batch too
             // (one immediate for both paths: on the last step it also waits
             // for the tail, as the verify walk's own counts do)
-            // (with masked loads the wait may also cover a tail load issued
-            // before the batch; the compiler's own counts keep every use safe)
+            static_assert(Src::kExact != 0, "the explicit wait needs exact load counts");
             __builtin_amdgcn_s_waitcnt(vmcnt_only(NU));
         }
         if constexpr (AL) {
