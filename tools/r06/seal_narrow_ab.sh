@@ -2,6 +2,7 @@
 # Round 6 (final): the seal flush with no load (LVK_SEAL_NARROW=1: the trailer
 # offset and type byte staged in LDS; the product re-reads the handle and type)
 # against the product.
+# (Measured flat, profiles/r06/seal_narrow/; the knob lived in 6564f5b and was reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06nw}
 mkdir -p "$out"
