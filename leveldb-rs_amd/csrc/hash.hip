@@ -71,13 +71,6 @@ constexpr uint32_t kM = 0xc6a4a793u;  // hash.rs:23
 constexpr uint32_t kFastDw = 17;      // dwords of the register fast path (keys <= 64 B + misalignment)
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-#if LVK_HASH_GLOBAL
-typedef const __attribute__((address_space(1))) uint32_t key_u32;  // global loads: vmcnt only
-typedef const __attribute__((address_space(1))) u32x4a4 key_u32x4;
-#else
-typedef const uint32_t key_u32;
-typedef const u32x4a4 key_u32x4;
-#endif
 
 __device__ __forceinline__ uint32_t mix(uint32_t h, uint32_t w) {  // hash.rs:31-35
     h += w;
@@ -237,13 +230,13 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
 #pragma unroll
             for (uint32_t j = 0; j < kFastDw; ++j) w[j] = sd[j];
         } else {
-            key_u32 *d = reinterpret_cast<key_u32 *>(reinterpret_cast<uintptr_t>(base + (o - bs)));
+            const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
             w[0] = d[0];
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
                 const uint32_t b = 4 * m + 1;
                 if (b + 3 < ndw) {
-                    const u32x4a4 v = *reinterpret_cast<key_u32x4 *>(d + b);
+                    const u32x4a4 v = *reinterpret_cast<const u32x4a4 *>(d + b);
                     w[b] = v.x;
                     w[b + 1] = v.y;
                     w[b + 2] = v.z;
@@ -270,7 +263,7 @@ __device__ __forceinline__ uint32_t hash_set(const uint8_t *__restrict__ base, u
                 t0 = sd[nw];
                 t1 = nw + 1 < ndw ? sd[nw + 1] : 0u;
             } else {
-                key_u32 *d = reinterpret_cast<key_u32 *>(reinterpret_cast<uintptr_t>(base + (o - bs)));
+                const uint32_t *d = reinterpret_cast<const uint32_t *>(base + (o - bs));
                 t0 = d[nw];
                 t1 = nw + 1 < ndw ? d[nw + 1] : 0u;
             }

@@ -251,8 +251,6 @@ __device__ __forceinline__ uint32_t fix_word(uint32_t w, int32_t rel, uint32_t s
 // load would count in both).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
-typedef const __attribute__((address_space(1))) uint32_t g_u32;
-typedef __attribute__((address_space(1))) uint8_t g_u8;
 
 __device__ __forceinline__ uint4 to_uint4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 

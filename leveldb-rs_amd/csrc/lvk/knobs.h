@@ -23,8 +23,6 @@
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
     defined(LVK_SST_RUN) || \
-    defined(LVK_HASH_GLOBAL) || \
-    defined(LVK_SST_GLOBAL) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_HASH_WGS_PER_CU) || \
@@ -62,12 +60,6 @@
 #endif
 #ifndef LVK_SST_RUN  // table walk: consecutive blocks per group (file-order runs; 1 = one block per round)
 #define LVK_SST_RUN 4
-#endif
-#ifndef LVK_SST_GLOBAL  // (variant) table walk: trailer loads / stores in the global address space, not flat
-#define LVK_SST_GLOBAL 0
-#endif
-#ifndef LVK_HASH_GLOBAL  // (variant) hash: key loads in the global address space, not flat
-#define LVK_HASH_GLOBAL 0
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

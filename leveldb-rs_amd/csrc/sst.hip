@@ -106,19 +106,14 @@ struct TableUnits {
         if constexpr (kExact != 0) {  // every lane loads two dwords (others: the zero block)
             const bool on = gl == 0 && (q.aux & 1u);
             const uint64_t end = q.a + q.len;
-#if LVK_SST_GLOBAL
-            const g_u32 *w = reinterpret_cast<const g_u32 *>(
-                on ? end & ~static_cast<uint64_t>(3) : reinterpret_cast<uint64_t>(&g_zero_granules[0]));
-#else
             const uint32_t *w = on ? reinterpret_cast<const uint32_t *>(end & ~static_cast<uint64_t>(3))
                                    : reinterpret_cast<const uint32_t *>(&g_zero_granules[0]);
-#endif
             const uint32_t w0 = w[0], w1 = w[(end & 3u) ? 1 : 0];  // (aligned: no dword past the stored crc)
             return on ? make_uint2(w0, (end & 3u) ? w1 : 0u) : make_uint2(0, 0);
         }
         if (gl != 0 || !(q.aux & 1u)) return make_uint2(0, 0);
         const uint64_t end = q.a + q.len;
-        const g_u32 *w = reinterpret_cast<const g_u32 *>(end & ~static_cast<uint64_t>(3));
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(end & ~static_cast<uint64_t>(3));
         return make_uint2(w[0], (end & 3u) ? w[1] : 0u);
     }
     __device__ __forceinline__ void stage(const Params &, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
@@ -148,11 +143,7 @@ struct TableUnits {
             if (bi == 0xffffffffu) return;
             const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
             const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
-#if LVK_SST_GLOBAL
-            g_u8 *p = reinterpret_cast<g_u8 *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
-#else
             uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
-#endif
             const uint32_t f = types ? types[bi] : 0u;
             const uint32_t m = g_ocrc[wave][lane];
             p[0] = static_cast<uint8_t>(f);

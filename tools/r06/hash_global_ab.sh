@@ -2,6 +2,7 @@
 # Round 6 (final): the hash kernel's direct key loads in the global address
 # space (LVK_HASH_GLOBAL=1) against the product, where the compiler merged the
 # tail-word loads of the staged (LDS) and direct paths into one flat load.
+# (Measured flat, profiles/r06/hash_global/; the knob lived in 3ec5f0f and was reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06hg}
 mkdir -p "$out"

@@ -2,6 +2,7 @@
 # Round 6 (final): the table walk with its trailer loads (verify) and stores
 # (seal) in the global address space (LVK_SST_GLOBAL=1) against the product,
 # whose flat ones count in lgkmcnt as well as vmcnt.
+# (Measured flat, profiles/r06/sst_global/; the knob lived in 3ec5f0f and was reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06gl}
 mkdir -p "$out"
