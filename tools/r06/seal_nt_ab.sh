@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6 (final): the seal with non-temporal trailer stores (LVK_SEAL_NT=1)
+# against the product, whose trailers sit dirty in L2 until the kernel ends.
+set -o pipefail
+out=${1:-gpurun_out/r06nt}
+mkdir -p "$out"
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$root"
+export TMPDIR=/tmp
+bash tools/build_variant.sh nt -DLVK_SEAL_NT=1 > "$out/build.txt" 2>&1 || exit 1
+VD=$root/leveldb-rs_amd/lib/variants
+LVGPU_SST_STRESS_TRIALS=400 LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_nt.so timeout -k 10 300 python3 -u -m pytest tests/test_table.py tests/test_gpu_table_stress.py -x -q --timeout 120 --timeout-method thread > "$out/pytest_nt.txt" 2>&1 || exit 1
+for r in 1 2 3; do
+  timeout -k 10 200 python3 bench.py --table --cpu-seconds 0 > "$out/prod_$r.json" 2>> "$out/err.txt" || exit 1
+  LVGPU_EXPERIMENT=1 LVGPU_LIB=$VD/liblvgpu_nt.so timeout -k 10 200 python3 bench.py --table --cpu-seconds 0 > "$out/nt_$r.json" 2>> "$out/err.txt" || exit 1
+done
+for f in "$out"/prod_*.json "$out"/nt_*.json; do python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().splitlines()[-1]);print(sys.argv[1], d['seal']['frac_of_8TBps'], d['verify']['frac_of_8TBps'])" "$f"; done
