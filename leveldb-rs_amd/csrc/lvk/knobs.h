@@ -23,10 +23,6 @@
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
     defined(LVK_SST_RUN) || \
-    defined(LVK_SEAL_NT) || \
-    defined(LVK_SEAL_NARROW) || \
-    defined(LVK_SEAL_SECTOR) || \
-    defined(LVK_SEAL_NOSTORE) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_HASH_WGS_PER_CU) || \
@@ -64,18 +60,6 @@
 #endif
 #ifndef LVK_SST_RUN  // table walk: consecutive blocks per group (file-order runs; 1 = one block per round)
 #define LVK_SST_RUN 4
-#endif
-#ifndef LVK_SEAL_NT  // (variant) seal: non-temporal trailer stores
-#define LVK_SEAL_NT 0
-#endif
-#ifndef LVK_SEAL_NOSTORE  // (timing study) seal: skip the trailer stores
-#define LVK_SEAL_NOSTORE 0
-#endif
-#ifndef LVK_SEAL_SECTOR  // (timing study) seal: write whole 32/64-B sectors around each trailer
-#define LVK_SEAL_SECTOR 0
-#endif
-#ifndef LVK_SEAL_NARROW  // (variant) seal: trailer offsets and types staged in LDS, a flush with no load
-#define LVK_SEAL_NARROW 0
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

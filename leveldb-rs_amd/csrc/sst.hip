@@ -48,13 +48,6 @@ __device__ __forceinline__ uint64_t sst_unit(uint64_t e) {  // e = rho * 4 + gro
     return (rho / kSstRun) * (4u * kSstRun) + g * kSstRun + rho % kSstRun;
 }
 
-// The seal's per-slot type bytes (16 waves x 64 slots), in combine table 4
-// (Shift_256), which the G = 16 table walk never reads.
-__device__ __forceinline__ uint8_t *seal_type_bytes() {
-    return reinterpret_cast<uint8_t *>(&g_lds[(kComb + 4 * 4096) / 4]);
-}
-static_assert(kWaves * 64 <= 4096, "type bytes inside combine table 4");
-
 template <bool SEAL, bool CRCOUT = false>
 struct TableUnits {
     const uint2 *handles;  // {offset, size} u64 pairs per block
@@ -63,10 +56,6 @@ struct TableUnits {
     uint32_t *crc_out;     // verify: optional crc32c(contents || type)
     uint64_t file_bytes;
     uint64_t nblocks;      // the blocks (P.n: the run-padded entry count)
-    // seal: every trailer offset fits 32 bits (file <= 4 GiB - 6): the slot
-    // keeps the trailer's offset and the type byte sits in LDS, so the flush
-    // writes with no load (otherwise it re-reads the handle and the type)
-    uint32_t narrow = 0;
     // seal: 64 slots of {block, masked crc} (16 rounds of 4 blocks per flush;
     // the trailer stores are partial-line writes, and fewer, larger bursts of
     // them measured faster); verify: 64 slots of {block, status}, or with
@@ -127,19 +116,13 @@ struct TableUnits {
         const uint32_t *w = reinterpret_cast<const uint32_t *>(end & ~static_cast<uint64_t>(3));
         return make_uint2(w[0], (end & 3u) ? w[1] : 0u);
     }
-    __device__ __forceinline__ void stage(const Params &P, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
+    __device__ __forceinline__ void stage(const Params &, uint32_t wave, uint32_t slot, const RGeo &q, uint32_t X,
                                           uint2 tr) const {
         const bool ok = q.aux & 1u;
         if constexpr (SEAL) {
             const uint32_t t = (q.aux >> 8) & 0xffu;
             const uint32_t crc = ~byte_step(X, t);
-            if (narrow) {
-                // (run padding: bid is ~0 and the clamped block is written by its own entry)
-                g_oidx[wave][slot] = ok && q.bid != 0xffffffffu ? static_cast<uint32_t>(q.a + q.len - P.base) : 0xffffffffu;
-                seal_type_bytes()[wave * 64u + slot] = static_cast<uint8_t>(t);
-            } else {
-                g_oidx[wave][slot] = ok ? q.bid : 0xffffffffu;  // the flush re-reads the handle and type
-            }
+            g_oidx[wave][slot] = ok ? q.bid : 0xffffffffu;  // the flush re-reads the handle and type
             g_ocrc[wave][slot] = mask_crc(crc);
         } else {
             const uint32_t crc = ~X;
@@ -158,85 +141,8 @@ struct TableUnits {
             if (lane >= nslots) return;
             const uint32_t bi = g_oidx[wave][lane];
             if (bi == 0xffffffffu) return;
-            if (narrow) {  // bi is the trailer's offset
-                const uint32_t f = seal_type_bytes()[wave * 64u + lane];
-                const uint32_t m = g_ocrc[wave][lane];
-#if LVK_SEAL_NT
-                typedef __attribute__((address_space(1))) uint8_t g_u8;
-                typedef __attribute__((address_space(1))) uint32_t g_u32u __attribute__((aligned(1)));
-                g_u8 *p = reinterpret_cast<g_u8 *>(P.base + bi);
-                __builtin_nontemporal_store(static_cast<uint8_t>(f), p);
-                __builtin_nontemporal_store(m, reinterpret_cast<g_u32u *>(p + 1));
-#else
-                typedef __attribute__((address_space(1))) uint8_t g_u8;
-                g_u8 *p = reinterpret_cast<g_u8 *>(P.base + bi);
-                p[0] = static_cast<uint8_t>(f);
-                p[1] = static_cast<uint8_t>(m);
-                p[2] = static_cast<uint8_t>(m >> 8);
-                p[3] = static_cast<uint8_t>(m >> 16);
-                p[4] = static_cast<uint8_t>(m >> 24);
-#endif
-                return;
-            }
             const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
             const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
-#if LVK_SEAL_NOSTORE  // timing study only: no trailer is written (wrong output by design)
-            if (sz != ~0ull) return;
-#endif
-#if LVK_SEAL_SECTOR
-            {  // timing study: whole aligned sectors around the trailer, re-read and written back
-               // (assumes no other trailer shares them, as in bench.py's table; not a general path)
-                constexpr uint32_t S = LVK_SEAL_SECTOR;  // 32 or 64
-                const uint64_t a = P.base + o + sz;
-                const uint64_t s0 = a & ~static_cast<uint64_t>(S - 1);
-                const bool two = ((a + 4) & ~static_cast<uint64_t>(S - 1)) != s0;
-                const uint64_t v40 = static_cast<uint64_t>(types ? types[bi] : 0u) |
-                                     (static_cast<uint64_t>(g_ocrc[wave][lane]) << 8);
-                const int32_t r = static_cast<int32_t>(a - s0);
-                constexpr uint32_t NQ = S / 16;  // 16-B quads per sector
-                uint4 q[2 * NQ];
-#pragma unroll
-                for (uint32_t k = 0; k < NQ; ++k) q[k] = load16_rt(s0 + 16 * k);
-#pragma unroll
-                for (uint32_t k = 0; k < NQ; ++k) q[NQ + k] = two ? load16_rt(s0 + S + 16 * k) : make_uint4(0, 0, 0, 0);
-                auto patch = [&](uint32_t w, int32_t j) {  // word j of the (one or two) sectors
-                    uint32_t keep = 0xffffffffu, val = 0;
-#pragma unroll
-                    for (int32_t b = 0; b < 4; ++b) {
-                        const int32_t t = 4 * j + b - r;
-                        if (t >= 0 && t < 5) {
-                            keep &= ~(0xffu << (8 * b));
-                            val |= static_cast<uint32_t>((v40 >> (8 * t)) & 0xffu) << (8 * b);
-                        }
-                    }
-                    return (w & keep) | val;
-                };
-#pragma unroll
-                for (uint32_t k = 0; k < 2 * NQ; ++k) {
-                    q[k].x = patch(q[k].x, 4 * k);
-                    q[k].y = patch(q[k].y, 4 * k + 1);
-                    q[k].z = patch(q[k].z, 4 * k + 2);
-                    q[k].w = patch(q[k].w, 4 * k + 3);
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < NQ; ++k) *reinterpret_cast<uint4 *>(s0 + 16 * k) = q[k];
-                if (two) {
-#pragma unroll
-                    for (uint32_t k = 0; k < NQ; ++k) *reinterpret_cast<uint4 *>(s0 + S + 16 * k) = q[NQ + k];
-                }
-                return;
-            }
-#endif
-#if LVK_SEAL_NT
-            // non-temporal: the trailers stream out instead of sitting dirty in L2 until the kernel's end
-            typedef __attribute__((address_space(1))) uint8_t g_u8;
-            g_u8 *p = reinterpret_cast<g_u8 *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
-            const uint32_t f = types ? types[bi] : 0u;
-            const uint32_t m = g_ocrc[wave][lane];
-            __builtin_nontemporal_store(static_cast<uint8_t>(f), p);
-            typedef __attribute__((address_space(1))) uint32_t g_u32u __attribute__((aligned(1)));
-            __builtin_nontemporal_store(m, reinterpret_cast<g_u32u *>(p + 1));  // (byte-aligned dword store)
-#else
             uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
             const uint32_t f = types ? types[bi] : 0u;
             const uint32_t m = g_ocrc[wave][lane];
@@ -245,7 +151,6 @@ struct TableUnits {
             p[2] = static_cast<uint8_t>(m >> 8);
             p[3] = static_cast<uint8_t>(m >> 16);
             p[4] = static_cast<uint8_t>(m >> 24);
-#endif
         } else if constexpr (!CRCOUT) {
             if (lane >= nslots) return;
             const uint32_t bi = g_oidx[wave][lane];
@@ -310,8 +215,7 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, claims))), block(lvk::kThreads);
     if (seal) {
-        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes, n,
-                                LVK_SEAL_NARROW && file_bytes <= 0xfffffffaull ? 1u : 0u};
+        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes, n};
         g_kernel = "sst_blocks_kernel<seal>";
         // (4 rows per batch: Shift_1024 is the G = 16 image's own row shift)
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P,

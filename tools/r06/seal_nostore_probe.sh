@@ -3,6 +3,7 @@
 # (LVK_SEAL_NOSTORE=1, wrong output by design; bench.py skips parity for
 # experiment variants) against the product -- what any change to how the
 # trailers are written could gain at most.
+# (Results in profiles/r06/seal_nostore/; the knobs lived in 02e8055 and were reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06ns}
 mkdir -p "$out"

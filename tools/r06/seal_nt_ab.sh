@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 6 (final): the seal with non-temporal trailer stores (LVK_SEAL_NT=1)
 # against the product, whose trailers sit dirty in L2 until the kernel ends.
+# (Results in profiles/r06/seal_nt/; the knobs lived in 02e8055 and were reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06nt}
 mkdir -p "$out"

@@ -3,6 +3,7 @@
 # around each trailer (LVK_SEAL_SECTOR=32/64: re-read, patched, written back;
 # valid only when no two trailers share a sector, as in bench.py's table)
 # against the product's 5-B partial writes.
+# (Results in profiles/r06/seal_sector/; the knobs lived in 02e8055 and were reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06sec}
 mkdir -p "$out"

@@ -4,6 +4,7 @@
 # load-free flush (LVK_SEAL_NARROW=1), and with or without non-temporal
 # stores (LVK_SEAL_NT=1), against the product.  The no-store timing study
 # (seal_nostore_probe.sh) put the trailer stores at ~10 us of ~200.
+# (Results in profiles/r06/seal_spread/; the knobs lived in 02e8055 and were reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06sp}
 mkdir -p "$out"
