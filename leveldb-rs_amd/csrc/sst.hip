@@ -141,11 +141,6 @@ struct TableUnits {
             if (lane >= nslots) return;
             const uint32_t bi = g_oidx[wave][lane];
             if (bi == 0xffffffffu) return;
-#if LVK_SEAL_SPLIT
-            // the masked CRCs by block index; seal_trailers_kernel writes the trailers
-            crc_out[bi] = g_ocrc[wave][lane];
-            return;
-#endif
             const uint2 ho = handles[2 * bi], hs = handles[2 * bi + 1];
             const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
             uint8_t *p = reinterpret_cast<uint8_t *>(P.base + o + sz);  // type byte, then LE32(mask(crc))
@@ -202,30 +197,6 @@ __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const ui
                                                                                           next);
 }
 
-#if LVK_SEAL_SPLIT
-// The seal's second launch: every block's trailer from the CRCs the walk
-// stored by block index (scattered 5-B stores from a grid with no loads
-// of its own in flight behind them).
-__global__ __launch_bounds__(256) void seal_trailers_kernel(uint64_t base, const uint2 *__restrict__ handles,
-                                                            const uint8_t *__restrict__ types,
-                                                            const uint32_t *__restrict__ crcs, uint64_t n,
-                                                            uint64_t file_bytes) {
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
-        const uint2 ho = handles[2 * i], hs = handles[2 * i + 1];
-        const uint64_t o = (static_cast<uint64_t>(ho.y) << 32) | ho.x, sz = (static_cast<uint64_t>(hs.y) << 32) | hs.x;
-        if (!sst_in_range(o, sz, file_bytes)) continue;
-        const uint32_t f = types ? types[i] : 0u;
-        const uint32_t m = crcs[i];
-        uint8_t *p = reinterpret_cast<uint8_t *>(base + o + sz);
-        p[0] = static_cast<uint8_t>(f);
-        p[1] = static_cast<uint8_t>(m);
-        p[2] = static_cast<uint8_t>(m >> 8);
-        p[3] = static_cast<uint8_t>(m >> 16);
-        p[4] = static_cast<uint8_t>(m >> 24);
-    }
-}
-#endif
-
 }  // namespace lvk
 
 namespace lvgpu_internal {
@@ -244,26 +215,11 @@ int launch_sst_blocks(bool seal, const uint8_t *d_file, uint64_t file_bytes, con
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(c->cus, claims))), block(lvk::kThreads);
     if (seal) {
-#if LVK_SEAL_SPLIT
-        uint8_t *ws = nullptr;
-        std::unique_lock<std::mutex> lk;
-        if (int rc = stream_ws_bytes(*c, s, n * 4, &ws, &lk)) return rc;
-        uint32_t *crcs = reinterpret_cast<uint32_t *>(ws);
-        lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, crcs, file_bytes, n};
-        g_kernel = "sst_blocks_kernel<seal>";
-        hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P,
-                           c->image[lvk::kSealRows == 4 ? 2 : kTableImage], u);
-        if (int rc = check_launch()) return rc;
-        const uint32_t tg = static_cast<uint32_t>(std::min<uint64_t>((n + 255) / 256, 65536));
-        hipLaunchKernelGGL(lvk::seal_trailers_kernel, dim3(tg), dim3(256), 0, s, P.base,
-                           reinterpret_cast<const uint2 *>(d_handles), d_types, crcs, static_cast<uint64_t>(n), file_bytes);
-#else
         lvk::TableUnits<true> u{reinterpret_cast<const uint2 *>(d_handles), d_types, nullptr, nullptr, file_bytes, n};
         g_kernel = "sst_blocks_kernel<seal>";
         // (4 rows per batch: Shift_1024 is the G = 16 image's own row shift)
         hipLaunchKernelGGL((lvk::sst_blocks_kernel<true, false>), grid, block, 0, s, P,
                            c->image[lvk::kSealRows == 4 ? 2 : kTableImage], u);
-#endif
     } else if (d_crc) {
         lvk::TableUnits<false, true> u{reinterpret_cast<const uint2 *>(d_handles), nullptr, d_status, d_crc, file_bytes,
                                         n};

@@ -3,6 +3,7 @@
 # stores each masked CRC by block index, as verify stores its status words,
 # and seal_trailers_kernel writes the trailers -- against the product, whose
 # walking waves write them at their end (~10 us of ~200, seal_nostore/).
+# (Results in profiles/r06/seal_split/; the knob lived in 34e25c4 and was reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06split}
 mkdir -p "$out"
