@@ -252,7 +252,7 @@ __device__ __forceinline__ uint32_t round_jfix_al(const RGeo &q, uint32_t nbw) {
 // end), so those batches take plain addresses, no range selects (C2 / C4 /
 // WAL +0.3-1 %; the table walk, 6 batches of 3 rows per unit, measured
 // -0.7 % and passes no jfix: Src::kAlMid, profiles/r03/walk/ab_al_mid.txt).
-template <uint32_t NU, bool RT = false>
+template <uint32_t NU>
 __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint32_t j, uint32_t gl,
                                                uint4 (&v)[NU], uint32_t jfix = 0xffffffffu) {
     const AGeo g = al_geo(q);
@@ -261,7 +261,7 @@ __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint
         const uint64_t a0 = ab + (static_cast<uint64_t>(static_cast<uint32_t>(
                                       16 * al_row<NU>(g, nbw, j, 0) + static_cast<int32_t>(gl) - g.ph)) << 4);
 #pragma unroll
-        for (uint32_t i = 0; i < NU; ++i) v[i] = RT ? load16_rt(a0 + 256u * i) : load16(a0 + 256u * i);
+        for (uint32_t i = 0; i < NU; ++i) v[i] = load16(a0 + 256u * i);
         return;
     }
     const int32_t dmax = static_cast<int32_t>(q.ng()) - 1;
@@ -270,7 +270,7 @@ __device__ __forceinline__ void load_rbatch_al(const RGeo &q, uint32_t nbw, uint
         const int32_t d = 16 * al_row<NU>(g, nbw, j, i) + static_cast<int32_t>(gl) - g.ph;
         const uint64_t ad = (d < 0 || d > dmax) ? reinterpret_cast<uint64_t>(&g_zero_granules[gl])
                                                 : ab + (static_cast<uint32_t>(d) << 4);
-        v[i] = RT ? load16_rt(ad) : load16(ad);
+        v[i] = load16(ad);
     }
 }
 
@@ -466,9 +466,6 @@ template <int G, class Src, class Next, uint32_t ALR = kAlRows>
 __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, uint32_t lane, const Lut &L,
                                               uint64_t rho, Next next) {
     constexpr bool AL = G == 16;  // 256-B-aligned rows (merge_al)
-    // (variant) first and last batches of a round load with the default
-    // policy: their lines are shared with the neighbouring buffers
-    constexpr bool kEdgeRt = LVK_EDGE_RT != 0;
     // exact wait counts (below): Src::kExact 0 = masked loads, 2 =
     // unconditional loads within each path
     static_assert(Src::kExact == 0 || Src::kExact == 2, "wait-count mode 0 or 2");
@@ -502,7 +499,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
     uint2 tr;
     uint4 slot0[NU], slot1[NU];
     if constexpr (AL)
-        load_rbatch_al<NU, kEdgeRt>(q, nbw, 0, gl, slot0);
+        load_rbatch_al<NU>(q, nbw, 0, gl, slot0);
     else
         load_rbatch<G>(q, nbw, 0, gl, slot0);
     uint32_t A[NU];
@@ -549,10 +546,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
         const bool more = rhon < nr;
         if (!lastj) {
             if constexpr (AL)
-                if (kEdgeRt && j + 2u == nbw)  // the round's last batch (wave-uniform)
-                    load_rbatch_al<NU, true>(q, nbw, j + 1, gl, nxt, Src::kAlMid ? jfix : 0xffffffffu);
-                else
-                    load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt, Src::kAlMid ? jfix : 0xffffffffu);
+                load_rbatch_al<NU>(q, nbw, j + 1, gl, nxt, Src::kAlMid ? jfix : 0xffffffffu);
             else
                 load_rbatch<G>(q, nbw, j + 1, gl, nxt);
         } else {
@@ -561,7 +555,7 @@ __device__ __forceinline__ void sorted_stream(const Params &P, const Src &src, u
             if (EX || more) {  // (exact: past the list, qn is the clamped last entry)
                 if constexpr (AL) {
                     nbwn = round_nbw_al<NU>(al_geo(qn));
-                    load_rbatch_al<NU, kEdgeRt>(qn, nbwn, 0, gl, nxt);
+                    load_rbatch_al<NU>(qn, nbwn, 0, gl, nxt);
                 } else {
                     nbwn = round_nbw<G>(qn);
                     load_rbatch<G>(qn, nbwn, 0, gl, nxt);

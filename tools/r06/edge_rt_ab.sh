@@ -4,6 +4,7 @@
 # batch with the default (L2-allocating) policy instead of non-temporal
 # (LVK_EDGE_RT=1), so a 128-B line shared by two neighbouring buffers is
 # fetched once, against the product.
+# (Results in profiles/r06/edge_rt/; the knob lived in 3f58364 and was reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06edge}
 mkdir -p "$out"
