@@ -23,7 +23,6 @@
     defined(LVK_SST_ROWS) || \
     defined(LVK_SEAL_ROWS) || \
     defined(LVK_SST_RUN) || \
-    defined(LVK_SST_PREFETCH) || \
     defined(LVK_SORT_MIN_WGS) || \
     defined(LVK_SMALL_ROUNDS) || \
     defined(LVK_HASH_WGS_PER_CU) || \
@@ -61,9 +60,6 @@
 #endif
 #ifndef LVK_SST_RUN  // table walk: consecutive blocks per group (file-order runs; 1 = one block per round)
 #define LVK_SST_RUN 4
-#endif
-#ifndef LVK_SST_PREFETCH  // (variant) table walk: first batches requested while the tables are staged
-#define LVK_SST_PREFETCH 0
 #endif
 #ifndef LVK_SORT_MIN_WGS
 #define LVK_SORT_MIN_WGS 1024

@@ -172,48 +172,9 @@ struct TableUnits {
 template <bool SEAL, bool CRCOUT>
 __global__ __launch_bounds__(kThreads) void sst_blocks_kernel(Params P, const uint4 *__restrict__ image,
                                                               TableUnits<SEAL, CRCOUT> src) {
-#if LVK_SST_PREFETCH
-    // The first round's blocks are requested while the table image is
-    // staged: wave w touches the first batch of the workgroup's w-th first
-    // claim (whichever wave takes that claim then reads it from L2).
-    uint32_t tx = 0;
-    {
-        constexpr uint32_t NU = SEAL ? kSealRows : kSstRows;
-        const uint32_t ln = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-        const uint64_t rr = (blockIdx.x + gridDim.x * static_cast<uint64_t>(wv)) * kSstRun;
-        const RGeo q0 = src.load(P, rr * 4u + ln / 16u);  // (clamped)
-        constexpr int kVec = kImageWords / 4;
-        constexpr int kPer = (kVec + kThreads - 1) / kThreads;
-        uint4 *l4 = reinterpret_cast<uint4 *>(g_lds);
-        g_u32x4 *img = reinterpret_cast<g_u32x4 *>(reinterpret_cast<uint64_t>(image));
-        u32x4 r[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int i = threadIdx.x + k * kThreads;
-            if (i < kVec) r[k] = img[i];
-        }
-        const uint64_t a0 = q0.a & ~static_cast<uint64_t>(255), e0 = q0.a + q0.len;
-#pragma unroll
-        for (uint32_t i = 0; i < NU; ++i) {  // every lane loads (past the block: its first granule)
-            typedef const __attribute__((address_space(1))) uint32_t g_u32;
-            const uint64_t ad = a0 + 256u * i + 16u * (ln & 15u);
-            tx ^= *reinterpret_cast<g_u32 *>(ad < e0 ? ad : (q0.a & ~static_cast<uint64_t>(15)));
-        }
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int i = threadIdx.x + k * kThreads;
-            if (i < kVec) l4[i] = to_uint4(r[k]);
-        }
-        __syncthreads();
-    }
-#else
     stage_tables(image);
-#endif
     if (threadIdx.x == 0) g_lds[kPoolWord] = 0;
     __syncthreads();
-#if LVK_SST_PREFETCH
-    asm volatile("" ::"v"(tx));  // the touches are kept
-#endif
     const uint32_t lane = threadIdx.x & 63u;
     const Lut L = make_lut(lane);
     const uint64_t grid = gridDim.x;

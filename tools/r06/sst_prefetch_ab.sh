@@ -2,6 +2,7 @@
 # Round 6 (final): the table walk requesting its first batches while the
 # table image is staged (LVK_SST_PREFETCH=1; wave w touches the first batch of
 # its workgroup's w-th first claim) against the product.
+# (Results in profiles/r06/sst_prefetch/; the knob lived in 3a6d0fc and was reverted.)
 set -o pipefail
 out=${1:-gpurun_out/r06pf}
 mkdir -p "$out"
