@@ -23,3 +23,20 @@ def test_integration_binds_every_declared_entry_point():
     assert not missing, missing
     stale = sorted(bound - _declared())
     assert not stale, stale
+
+
+def test_design_evidence_paths_exist():
+    """Every evidence directory DESIGN.md, README.md and HISTORY.md cite exists: full
+    `profiles/rNN/<dir>/` paths, and the bare `<dir>/` names the round
+    tables use for a directory under some round's profiles (or one level
+    below, e.g. final/recovery5/)."""
+    text = "".join(open(os.path.join(ROOT, f)).read() for f in ("DESIGN.md", "README.md", "HISTORY.md"))
+    full = set(re.findall(r"profiles/(r\d\d)/([A-Za-z0-9_]+)/", text))
+    missing = sorted(f"profiles/{r}/{d}/" for r, d in full if not os.path.isdir(os.path.join(ROOT, "profiles", r, d)))
+    assert not missing, missing
+    dirs = {os.path.basename(p.rstrip("/")) for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "*", ""))}
+    dirs |= {os.path.basename(p.rstrip("/")) for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "*", "*", ""))}
+    top = {"oracle", "profiles", "tests", "tools", "include", "leveldb-rs_amd"}
+    bare = set(re.findall(r"`([a-z0-9_]+)/`", text)) - top
+    unresolved = sorted(bare - dirs)
+    assert not unresolved, unresolved
